@@ -1,0 +1,212 @@
+#!/usr/bin/env python
+"""Training-throughput benchmark of buck-gnn's GraphSAGE hot path on MI355X.
+
+Metric (BASELINE.json): graphs/sec of a full train step (fwd + bwd + Adam) of the
+6-layer, hidden-512 GraphSage_addAggr BuckGNN on batches of 16 synthetic FE meshes
+per GPU (configs[1] = cfg2: 16 non-stiffened 71x71 quad+diagonal meshes with 13.33 %
+random virtual edges; N = 80,656 nodes, E = 715,872 directed edges per GPU).
+
+One step = the reference's inner-loop body (TRAIN_FINAL.py:253-298): graph structure
+built from edge_index (CSR + plans; rebuilt every step, as a new batch would need),
+forward, RelativeErrorLoss on denormalised eigenvalues, backward, gradient all-reduce
+(N > 1), Adam. Inputs (x, edge_index, batch, y) are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
+
+Rank 0 prints ONE JSON line. `roofline` is for the fused aggregation kernel
+(bgnn_sage_fwd: neighbour sum + lin_r term + bias + L2 normalize + BN statistics),
+HBM-bound; `roofline_mfma` for the forward GEMM. Both use HIP events recorded on the
+launching stream around each launch inside the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3"])
+    ap.add_argument("--model", default="GraphSage_addAggr")
+    ap.add_argument("--gemm", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, model_state, model_name, steps):
+    """The oracle (plain-PyTorch CPU restatement of the reference path) timed on the host cores."""
+    import torch
+    from oracle.buckgnn_ref import TrainStep
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    st = TrainStep(model_state, model_name, lr=1e-2, weight_decay=1e-8, dropout=0.1)
+    x, ei, b, y = batch.x.cpu(), batch.edge_index.cpu(), batch.batch.cpu(), batch.y.cpu()
+    st(x, ei, b, y)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st(x, ei, b, y)
+    dt = time.perf_counter() - t0
+    g = batch.num_graphs * steps
+    return {"value": round(g / dt, 4), "unit": "graphs/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} timed train steps (fwd+bwd+Adam, dropout 0.1) of the oracle on the same "
+                      f"{batch.num_graphs}-graph batch ({batch.num_nodes} nodes) after 1 warm-up, "
+                      f"torch CPU with {threads} threads; {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import bgnn
+    from bgnn import fused, synthetic
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    fused.GEMM_BACKEND = args.gemm
+
+    # data: each rank owns its own 16 graphs (seeds 1000*rank + g); resident in HBM
+    batch_cpu = synthetic.make_config_batch(args.config, rank=rank)
+    batch = batch_cpu.to(dev)
+    torch.manual_seed(0)
+    model = bgnn.BuckGNN(synthetic.NUM_NODE_FEATURES, synthetic.NUM_EDGE_FEATURES, hidden_channels=512,
+                         num_layers=6, pooling_layer="mean", prediction_type="buckling", dropout_rate=0.1,
+                         model_name=args.model)
+    state0 = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).train()
+    try:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8)
+    crit = bgnn.RelativeErrorLoss()
+    norm = bgnn.EigenvalueScaler(center=1.0, scale=0.5)
+    ar = bgnn.GradAllReduce(model) if world > 1 else None
+
+    def step():
+        if not args.cache_graph:
+            bgnn.clear_caches()
+        return bgnn.train_step(model, batch, opt, crit, norm, allreduce=ar)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    fused.TIMERS = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timers, fused.TIMERS = fused.TIMERS, None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_v = float(loss.item())
+
+    def avg_ms(name):
+        ev = timers.get(name, [])
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev) if ev else float("nan")
+
+    N, E, H = batch.num_nodes, batch.num_edges, 512
+    agg_ms = avg_ms("sage_fwd")
+    agg_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
+    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_sage_fwd.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+    gemm_ms = avg_ms("gemm_fwd")
+    gemm_flop = 2.0 * N * (2 * H) * H
+    gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
+    graphs = 16 * world * args.steps
+    out = {
+        "metric": METRIC,
+        "value": round(graphs / elapsed, 3),
+        "unit": "graphs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.config}: 16 synthetic 71x71 quad+diagonal FE meshes per GPU"
+                        + (" + super node" if args.config == "cfg3" else " + 13.33% random virtual edges")
+                        + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam; CSR rebuilt every step"
+                        if not args.cache_graph else f"{args.config} (CSR cached across steps)",
+            "global_batch": 16 * world,
+            "nodes_per_gpu": N,
+            "edges_per_gpu": E,
+            "hidden": H,
+            "layers": 6,
+            "parallelism": f"dp{world}",
+            "gemm": args.gemm,
+        },
+        "roofline": {
+            "kernel": "bgnn_sage_fwd (k_seg_light<4,2,64,SUM,SAGE> [+chunk/combine for super nodes])",
+            "bound": "hbm",
+            "achieved": round(agg_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(agg_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes": agg_bytes,
+            "avg_launch_ms": round(agg_ms, 5),
+            "launches": len(timers.get("sage_fwd", [])),
+        },
+        "roofline_mfma": {
+            "kernel": "bgnn_gemm_f32 forward z = x [W_l;W_r]^T" if args.gemm == "hip" else "torch.mm",
+            "bound": "mfma",
+            "achieved": round(gemm_tfs, 2),
+            "peak": FP32_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s",
+            "frac": round(gemm_tfs / FP32_MFMA_PEAK_TFS, 4),
+            "avg_launch_ms": round(gemm_ms, 5),
+        },
+        "spmm_bwd_avg_ms": round(avg_ms("spmm_bwd"), 5),
+        "final_loss": loss_v,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(batch_cpu, state0, args.model, args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

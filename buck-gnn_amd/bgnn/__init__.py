@@ -1,0 +1,28 @@
+"""bgnn — MI355X-native (gfx950) GraphSAGE message-passing hot path of buck-gnn.
+
+Host side (this package) mirrors the PyG / torch_scatter call surface the
+reference uses; all arithmetic runs in libbgnn.so (HIP kernels, C-ABI in
+include/bgnn.h). Importing the package does not touch the GPU.
+"""
+from . import _lib
+from .buckgnn import BuckGNN, GraphNetBlock, MLPPooling
+from .data import Batch, Data, DataLoader
+from .graph import Graph, SegmentIndex, clear_caches, graph_for, segments_for
+from .nn import (SAGEConv, global_add_pool, global_max_pool, global_mean_pool, scatter_add, scatter_mean,
+                 scatter_sum)
+from .ops import aggregate, segment_reduce
+from .pyg_shim import install_pyg_shim, uninstall_pyg_shim
+from .train import EigenvalueScaler, GradAllReduce, RelativeErrorLoss, mape_error, train_step
+
+__all__ = [
+    "BuckGNN", "GraphNetBlock", "MLPPooling", "Batch", "Data", "DataLoader", "Graph", "SegmentIndex",
+    "clear_caches", "graph_for", "segments_for", "SAGEConv", "global_add_pool", "global_max_pool",
+    "global_mean_pool", "scatter_add", "scatter_mean", "scatter_sum", "aggregate", "segment_reduce",
+    "install_pyg_shim", "uninstall_pyg_shim", "EigenvalueScaler", "GradAllReduce", "RelativeErrorLoss",
+    "mape_error", "train_step", "load_library",
+]
+
+
+def load_library():
+    """Load libbgnn.so (raises ImportError when it is missing)."""
+    return _lib.load()

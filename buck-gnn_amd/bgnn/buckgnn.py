@@ -1,0 +1,265 @@
+"""BuckGNN on MI355X: same constructor, same submodules / state-dict keys, same
+forward contract as Models/BuckGNN.py:9-526, with the SAGE layer loop run as
+fused HIP layers (bgnn.fused) instead of per-op modules.
+
+Variants and where their loop is defined in the reference:
+    GraphSage_addAggr / _sumAggr / _meanAggr      :430-458 -> fused (BN, ReLU, skip, dropout)
+    GraphSage_addAggr_Shared (TRAIN_FINAL default)  :338-352 -> fused (no BN)
+    GraphSage_maxAggr                               :459-471 -> per-op (bgnn SAGEConv max + torch BN)
+    EA_GNN / EA_GNN_Shared                          :326-336,375-387 -> per-op (GraphNetBlock on bgnn scatter_mean)
+    GraphSage_MLP / *_woBatchNorm / GraphSAGE_SAG / EAGNN_SAG -> reproduce the reference's behaviour
+      (AttributeError for the first three: their ModuleLists are never built, :404-429,472-492;
+       SAG variants need SAGPooling, out of scope).
+Pooling (get_pooling_layer, :246-307) is vectorised: the reference's per-node Python
+loop over `batch` (:256-271) is `last index of every run of equal batch ids`.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import Tensor, nn
+
+from .fused import sage_layer
+from .graph import Graph, SegmentIndex, graph_for, _index_cache
+from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
+from .ops import segment_reduce
+
+_SAGE_VARIANTS = {
+    # model_name: (ModuleList attribute, aggr, has BatchNorm)
+    "GraphSage_sumAggr": ("sage_blocks_sum", "sum", True),
+    "GraphSage_addAggr": ("sage_blocks_add", "add", True),
+    "GraphSage_meanAggr": ("sage_blocks_mean", "mean", True),
+    "GraphSage_maxAggr": ("sage_blocks_max", "max", True),
+}
+
+
+def _mlp(dims, final_relu=False):
+    layers = []
+    for a, b in zip(dims[:-1], dims[1:]):
+        layers += [nn.Linear(a, b), nn.ReLU()]
+    if not final_relu:
+        layers.pop()
+    return nn.Sequential(*layers)
+
+
+class GraphNetBlock(nn.Module):
+    """Edge-feature message block (Models/BuckGNN.py:528-566): edge MLP on
+    [x_row, x_col, e], message MLP phi on [x_col, e'], scatter_mean at row =
+    edge_index[0], node MLPs gamma and beta."""
+
+    def __init__(self, hidden_channels: int):
+        super().__init__()
+        h = hidden_channels
+        self.edge_mlp = _mlp([3 * h, h, h])
+        self.node_mlp_phi = _mlp([2 * h, h, h])
+        self.node_mlp_gamma = _mlp([2 * h, h, h])
+        self.node_mlp_beta = _mlp([h, h, h])
+
+    def forward(self, x: Tensor, edge_index: Tensor, edge_attr: Tensor):
+        row, col = edge_index[0], edge_index[1]
+        e = self.edge_mlp(torch.cat([x[row], x[col], edge_attr], 1))
+        m = self.node_mlp_phi(torch.cat([x[col], e], 1))
+        agg = scatter_mean(m, row, dim=0, dim_size=x.size(0))
+        out = self.node_mlp_gamma(torch.cat([x, agg], 1))
+        return out + self.node_mlp_beta(out), e
+
+
+class MLPPooling(nn.Module):
+    """global mean pool then Linear+ReLU (Models/BuckGNN.py:568-581)."""
+
+    def __init__(self, in_channels: int, hidden_channels: int, out_channels: int):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(in_channels, hidden_channels), nn.ReLU())
+
+    def forward(self, x: Tensor, batch: Optional[Tensor]):
+        return self.mlp(global_mean_pool(x, batch))
+
+
+def _output_dim(prediction_type: str, use_z_coord: bool, use_rotations: bool) -> int:
+    if prediction_type == "buckling":
+        return 1
+    if prediction_type == "static_disp":
+        return {(True, True): 6, (True, False): 3, (False, True): 4, (False, False): 2}[(use_z_coord, use_rotations)]
+    if prediction_type == "static_stress":
+        return 3
+    if prediction_type == "mode_shape":
+        return 6 if use_rotations else 3
+    return 1
+
+
+def batch_segments(batch: Tensor) -> SegmentIndex:
+    """Segment structure of a `batch` vector, cached per tensor (one host sync per new batch)."""
+    def build():
+        n = int(batch.max().item()) + 1 if batch.numel() else 0
+        return SegmentIndex.build(batch, n)
+    return _index_cache.get(batch, ("batch",), build)
+
+
+def super_node_index(batch: Optional[Tensor], n_nodes: int, device) -> Tensor:
+    """Index of the last node of every graph (the super node, VirtualEdgeCreate.py:106-107);
+    vectorised form of the reference's loop at Models/BuckGNN.py:256-266."""
+    if batch is None:
+        return torch.tensor([n_nodes - 1], device=device)
+    if batch.numel() == 0:
+        return torch.zeros(0, dtype=torch.long, device=device)
+    change = torch.nonzero(batch[1:] != batch[:-1]).flatten()
+    return torch.cat([change, torch.tensor([batch.numel() - 1], device=batch.device)])
+
+
+class BuckGNN(nn.Module):
+    def __init__(self, num_node_features, num_edge_features, hidden_channels=128, num_layers=6,
+                 pooling_layer="mean", prediction_type="buckling", use_z_coord=False, use_rotations=False,
+                 dropout_rate=0.1, model_name="GraphSAGE_MLP"):
+        super().__init__()
+        h = hidden_channels
+        self.hidden_channels = h
+        self.prediction_type = prediction_type
+        self.pooling_layer = pooling_layer
+        self.num_layers = num_layers
+        self.model_name = model_name
+        out_dim = _output_dim(prediction_type, use_z_coord, use_rotations)
+        dec_in = 2 * h if (pooling_layer == "supernode_with_pooling" and prediction_type == "buckling") else h
+        # encoders / decoder (Models/BuckGNN.py:41-100; nothing is built for 128 < h < 256)
+        if h <= 128:
+            self.node_encoder = _mlp([num_node_features, 64, h])
+            self.edge_encoder = _mlp([num_edge_features, 64, h])
+            self.decoder = _mlp([dec_in, 64, out_dim])
+        elif h >= 256:
+            self.node_encoder = _mlp([num_node_features, 64, 128, h])
+            self.edge_encoder = _mlp([num_edge_features, 64, 128, h])
+            self.decoder = _mlp([dec_in, 128, 64, out_dim])
+        # processors (Models/BuckGNN.py:103-180)
+        if model_name == "EA_GNN_Shared":
+            self.shared_gn_block = GraphNetBlock(h)
+        if model_name == "EA_GNN":
+            self.gn_blocks = nn.ModuleList([GraphNetBlock(h) for _ in range(num_layers)])
+        if model_name == "GraphSage_addAggr_Shared":
+            self.shared_graphsage_block = SAGEConv(in_channels=h, out_channels=h, normalize=True, aggr="add")
+        if model_name in _SAGE_VARIANTS:
+            attr, aggr, _ = _SAGE_VARIANTS[model_name]
+            setattr(self, attr, nn.ModuleList())
+            self.batch_norms = nn.ModuleList()
+            self.sage_mlps = nn.ModuleList()
+            for _ in range(num_layers):
+                getattr(self, attr).append(SAGEConv(in_channels=h, out_channels=h, normalize=True, aggr=aggr))
+                self.batch_norms.append(nn.BatchNorm1d(h))
+                self.sage_mlps.append(nn.Linear(h, h))
+        self.batch_norm = nn.BatchNorm1d(h)
+        self.relu = nn.ReLU()
+        self.dropout = nn.Dropout(p=dropout_rate)
+        self.pooling_mpl = MLPPooling(h, h, h)
+        if model_name in ("GraphSAGE_SAG", "EAGNN_SAG"):
+            self.pool = SAGPooling(h, ratio=0.5)  # raises: out of scope
+        # fused-path switch (tests compare both paths)
+        self.use_fused = True
+        self._step = 0
+
+    # ------------------------------------------------------------------ pooling
+    def get_pooling_layer(self, x: Tensor, edge_index: Tensor, batch: Optional[Tensor]) -> Tensor:
+        mode = self.pooling_layer
+        if mode == "mean":
+            if batch is None:
+                return global_mean_pool(x, None)
+            return segment_reduce(x, batch_segments(batch), "mean")
+        if mode == "hybrid":
+            raise AttributeError("'BuckGNN' object has no attribute 'hybrid_pooling'")  # Models/BuckGNN.py:188,276
+        if mode == "mlp":
+            return self.pooling_mpl(x, batch)
+        if "super" not in mode and mode != "mlp_no_super" and mode != "mean_no_super":
+            raise ValueError(f"Unknown pooling layer: {mode}")
+        sup = super_node_index(batch, x.size(0), x.device)
+        keep = torch.ones(x.size(0), dtype=torch.bool, device=x.device)
+        keep[sup] = False
+        real = torch.nonzero(keep).flatten()
+        if batch is None:
+            rb = torch.zeros(real.numel(), dtype=torch.long, device=x.device)
+        else:
+            rb = batch[real]
+        if mode == "mean_no_super":
+            return global_mean_pool(x[real], rb)
+        if mode == "supernode_only":
+            return x[sup]
+        if mode == "supernode_with_pooling":
+            return torch.cat([global_mean_pool(x[real], rb), x[sup]], 1)
+        if mode == "mlp_no_super":
+            return self.pooling_mpl(x[real], rb)
+        raise ValueError(f"Unknown pooling layer: {mode}")
+
+    # ------------------------------------------------------------------ forward
+    def _seed(self) -> int:
+        # dropout mask seed drawn from torch's CPU generator: reproducible under torch.manual_seed
+        return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+    def _fused_ok(self, x: Tensor) -> bool:
+        return self.use_fused and x.is_cuda and self.hidden_channels % 4 == 0 and self.hidden_channels <= 512
+
+    def _sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, aggr: str, skip_last_excluded: bool):
+        L = len(convs) if convs is not None else self.num_layers
+        p = self.dropout.p
+        if self._fused_ok(x) and aggr in ("add", "sum", "mean"):
+            graph = graph_for(edge_index, x.size(0))
+            red = 1 if aggr == "mean" else 0
+            for i in range(L):
+                conv = convs[i] if convs is not None else self.shared_graphsage_block
+                bn = bns[i] if bns is not None else None
+                skip = 0 < i < L - 1
+                x = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
+                               skip, p, self.training, self._seed())
+            return x
+        for i in range(L):
+            x_prev = x
+            conv = convs[i] if convs is not None else self.shared_graphsage_block
+            x = conv(x, edge_index)
+            if bns is not None:
+                x = bns[i](x)
+            x = self.relu(x)
+            if 0 < i < L - 1:
+                x = x + x_prev
+            x = self.dropout(x)
+        return x
+
+    def forward(self, x, edge_index, edge_attr, batch=None, mask=None):
+        name = self.model_name
+        if "super" in self.pooling_layer:
+            is_real_node = x[:, -1] == 0 if x.size(1) > 0 else torch.ones(x.size(0), dtype=torch.bool,
+                                                                           device=x.device)
+            real_node_batch = batch[is_real_node] if batch is not None else None
+        x = self.node_encoder(x)
+        if name == "EA_GNN_Shared":
+            e = self.edge_encoder(edge_attr)
+            for i in range(self.num_layers):
+                x_prev, e_prev = x, e
+                x, e = self.shared_gn_block(x, edge_index, e)
+                if 0 < i < self.num_layers - 1:
+                    x, e = x + x_prev, e + e_prev
+                x, e = self.dropout(x), self.dropout(e)
+        if name == "GraphSage_addAggr_Shared":
+            x = self._sage_loop(x, edge_index, None, None, "add", True)
+        elif name == "EA_GNN":
+            e = self.edge_encoder(edge_attr)
+            L = len(self.gn_blocks)
+            for i, blk in enumerate(self.gn_blocks):
+                x_prev, e_prev = x, e
+                x, e = blk(x, edge_index, e)
+                if 0 < i < L - 1:
+                    x, e = x + x_prev, e + e_prev
+                x, e = self.dropout(x), self.dropout(e)
+        elif name in _SAGE_VARIANTS:
+            attr, aggr, _ = _SAGE_VARIANTS[name]
+            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True)
+        elif name in ("GraphSage_addAggr_woBatchNorm", "GraphSage_MLP"):
+            getattr(self, "sage_blocks_add")  # AttributeError, as in the reference (:405,473)
+        elif name == "GraphSage_sumAggr_woBatchNorm":
+            getattr(self, "sage_blocks_sum")  # AttributeError, as in the reference (:418)
+        elif name in ("GraphSAGE_SAG", "EAGNN_SAG"):
+            raise NotImplementedError(f"{name}: SAGPooling variants are out of scope")
+
+        if self.prediction_type == "buckling":
+            pooled = self.get_pooling_layer(x, edge_index, batch)
+            return self.decoder(pooled).squeeze(), batch
+        if "static" in self.prediction_type or "mode_shape" in self.prediction_type:
+            if "super" in self.pooling_layer:
+                return self.decoder(x[is_real_node]), real_node_batch
+            return self.decoder(x), batch
+        raise ValueError(f"Unknown prediction type: {self.prediction_type}")

@@ -1,0 +1,232 @@
+"""Fused GraphSAGE layer for the BuckGNN layer loop (Models/BuckGNN.py:430-444).
+
+One autograd node per layer computes, for train or eval mode,
+
+    x_next = Dropout_p( ReLU( BN( normalize( SAGEConv(x_prev, edge_index) ) ) ) + [skip] x_prev )
+
+with SAGEConv(aggr in {add, sum, mean}, normalize=True) evaluated transform-first:
+
+    z   = x_prev · [W_l ; W_r]^T                 one fp32 MFMA GEMM, [N, 2H]
+    h_i = AGG_{j->i} z_l[j] + z_r[i] + b_l        (= lin_l(AGG x) + lin_r(x): AGG is linear)
+    o_i = h_i / max(||h_i||, 1e-12)               fused into the aggregation kernel,
+                                                  which also emits BatchNorm partial sums
+
+The backward mirrors it: BN statistics of dL/dx_next, a row-wise kernel for the
+BN + normalize backward giving dh, the transpose aggregation dz_l = A^T dh, and
+two GEMMs  dx = [dz_l | dh] · [W_l ; W_r]  and  d[W_l ; W_r] = [dz_l | dh]^T · x_prev.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .graph import Graph, _stream, require_cuda
+
+# "hip" = bgnn_gemm_f32 (hand-written f32 MFMA); "torch" = torch.mm (rocBLAS/hipBLASLt),
+# kept only for A/B measurement. Both run on the GPU.
+GEMM_BACKEND = "hip"
+
+# Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
+# on the launching stream around the named launch.
+TIMERS = None
+
+
+class _timed:
+    __slots__ = ("name", "ev")
+
+    def __init__(self, name):
+        self.name = name
+        self.ev = None
+
+    def __enter__(self):
+        if TIMERS is not None:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ev is not None:
+            self.ev[1].record()
+            TIMERS.setdefault(self.name, []).append(self.ev)
+        return False
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool, trans_b: bool, out: torch.Tensor = None,
+         beta: float = 0.0, alpha: float = 1.0) -> torch.Tensor:
+    """C = alpha * op(a) @ op(b) + beta * C (fp32, row-major operands, unit column stride)."""
+    M = a.size(1) if trans_a else a.size(0)
+    K = a.size(0) if trans_a else a.size(1)
+    N = b.size(0) if trans_b else b.size(1)
+    Kb = b.size(1) if trans_b else b.size(0)
+    if K != Kb:
+        raise ValueError(f"gemm: inner dims differ ({K} vs {Kb})")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+        beta = 0.0
+    if GEMM_BACKEND == "torch":
+        ra = a.t() if trans_a else a
+        rb = b.t() if trans_b else b
+        if beta == 0.0:
+            torch.mm(ra, rb, out=out)
+            if alpha != 1.0:
+                out.mul_(alpha)
+        else:
+            out.mul_(beta).addmm_(ra, rb, alpha=alpha)
+        return out
+    for t, nm in ((a, "A"), (b, "B"), (out, "C")):
+        if t.stride(1) != 1:
+            raise ValueError(f"gemm: {nm} must have unit column stride")
+    ws_bytes = _lib.query("bgnn_gemm_ws_bytes", M, N, K, int(trans_a), int(trans_b))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=a.device) if ws_bytes else None
+    _lib.call("bgnn_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), a.data_ptr(), a.stride(0),
+              b.data_ptr(), b.stride(0), float(beta), out.data_ptr(), out.stride(0),
+              None if ws is None else ws.data_ptr(), ws_bytes, _stream())
+    return out
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class LayerConfig:
+    __slots__ = ("reduce", "bn", "training", "momentum", "eps", "skip", "p", "seed")
+
+    def __init__(self, reduce: int, bn: bool, training: bool, momentum: float, eps: float, skip: bool,
+                 p: float, seed: int):
+        self.reduce = reduce
+        self.bn = bn
+        self.training = training
+        self.momentum = momentum
+        self.eps = eps
+        self.skip = skip
+        self.p = p if training else 0.0
+        self.seed = seed
+
+
+class SageLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_prev, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
+                cfg: LayerConfig):
+        N, H = x_prev.shape
+        dev = x_prev.device
+        x_prev = x_prev.contiguous()
+        wcat = torch.cat([w_l, w_r], 0).contiguous()             # [2H, H]
+        with _timed("gemm_fwd"):
+            z = gemm(x_prev, wcat, trans_a=False, trans_b=True)   # [N, 2H]
+        o = torch.empty(N, H, dtype=torch.float32, device=dev)
+        nrm = torch.empty(N, dtype=torch.float32, device=dev)
+        slots = _lib.query("bgnn_sage_fwd_slots", N) + graph.fwd.plan.n_heavy
+        bn_part = torch.empty(slots, 2, H, dtype=torch.float32, device=dev)
+        part = (torch.empty(graph.fwd.plan.n_chunks * H, dtype=torch.float32, device=dev)
+                if graph.fwd.plan.n_chunks else None)
+        s = _stream()
+        with _timed("sage_fwd"):
+            _lib.call("bgnn_sage_fwd", graph.fwd.ref(), z.data_ptr(), z.stride(0), b_l.data_ptr(), H, cfg.reduce,
+                      o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part), s)
+        del z
+        scale = shift = mean = invstd = None
+        if cfg.bn:
+            scale = torch.empty(H, dtype=torch.float32, device=dev)
+            shift = torch.empty(H, dtype=torch.float32, device=dev)
+            mean = torch.empty(H, dtype=torch.float32, device=dev)
+            invstd = torch.empty(H, dtype=torch.float32, device=dev)
+            if cfg.training:
+                _lib.call("bgnn_bn_finalize", bn_part.data_ptr(), slots, H, N, _ptr(gamma), _ptr(beta), cfg.eps,
+                          cfg.momentum, _ptr(running_mean), _ptr(running_var), mean.data_ptr(), invstd.data_ptr(),
+                          scale.data_ptr(), shift.data_ptr(), s)
+            else:
+                _lib.call("bgnn_bn_eval_coeffs", H, _ptr(gamma), _ptr(beta), cfg.eps, running_mean.data_ptr(),
+                          running_var.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
+                mean.copy_(running_mean)
+                invstd.copy_(torch.rsqrt(running_var + cfg.eps))
+        x_next = torch.empty(N, H, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_sage_apply", o.data_ptr(), _ptr(scale), _ptr(shift), x_prev.data_ptr(), int(cfg.skip),
+                  float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), s)
+        ctx.graph = graph
+        ctx.cfg = cfg
+        ctx.save_for_backward(x_prev, o, nrm, wcat, gamma if gamma is not None else torch.empty(0, device=dev),
+                              scale if scale is not None else torch.empty(0, device=dev),
+                              shift if shift is not None else torch.empty(0, device=dev),
+                              mean if mean is not None else torch.empty(0, device=dev),
+                              invstd if invstd is not None else torch.empty(0, device=dev))
+        return x_next
+
+    @staticmethod
+    def backward(ctx, g):
+        x_prev, o, nrm, wcat, gamma, scale, shift, mean, invstd = ctx.saved_tensors
+        cfg: LayerConfig = ctx.cfg
+        graph: Graph = ctx.graph
+        g = g.contiguous()
+        N, H = o.shape
+        dev = o.device
+        s = _stream()
+        bn = cfg.bn
+        dgamma = dbeta = None
+        sum_g2 = sum_g2xhat = None
+        if bn:
+            rs = _lib.query("bgnn_rows_slots", N)
+            part2 = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
+            _lib.call("bgnn_sage_bwd_stats", g.data_ptr(), o.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                      mean.data_ptr(), invstd.data_ptr(), float(cfg.p), cfg.seed, N, H, part2.data_ptr(), s)
+            sums = torch.empty(2, H, dtype=torch.float32, device=dev)
+            _lib.call("bgnn_reduce_partials", part2.data_ptr(), rs, H, sums[0].data_ptr(), sums[1].data_ptr(), 0, s)
+            dbeta, dgamma = sums[0], sums[1]
+            if cfg.training:
+                sum_g2, sum_g2xhat = sums[0], sums[1]
+            else:
+                sum_g2 = sum_g2xhat = torch.zeros(H, dtype=torch.float32, device=dev)
+        dz = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)
+        dh = dz[:, H:]
+        gskip = torch.empty(N, H, dtype=torch.float32, device=dev) if cfg.skip else None
+        rs = _lib.query("bgnn_rows_slots", N)
+        part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), o.data_ptr(), nrm.data_ptr(),
+                  _ptr(scale) if bn else None, _ptr(shift) if bn else None,
+                  _ptr(gamma) if (bn and gamma.numel()) else None,
+                  _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
+                  float(cfg.p), cfg.seed, int(cfg.skip), N, H, dh.data_ptr(), dz.stride(0), _ptr(gskip),
+                  part_db.data_ptr(), s)
+        db = torch.empty(H, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
+        # dz_l = A^T dh (transpose CSR; MEAN scales by the target's in-degree)
+        bw = graph.bwd
+        part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
+        with _timed("spmm_bwd"):
+            _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
+                      dh.data_ptr(), dz.stride(0), H, cfg.reduce, None, dz.data_ptr(), dz.stride(0), _ptr(part), s)
+        # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
+        if gskip is not None:
+            dx = gemm(dz, wcat, trans_a=False, trans_b=False, out=gskip, beta=1.0)
+        else:
+            dx = gemm(dz, wcat, trans_a=False, trans_b=False)
+        dw = gemm(dz, x_prev, trans_a=True, trans_b=False)      # [2H, H]
+        dw_l, dw_r = dw[:H], dw[H:]
+        has_affine = bn and gamma.numel() > 0
+        return (dx, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
+                None, None, None, None)
+
+
+def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,
+               bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
+               seed: int) -> torch.Tensor:
+    """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN)."""
+    require_cuda(x_prev, w_l, b_l, w_r, what="sage_layer")
+    H = x_prev.size(1)
+    if H % 4 or H > 512:
+        raise ValueError(f"sage_layer: fused path needs H % 4 == 0 and H <= 512 (got {H})")
+    if reduce not in (0, 1):
+        raise ValueError("sage_layer: fused path supports sum/mean aggregation only")
+    if bn_module is not None:
+        use_batch_stats = training or not bn_module.track_running_stats
+        momentum = bn_module.momentum
+        if training and bn_module.track_running_stats:
+            bn_module.num_batches_tracked.add_(1)
+            if momentum is None:
+                momentum = 1.0 / float(bn_module.num_batches_tracked.item())
+        cfg = LayerConfig(reduce, True, use_batch_stats, float(momentum or 0.0) if bn_module.track_running_stats
+                          else 0.0, float(bn_module.eps), skip, p, seed)
+        cfg.p = p if training else 0.0
+        return SageLayerFn.apply(x_prev, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
+                                 bn_module.running_mean, bn_module.running_var, graph, cfg)
+    cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
+    return SageLayerFn.apply(x_prev, w_l, b_l, w_r, None, None, None, None, graph, cfg)

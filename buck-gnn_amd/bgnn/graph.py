@@ -1,0 +1,203 @@
+"""Device-side graph structure: edge_index -> CSR (+ transpose) and heavy-row plans.
+
+PyG's `SAGEConv(x, edge_index)` (flow='source_to_target') aggregates, for every
+target i = edge_index[1, e], the source rows j = edge_index[0, e]
+(Models/BuckGNN.py:342,434). Here edge_index is sorted once per distinct tensor
+into a CSR over targets (for the forward) and a CSR over sources (for the
+backward), both stable, by `bgnn_graph_build`. Rows with more than `chunk`
+entries (the super node of VirtualEdgeCreate.py:81-113 has in-degree N_g) get a
+split plan so that one wave never walks thousands of neighbours alone.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+DEFAULT_CHUNK = 64
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_cuda(*tensors: torch.Tensor, what: str = "bgnn") -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                f"{what}: tensors must be on a ROCm GPU (got device {t.device}); "
+                "bgnn has no CPU fallback")
+
+
+@dataclass
+class Plan:
+    """Heavy-row split plan of one CSR (rows with deg > chunk)."""
+
+    heavy_row: torch.Tensor
+    heavy_chunk0: torch.Tensor
+    chunk_heavy: torch.Tensor
+    n_heavy: int
+    n_chunks: int
+    chunk: int
+
+
+def make_plan(rowptr: torch.Tensor, n_rows: int, nnz: int, chunk: int = DEFAULT_CHUNK) -> Plan:
+    dev = rowptr.device
+    heavy_row = torch.empty(max(n_rows, 1), dtype=torch.int32, device=dev)
+    heavy_chunk0 = torch.empty(max(n_rows, 1) + 1, dtype=torch.int32, device=dev)
+    # sum over heavy rows of ceil(deg/chunk) <= nnz/chunk + n_heavy <= 2*nnz/chunk
+    chunk_heavy = torch.empty(2 * (nnz // chunk) + 2, dtype=torch.int32, device=dev)
+    ws = torch.empty(_lib.query("bgnn_heavy_plan_ws_bytes", n_rows), dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_int32 * 2)()
+    _lib.call("bgnn_heavy_plan", rowptr.data_ptr(), n_rows, nnz, chunk, heavy_row.data_ptr(),
+              heavy_chunk0.data_ptr(), chunk_heavy.data_ptr(), ws.data_ptr(), ws.numel(),
+              ctypes.cast(counts, ctypes.c_void_p), _stream())
+    return Plan(heavy_row, heavy_chunk0, chunk_heavy, int(counts[0]), int(counts[1]), chunk)
+
+
+@dataclass
+class Csr:
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    n_rows: int
+    nnz: int
+    plan: Plan
+    _struct: Optional[_lib.CsrStruct] = field(default=None, repr=False)
+
+    def struct(self) -> _lib.CsrStruct:
+        if self._struct is None:
+            p = self.plan
+            self._struct = _lib.CsrStruct(
+                self.rowptr.data_ptr(), self.col.data_ptr(), p.heavy_row.data_ptr(),
+                p.heavy_chunk0.data_ptr(), p.chunk_heavy.data_ptr(), self.n_rows, self.nnz,
+                p.n_heavy, p.n_chunks, p.chunk, 0)
+        return self._struct
+
+    def ref(self):
+        return ctypes.byref(self.struct())
+
+    def degree(self) -> torch.Tensor:
+        return (self.rowptr[1:] - self.rowptr[:-1])
+
+
+@dataclass
+class Graph:
+    """Forward CSR (rows = targets) + transpose CSR (rows = sources) of an edge_index."""
+
+    num_nodes: int
+    num_edges: int
+    fwd: Csr
+    bwd: Csr
+    perm_t: torch.Tensor
+    edge_index: Optional[torch.Tensor] = field(default=None, repr=False)
+
+    @staticmethod
+    def build(edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK,
+              check: bool = True) -> "Graph":
+        require_cuda(edge_index, what="Graph.build")
+        if edge_index.dim() != 2 or edge_index.size(0) != 2:
+            raise ValueError(f"edge_index must have shape [2, E], got {tuple(edge_index.shape)}")
+        ei = edge_index.to(torch.int64).contiguous()
+        E = ei.size(1)
+        N = int(num_nodes)
+        dev = ei.device
+        rowptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
+        rowptr_t = torch.empty(N + 1, dtype=torch.int32, device=dev)
+        col = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+        col_t = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+        perm_t = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(_lib.query("bgnn_graph_build_ws_bytes", E, N), dtype=torch.uint8, device=dev)
+        status = (ctypes.c_int32 * 1)(0)
+        _lib.call("bgnn_graph_build", ei.data_ptr(), E, N, rowptr.data_ptr(), col.data_ptr(),
+                  rowptr_t.data_ptr(), col_t.data_ptr(), perm_t.data_ptr(), ws.data_ptr(), ws.numel(),
+                  ctypes.cast(status, ctypes.c_void_p) if check else None, _stream())
+        if check and status[0] != 0:
+            raise IndexError(f"edge_index contains indices outside [0, {N})")
+        fwd = Csr(rowptr, col, N, E, make_plan(rowptr, N, E, chunk))
+        bwd = Csr(rowptr_t, col_t, N, E, make_plan(rowptr_t, N, E, chunk))
+        return Graph(N, E, fwd, bwd, perm_t, edge_index)
+
+
+@dataclass
+class SegmentIndex:
+    """CSR of `index -> positions` (global_mean_pool's batch, scatter's index) + its transpose."""
+
+    n: int
+    num_rows: int
+    fwd: Csr          # rows = segments (graphs), col = positions
+    bwd: Csr          # rows = positions, exactly one entry: its segment
+
+    @staticmethod
+    def build(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK,
+              check: bool = True) -> "SegmentIndex":
+        require_cuda(index, what="SegmentIndex.build")
+        idx = index.to(torch.int64).contiguous().view(-1)
+        n = idx.numel()
+        R = int(num_rows)
+        dev = idx.device
+        rowptr = torch.empty(R + 1, dtype=torch.int32, device=dev)
+        col = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        ws = torch.empty(_lib.query("bgnn_graph_build_ws_bytes", n, R), dtype=torch.uint8, device=dev)
+        status = (ctypes.c_int32 * 1)(0)
+        _lib.call("bgnn_index_csr_build", idx.data_ptr(), n, R, rowptr.data_ptr(), col.data_ptr(),
+                  ws.data_ptr(), ws.numel(), ctypes.cast(status, ctypes.c_void_p) if check else None,
+                  _stream())
+        if check and status[0] != 0:
+            raise IndexError(f"index contains values outside [0, {R})")
+        fwd = Csr(rowptr, col, R, n, make_plan(rowptr, R, n, chunk))
+        rowptr_t = torch.arange(n + 1, dtype=torch.int32, device=dev)
+        col_t = idx.to(torch.int32)
+        empty = Plan(torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
+                     torch.zeros(1, dtype=torch.int32, device=dev), 0, 0, chunk)
+        bwd = Csr(rowptr_t, col_t if n > 0 else torch.zeros(1, dtype=torch.int32, device=dev), n, n, empty)
+        return SegmentIndex(n, R, fwd, bwd)
+
+
+class _Cache:
+    """Small identity cache: structure built once per distinct index tensor (and version)."""
+
+    def __init__(self, size: int = 8):
+        self.size = size
+        self.items = []  # list of (tensor, version, key, value)
+
+    def get(self, t: torch.Tensor, key, builder):
+        ver = t._version
+        for i, (tt, v, k, val) in enumerate(self.items):
+            if tt is t and v == ver and k == key:
+                if i:
+                    self.items.insert(0, self.items.pop(i))
+                return val
+        val = builder()
+        self.items.insert(0, (t, ver, key, val))
+        del self.items[self.size:]
+        return val
+
+    def clear(self):
+        self.items.clear()
+
+
+_graph_cache = _Cache()
+_index_cache = _Cache()
+
+
+def graph_for(edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK) -> Graph:
+    return _graph_cache.get(edge_index, (int(num_nodes), chunk),
+                            lambda: Graph.build(edge_index, num_nodes, chunk))
+
+
+def segments_for(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK) -> SegmentIndex:
+    return _index_cache.get(index, (int(num_rows), chunk),
+                            lambda: SegmentIndex.build(index, num_rows, chunk))
+
+
+def clear_caches() -> None:
+    _graph_cache.clear()
+    _index_cache.clear()

@@ -1,0 +1,163 @@
+"""PyG-compatible module / functional surface backed by libbgnn.
+
+Mirrors exactly the parts of torch_geometric / torch_scatter that buck-gnn calls
+(Models/BuckGNN.py:3-6, Utils/Losses.py:4):
+
+    SAGEConv(in_channels, out_channels, aggr='mean', normalize=False,
+             root_weight=True, project=False, bias=True)      -> forward(x, edge_index)
+    global_mean_pool / global_add_pool / global_max_pool(x, batch, size=None)
+    scatter_add / scatter_mean / scatter_max(src, index, dim=0, out=None, dim_size=None)
+
+State-dict keys of SAGEConv are PyG's (`lin_l.weight`, `lin_l.bias`, `lin_r.weight`,
+plus `lin.*` when project=True), so reference checkpoints load unchanged.
+PyG is not installed here and its version is not pinned by the reference
+(README.md:64-70); the semantics restated are those of PyG's documented
+SAGEConv: out_i = lin_l(AGG_{j->i} x_j) + lin_r(x_i), then F.normalize when
+normalize=True, with 'add' == 'sum' and empty neighbourhoods giving 0.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple, Union
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+from .graph import graph_for, segments_for
+from .ops import REDUCE, aggregate, segment_reduce
+
+
+class Linear(nn.Linear):
+    """torch.nn.Linear with PyG's initialisation (kaiming_uniform(a=sqrt(5)) weight,
+    uniform(±1/sqrt(in)) bias) — same distribution as nn.Linear's default."""
+
+    def reset_parameters(self) -> None:
+        bound_w = math.sqrt(6.0 / ((1 + 5.0) * self.in_features)) if self.in_features > 0 else 0.0
+        with torch.no_grad():
+            self.weight.uniform_(-bound_w, bound_w)
+            if self.bias is not None:
+                b = 1.0 / math.sqrt(self.in_features) if self.in_features > 0 else 0.0
+                self.bias.uniform_(-b, b)
+
+
+class SAGEConv(nn.Module):
+    """GraphSAGE operator with PyG's constructor, forward and state-dict layout."""
+
+    def __init__(self, in_channels: Union[int, Tuple[int, int]], out_channels: int, aggr: str = "mean",
+                 normalize: bool = False, root_weight: bool = True, project: bool = False, bias: bool = True,
+                 **kwargs):
+        super().__init__()
+        if isinstance(in_channels, int):
+            in_channels = (in_channels, in_channels)
+        if aggr not in REDUCE:
+            raise ValueError(f"SAGEConv: unsupported aggr '{aggr}' (supported: {sorted(REDUCE)})")
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.aggr = aggr
+        self.normalize = normalize
+        self.root_weight = root_weight
+        self.project = project
+        if project:
+            self.lin = Linear(in_channels[0], in_channels[0], bias=True)
+        self.lin_l = Linear(in_channels[0], out_channels, bias=bias)
+        if root_weight:
+            self.lin_r = Linear(in_channels[1], out_channels, bias=False)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        if self.project:
+            self.lin.reset_parameters()
+        self.lin_l.reset_parameters()
+        if self.root_weight:
+            self.lin_r.reset_parameters()
+
+    def forward(self, x: Union[Tensor, Tuple[Tensor, Tensor]], edge_index: Tensor, size=None) -> Tensor:
+        if size is not None:
+            raise NotImplementedError("SAGEConv: bipartite `size` is not supported by bgnn")
+        if isinstance(x, Tensor):
+            x = (x, x)
+        x_src, x_dst = x
+        if x_src.size(0) != x_dst.size(0):
+            raise NotImplementedError("SAGEConv: bipartite graphs are not supported by bgnn")
+        if self.project:
+            x_src = F.relu(self.lin(x_src))
+        graph = graph_for(edge_index, x_src.size(0))
+        out = self.lin_l(aggregate(x_src, graph, self.aggr))
+        if self.root_weight and x_dst is not None:
+            out = out + self.lin_r(x_dst)
+        if self.normalize:
+            out = F.normalize(out, p=2.0, dim=-1)
+        return out
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.in_channels[0]}, {self.out_channels}, aggr={self.aggr})"
+
+
+def _num_segments(index: Tensor, size: Optional[int]) -> int:
+    if size is not None:
+        return int(size)
+    return int(index.max().item()) + 1 if index.numel() else 0
+
+
+def _pool(x: Tensor, batch: Optional[Tensor], size: Optional[int], reduce: str) -> Tensor:
+    if batch is None:
+        if reduce == "mean":
+            return x.mean(dim=-2, keepdim=x.dim() == 2)
+        if reduce == "sum":
+            return x.sum(dim=-2, keepdim=x.dim() == 2)
+        return x.max(dim=-2, keepdim=x.dim() == 2)[0]
+    n = _num_segments(batch, size)
+    return segment_reduce(x, segments_for(batch, n), reduce)
+
+
+def global_mean_pool(x: Tensor, batch: Optional[Tensor], size: Optional[int] = None) -> Tensor:
+    return _pool(x, batch, size, "mean")
+
+
+def global_add_pool(x: Tensor, batch: Optional[Tensor], size: Optional[int] = None) -> Tensor:
+    return _pool(x, batch, size, "sum")
+
+
+def global_max_pool(x: Tensor, batch: Optional[Tensor], size: Optional[int] = None) -> Tensor:
+    return _pool(x, batch, size, "max")
+
+
+def _scatter(src: Tensor, index: Tensor, dim: int, out: Optional[Tensor], dim_size: Optional[int],
+             reduce: str) -> Tensor:
+    if src.dim() != 2 or dim not in (0, -2) or index.dim() != 1:
+        raise NotImplementedError("bgnn scatter: only 2-D src with a 1-D index along dim 0 is supported")
+    n = dim_size if dim_size is not None else (out.size(0) if out is not None else None)
+    n = _num_segments(index, n)
+    res = segment_reduce(src, segments_for(index, n), reduce)
+    if out is not None:
+        if reduce == "sum":
+            out.add_(res)
+        else:
+            out.copy_(res)
+        return out
+    return res
+
+
+def scatter_add(src: Tensor, index: Tensor, dim: int = 0, out: Optional[Tensor] = None,
+                dim_size: Optional[int] = None) -> Tensor:
+    return _scatter(src, index, dim, out, dim_size, "sum")
+
+
+def scatter_sum(src: Tensor, index: Tensor, dim: int = 0, out: Optional[Tensor] = None,
+                dim_size: Optional[int] = None) -> Tensor:
+    return _scatter(src, index, dim, out, dim_size, "sum")
+
+
+def scatter_mean(src: Tensor, index: Tensor, dim: int = 0, out: Optional[Tensor] = None,
+                 dim_size: Optional[int] = None) -> Tensor:
+    return _scatter(src, index, dim, out, dim_size, "mean")
+
+
+class SAGPooling(nn.Module):
+    """Placeholder for torch_geometric.nn.SAGPooling (GraphSAGE_SAG / EAGNN_SAG variants,
+    Models/BuckGNN.py:190-244). Not part of the hot path."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        raise NotImplementedError("bgnn: SAGPooling is not implemented (out of the hot-path scope)")

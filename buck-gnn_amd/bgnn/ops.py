@@ -1,0 +1,115 @@
+"""Autograd-wrapped segment reductions on libbgnn (no CPU fallback).
+
+* `aggregate(x, graph, reduce)` — SAGEConv's neighbour aggregation
+  (PyG semantics: sum over in-edges of target = edge_index[1]; 'add' == 'sum';
+  mean divides by the in-degree; max takes the element-wise maximum; empty
+  rows are 0 for all three). Used at Models/BuckGNN.py:342,393,434,449,463.
+* `segment_reduce(src, segments, reduce)` — global_mean_pool
+  (Models/BuckGNN.py:274) and torch_scatter.scatter_add / scatter_mean
+  (Models/BuckGNN.py:561,605).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .graph import Graph, SegmentIndex, _stream, require_cuda
+
+REDUCE = {"sum": 0, "add": 0, "mean": 1, "max": 2}
+
+
+def _check_x(x: torch.Tensor, what: str) -> torch.Tensor:
+    require_cuda(x, what=what)
+    if x.dtype != torch.float32:
+        raise TypeError(f"{what}: only float32 features are supported (got {x.dtype})")
+    if x.dim() != 2:
+        raise ValueError(f"{what}: expected a 2-D [rows, channels] tensor, got {tuple(x.shape)}")
+    return x.contiguous()
+
+
+def _partial(csr, H: int, reduce: int, dev) -> torch.Tensor:
+    n = csr.plan.n_chunks
+    if n == 0:
+        return None
+    # MAX keeps an int32 arg plane after the float plane
+    return torch.empty(n * H * (2 if reduce == 2 else 1), dtype=torch.float32, device=dev)
+
+
+def spmm_fwd(csr, x: torch.Tensor, reduce: int, out_rows: int, want_arg: bool = False):
+    H = x.size(1)
+    out = torch.empty(out_rows, H, dtype=torch.float32, device=x.device)
+    arg = torch.empty(out_rows, H, dtype=torch.int32, device=x.device) if (reduce == 2 and want_arg) else None
+    part = _partial(csr, H, reduce, x.device)
+    if out_rows > 0 and H > 0:
+        _lib.call("bgnn_spmm_fwd", csr.ref(), x.data_ptr(), x.stride(0), H, reduce, out.data_ptr(), out.stride(0),
+                  None if arg is None else arg.data_ptr(), None if part is None else part.data_ptr(), _stream())
+    return out, arg
+
+
+def spmm_bwd(csr_t, perm_t, fwd_rowptr, g: torch.Tensor, reduce: int, arg, out_rows: int):
+    g = g.contiguous()
+    H = g.size(1)
+    gx = torch.empty(out_rows, H, dtype=torch.float32, device=g.device)
+    part = _partial(csr_t, H, 0, g.device)
+    if out_rows > 0 and H > 0:
+        _lib.call("bgnn_spmm_bwd", csr_t.ref(), None if perm_t is None else perm_t.data_ptr(),
+                  None if fwd_rowptr is None else fwd_rowptr.data_ptr(), g.data_ptr(), g.stride(0), H, reduce,
+                  None if arg is None else arg.data_ptr(), gx.data_ptr(), gx.stride(0),
+                  None if part is None else part.data_ptr(), _stream())
+    return gx
+
+
+class _Aggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, graph: Graph, reduce: int):
+        out, arg = spmm_fwd(graph.fwd, x, reduce, graph.num_nodes, want_arg=x.requires_grad)
+        ctx.graph = graph
+        ctx.reduce = reduce
+        ctx.save_for_backward(arg if arg is not None else torch.empty(0, device=x.device))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        graph = ctx.graph
+        gx = spmm_bwd(graph.bwd, graph.perm_t, graph.fwd.rowptr, g, ctx.reduce,
+                      arg if ctx.reduce == 2 else None, graph.num_nodes)
+        return gx, None, None
+
+
+def aggregate(x: torch.Tensor, graph: Graph, reduce: str = "sum") -> torch.Tensor:
+    """out[i] = AGG_{j: (j -> i) in E} x[j]  (PyG SAGEConv aggregation)."""
+    x = _check_x(x, "aggregate")
+    if x.size(0) != graph.num_nodes:
+        raise ValueError(f"aggregate: x has {x.size(0)} rows, graph has {graph.num_nodes} nodes")
+    r = REDUCE[reduce]
+    return _Aggregate.apply(x, graph, r)
+
+
+class _SegmentReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, seg: SegmentIndex, reduce: int):
+        out, arg = spmm_fwd(seg.fwd, src, reduce, seg.num_rows, want_arg=src.requires_grad)
+        ctx.seg = seg
+        ctx.reduce = reduce
+        ctx.save_for_backward(arg if arg is not None else torch.empty(0, device=src.device))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        seg = ctx.seg
+        r = ctx.reduce
+        if r == 2:
+            (arg,) = ctx.saved_tensors
+            # position i receives g[seg(i), c] where arg[seg(i), c] is i's slot in the forward CSR.
+            slot = torch.empty(seg.n, dtype=torch.int32, device=g.device)
+            slot[seg.fwd.col[:seg.n].long()] = torch.arange(seg.n, dtype=torch.int32, device=g.device)
+            return spmm_bwd(seg.bwd, slot, seg.fwd.rowptr, g, 2, arg, seg.n), None, None
+        return spmm_bwd(seg.bwd, None, seg.fwd.rowptr, g, r, None, seg.n), None, None
+
+
+def segment_reduce(src: torch.Tensor, seg: SegmentIndex, reduce: str = "sum") -> torch.Tensor:
+    src = _check_x(src, "segment_reduce")
+    if src.size(0) != seg.n:
+        raise ValueError(f"segment_reduce: src has {src.size(0)} rows, index has {seg.n} entries")
+    return _SegmentReduce.apply(src, seg, REDUCE[reduce])

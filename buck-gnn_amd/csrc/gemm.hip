@@ -1,0 +1,264 @@
+// fp32 GEMM on the gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32): the dense
+// lin_l / lin_r of SAGEConv (Models/BuckGNN.py:135-149), i.e.
+//   forward  z  = x · [W_l ; W_r]^T          (M = nodes, N = 2H, K = H)
+//   dgrad    dx = [dz_l | dh] · [W_l ; W_r]   (M = nodes, N = H,  K = 2H)
+//   wgrad    dW = [dz_l | dh]^T · x           (M = 2H,    N = H,  K = nodes; split-K)
+// The f32 MFMA is an exact k-ordered fmaf chain (no TF32/xf32 on gfx950), so the
+// result is fp32-accurate like the reference's torch.mm.
+//
+// Tiling: 128x128 output tile per 256-thread workgroup, 4 waves as 2x2, each wave
+// 64x64 = 2x2 MFMA tiles of 32x32 (64 accumulator registers). K is staged through
+// LDS in BK=16 slices, double-buffered (one barrier per slice); the next slice's
+// global loads are issued before the current slice's MFMAs. Both operands are kept
+// in LDS as [k][m] / [k][n] images so each MFMA operand is one conflict-free
+// ds_read_b32 per lane. K-contiguous operands are transposed on the LDS store (row
+// pad of 2 floats makes those scalar stores conflict-free). Tile order is remapped
+// so each XCD owns a contiguous band of output rows (shared A panels stay in its L2).
+#include "common.h"
+
+namespace bgnn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+    const float* A;
+    const float* B;
+    float* C;
+    float* ws;
+    int64_t M, N, K, lda, ldb, ldc;
+    float alpha, beta;
+    int64_t kchunk;   // K range per split-K slice (multiple of BK)
+    int split;
+};
+
+constexpr int GBM = 128, GBN = 128, GBK = 16;
+
+template <int T>  // T = 1: operand is K-contiguous in global memory (needs transpose into LDS)
+struct OpLayout {
+    static constexpr int PAD = T ? 2 : 4;
+};
+
+// Load one BK x 128 slice of an operand into registers (2 float4 per thread).
+//   KCONTIG = 1: element (r, k) at P[r * ld + k]  (r = m or n, k contiguous)
+//   KCONTIG = 0: element (r, k) at P[k * ld + r]  (r contiguous)
+template <int KCONTIG>
+__device__ __forceinline__ void load_slice(const float* __restrict__ P, int64_t ld, int64_t R, int64_t r0,
+                                           int64_t k0, int64_t kend, bool vec_ok, float (&reg)[2][4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = t + 256 * i;
+        if constexpr (KCONTIG) {
+            const int r = idx >> 2, kq = idx & 3;
+            const int64_t gr = r0 + r, gk = k0 + kq * 4;
+            if (vec_ok && gr < R && gk + 3 < kend) {
+                const float4 v = *reinterpret_cast<const float4*>(P + gr * ld + gk);
+                reg[i][0] = v.x; reg[i][1] = v.y; reg[i][2] = v.z; reg[i][3] = v.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    reg[i][q] = (gr < R && gk + q < kend) ? P[gr * ld + gk + q] : 0.f;
+            }
+        } else {
+            const int kr = idx >> 5, rq = idx & 31;
+            const int64_t gk = k0 + kr, gr = r0 + rq * 4;
+            if (vec_ok && gk < kend && gr + 3 < R) {
+                const float4 v = *reinterpret_cast<const float4*>(P + gk * ld + gr);
+                reg[i][0] = v.x; reg[i][1] = v.y; reg[i][2] = v.z; reg[i][3] = v.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    reg[i][q] = (gk < kend && gr + q < R) ? P[gk * ld + gr + q] : 0.f;
+            }
+        }
+    }
+}
+
+template <int KCONTIG, int LDS_LD>
+__device__ __forceinline__ void store_slice(float* __restrict__ S, const float (&reg)[2][4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int idx = t + 256 * i;
+        if constexpr (KCONTIG) {
+            const int r = idx >> 2, kq = idx & 3;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) S[(kq * 4 + q) * LDS_LD + r] = reg[i][q];
+        } else {
+            const int kr = idx >> 5, rq = idx & 31;
+            *reinterpret_cast<float4*>(S + kr * LDS_LD + rq * 4) =
+                make_float4(reg[i][0], reg[i][1], reg[i][2], reg[i][3]);
+        }
+    }
+}
+
+// TA: 0 -> A is [M,K] (K-contiguous), 1 -> A is [K,M].
+// TB: 0 -> B is [K,N] (N-contiguous), 1 -> B is [N,K] (K-contiguous).
+template <int TA, int TB>
+__global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
+    constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
+    constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
+    constexpr int LDA_S = GBM + OpLayout<AK>::PAD;
+    constexpr int LDB_S = GBN + OpLayout<BKc>::PAD;
+    __shared__ __attribute__((aligned(16))) float As[2][GBK * LDA_S];
+    __shared__ __attribute__((aligned(16))) float Bs[2][GBK * LDB_S];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int64_t ntn = (g.N + GBN - 1) / GBN;
+    const int64_t ntm = (g.M + GBM - 1) / GBM;
+    const int tiles = (int)(ntm * ntn);
+    const int lt = xcd_remap(blockIdx.x, tiles);
+    const int64_t tm = lt / ntn, tn = lt % ntn;
+    const int64_t m0 = tm * GBM, n0 = tn * GBN;
+    const int64_t kb = (int64_t)blockIdx.y * g.kchunk;
+    const int64_t ke = min(g.K, kb + g.kchunk);
+
+    const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % 4 == 0);
+    const bool b_vec = (((uintptr_t)g.B & 15) == 0) && (g.ldb % 4 == 0);
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    float ra[2][4], rb[2][4];
+    const int64_t nk = (ke > kb) ? (ke - kb + GBK - 1) / GBK : 0;
+    if (nk > 0) {
+        load_slice<AK>(g.A, g.lda, g.M, m0, kb, ke, a_vec, ra);
+        load_slice<BKc>(g.B, g.ldb, g.N, n0, kb, ke, b_vec, rb);
+        store_slice<AK, LDA_S>(As[0], ra);
+        store_slice<BKc, LDB_S>(Bs[0], rb);
+    }
+    __syncthreads();
+
+    const int li = lane & 31, lk = lane >> 5;
+    for (int64_t kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) {
+            const int64_t k0 = kb + (kt + 1) * GBK;
+            load_slice<AK>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
+            load_slice<BKc>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
+        }
+        const float* as = As[cur];
+        const float* bs = Bs[cur];
+#pragma unroll
+        for (int kk = 0; kk < GBK / 2; ++kk) {
+            const int kr = 2 * kk + lk;
+            const float a0 = as[kr * LDA_S + wm * 64 + li];
+            const float a1 = as[kr * LDA_S + wm * 64 + 32 + li];
+            const float b0 = bs[kr * LDB_S + wn * 64 + li];
+            const float b1 = bs[kr * LDB_S + wn * 64 + 32 + li];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (more) {
+            store_slice<AK, LDA_S>(As[cur ^ 1], ra);
+            store_slice<BKc, LDB_S>(Bs[cur ^ 1], rb);
+        }
+        __syncthreads();
+    }
+
+    // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)blockIdx.y * g.M * g.N : g.C;
+    const int64_t ldd = g.split > 1 ? g.N : g.ldc;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t col = n0 + wn * 64 + j * 32 + li;
+            if (col >= g.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                if (row >= g.M) continue;
+                float v = acc[i][j][r];
+                if (g.split > 1) {
+                    dst[row * ldd + col] = v;
+                } else {
+                    v *= g.alpha;
+                    if (g.beta != 0.f) v += g.beta * dst[row * ldd + col];
+                    dst[row * ldd + col] = v;
+                }
+            }
+        }
+}
+
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ ws, int split, int64_t M,
+                                                       int64_t N, float alpha, float beta, float* __restrict__ C,
+                                                       int64_t ldc) {
+    const int64_t total = M * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < split; ++k) s += ws[(int64_t)k * total + i];
+        const int64_t r = i / N, c = i % N;
+        float v = alpha * s;
+        if (beta != 0.f) v += beta * C[r * ldc + c];
+        C[r * ldc + c] = v;
+    }
+}
+
+inline int choose_split(int64_t M, int64_t N, int64_t K) {
+    const int64_t tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+    if (tiles >= 512 || K < 4 * 256) return 1;
+    int64_t s = (1024 + tiles - 1) / tiles;
+    const int64_t smax = K / 256;   // keep >= 256 of K per slice
+    if (s > smax) s = smax;
+    if (s > 64) s = 64;
+    return s < 1 ? 1 : (int)s;
+}
+
+}  // namespace bgnn
+
+using namespace bgnn;
+
+extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb) {
+    (void)ta; (void)tb;
+    const int s = choose_split(M, N, K);
+    return s > 1 ? (size_t)s * (size_t)M * (size_t)N * sizeof(float) : 0;
+}
+
+extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                             int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, void* ws,
+                             size_t ws_bytes, void* stream) {
+    BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
+    BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
+    BGNN_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M) || M == 0 || K == 0, "gemm: bad lda");
+    BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm: bad ldb");
+    BGNN_REQUIRE(ldc >= N || M == 0, "gemm: bad ldc");
+    if (M == 0 || N == 0) return BGNN_OK;
+    const int64_t tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+    BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
+    hipStream_t s = as_stream(stream);
+    int split = choose_split(M, N, K);
+    if (split > 1 && (ws == nullptr || ws_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
+    GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split};
+    int64_t kc = (K + split - 1) / split;
+    kc = (kc + GBK - 1) / GBK * GBK;
+    g.kchunk = kc > 0 ? kc : GBK;
+    dim3 grid((unsigned)tiles, split);
+#define BGNN_G(TA, TB)                                                                          \
+    if (ta == TA && tb == TB) hipLaunchKernelGGL((k_gemm_f32<TA, TB>), grid, dim3(256), 0, s, g);
+    BGNN_G(0, 0)
+    BGNN_G(0, 1)
+    BGNN_G(1, 0)
+    BGNN_G(1, 1)
+#undef BGNN_G
+    BGNN_CHECK_LAUNCH();
+    if (split > 1) {
+        int64_t blocks = (M * N + 255) / 256;
+        if (blocks > 4096) blocks = 4096;
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, split, M, N,
+                           alpha, beta, C, ldc);
+        BGNN_CHECK_LAUNCH();
+    }
+    return BGNN_OK;
+}

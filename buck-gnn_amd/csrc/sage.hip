@@ -1,0 +1,423 @@
+// Fused element-wise / row-wise pieces of the GraphSAGE layer loop
+// (Models/BuckGNN.py:430-444):  BatchNorm1d(train) -> ReLU -> skip -> Dropout,
+// and the backward of BatchNorm + the L2 normalize of SAGEConv(normalize=True).
+//
+// All kernels stream [N, H] fp32 rows with 16-B (float4) accesses. Reductions
+// over N (BatchNorm statistics, bias gradient) are per-block partial sums over
+// contiguous row ranges, reduced afterwards in fp64 in a fixed order, so results
+// do not depend on scheduling.
+#include "common.h"
+
+namespace bgnn {
+
+constexpr int kRowsBlocks = 1024;   // max partial slots for row-blocked reductions
+
+inline int64_t rows_grid(int64_t n_rows, int rows_per_block_min, int64_t* rpb) {
+    int64_t blocks = (n_rows + rows_per_block_min - 1) / rows_per_block_min;
+    if (blocks > kRowsBlocks) blocks = kRowsBlocks;
+    if (blocks < 1) blocks = 1;
+    *rpb = (n_rows + blocks - 1) / blocks;
+    return blocks;
+}
+
+// ---------------------------------------------------------------------------
+// Reduce [n_slots, 2, H] partials; one thread per (channel, slot-phase).
+__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int n_slots, int H,
+                                                         float* __restrict__ out0, float* __restrict__ out1,
+                                                         int accumulate) {
+    __shared__ double red[4][2][64];
+    const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    double s0 = 0.0, s1 = 0.0;
+    if (c < H)
+        for (int sl = ph; sl < n_slots; sl += 4) {
+            s0 += (double)part[(int64_t)sl * 2 * H + c];
+            s1 += (double)part[(int64_t)sl * 2 * H + H + c];
+        }
+    red[ph][0][cl] = s0;
+    red[ph][1][cl] = s1;
+    __syncthreads();
+    if (ph == 0 && c < H) {
+        s0 = (red[0][0][cl] + red[1][0][cl]) + (red[2][0][cl] + red[3][0][cl]);
+        s1 = (red[0][1][cl] + red[1][1][cl]) + (red[2][1][cl] + red[3][1][cl]);
+        if (out0) out0[c] = accumulate ? out0[c] + (float)s0 : (float)s0;
+        if (out1) out1[c] = accumulate ? out1[c] + (float)s1 : (float)s1;
+    }
+}
+
+// BatchNorm1d finalize (train mode), torch semantics: biased var for
+// normalisation, unbiased var for running_var, momentum update.
+__global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ part, int n_slots, int H,
+                                                     int64_t count, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, float momentum,
+                                                     float* __restrict__ rmean, float* __restrict__ rvar,
+                                                     float* __restrict__ mean, float* __restrict__ invstd,
+                                                     float* __restrict__ scale, float* __restrict__ shift) {
+    __shared__ double red[4][2][64];
+    const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    double s0 = 0.0, s1 = 0.0;
+    if (c < H)
+        for (int sl = ph; sl < n_slots; sl += 4) {
+            s0 += (double)part[(int64_t)sl * 2 * H + c];
+            s1 += (double)part[(int64_t)sl * 2 * H + H + c];
+        }
+    red[ph][0][cl] = s0;
+    red[ph][1][cl] = s1;
+    __syncthreads();
+    if (ph == 0 && c < H) {
+        s0 = (red[0][0][cl] + red[1][0][cl]) + (red[2][0][cl] + red[3][0][cl]);
+        s1 = (red[0][1][cl] + red[1][1][cl]) + (red[2][1][cl] + red[3][1][cl]);
+        const double n = (double)count;
+        const double mu = s0 / n;
+        double var = s1 / n - mu * mu;
+        if (var < 0.0) var = 0.0;
+        const double is = 1.0 / sqrt(var + (double)eps);
+        const float g = gamma ? gamma[c] : 1.f;
+        const float b = beta ? beta[c] : 0.f;
+        mean[c] = (float)mu;
+        invstd[c] = (float)is;
+        scale[c] = (float)((double)g * is);
+        shift[c] = (float)((double)b - mu * (double)g * is);
+        if (rmean && rvar && momentum > 0.f) {
+            const double unb = count > 1 ? var * n / (n - 1.0) : var;
+            rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mu);
+            rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+        }
+    }
+}
+
+__global__ void k_bn_eval(int H, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                          const float* __restrict__ rmean, const float* __restrict__ rvar,
+                          float* __restrict__ scale, float* __restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= H) return;
+    const double is = 1.0 / sqrt((double)rvar[c] + (double)eps);
+    const double g = gamma ? gamma[c] : 1.0;
+    const double b = beta ? beta[c] : 0.0;
+    scale[c] = (float)(g * is);
+    shift[c] = (float)(b - (double)rmean[c] * g * is);
+}
+
+// ---------------------------------------------------------------------------
+// x_next = drop(relu(o*scale+shift) + skip*x_prev). Grid-stride over float4s.
+__global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift,
+                                                    const float4* __restrict__ xprev, int skip, uint32_t thr,
+                                                    float inv_keep, uint64_t seed, int64_t n4, int H4,
+                                                    float4* __restrict__ xn) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % H4) * 4;
+        float4 v = o[i];
+        float y[4] = {v.x, v.y, v.z, v.w};
+        if (scale) {
+            const float4 sc = *reinterpret_cast<const float4*>(scale + c);
+            const float4 sh = *reinterpret_cast<const float4*>(shift + c);
+            y[0] = y[0] * sc.x + sh.x; y[1] = y[1] * sc.y + sh.y;
+            y[2] = y[2] * sc.z + sh.z; y[3] = y[3] * sc.w + sh.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) y[k] = fmaxf(y[k], 0.f);
+        if (skip) {
+            const float4 p = xprev[i];
+            y[0] += p.x; y[1] += p.y; y[2] += p.z; y[3] += p.w;
+        }
+        if (thr) {
+            const uint32_t m = keep_bits4(seed, (uint64_t)i, thr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[k] = ((m >> k) & 1u) ? y[k] * inv_keep : 0.f;
+        }
+        xn[i] = make_float4(y[0], y[1], y[2], y[3]);
+    }
+}
+
+// Backward pass 1: partial sums over rows of g2 and g2*xhat per channel.
+// Thread layout: H4 = H/4 threads per row, 256/H4 rows per step.
+__global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict__ g, const float* __restrict__ o,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, uint32_t thr,
+                                                        float inv_keep, uint64_t seed, int64_t n_rows, int H,
+                                                        int64_t rows_per_block, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float red[2][2][512];
+    const int H4 = H / 4;
+    const int rpi = 256 / H4;                 // rows per iteration
+    const int t = threadIdx.x;
+    const int c4 = t % H4, ph = t / H4;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t r0 = (int64_t)lb * rows_per_block;
+    const int64_t r1 = min(n_rows, r0 + rows_per_block);
+    float s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+    const int c = c4 * 4;
+    if (ph < rpi) {
+        const float4 sc = *reinterpret_cast<const float4*>(scale + c);
+        const float4 sh = *reinterpret_cast<const float4*>(shift + c);
+        const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+        const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+        const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+        for (int64_t r = r0 + ph; r < r1; r += rpi) {
+            const int64_t i4 = r * H4 + c4;
+            const float4 gv = reinterpret_cast<const float4*>(g)[i4];
+            const float4 ov = reinterpret_cast<const float4*>(o)[i4];
+            float gg[4] = {gv.x, gv.y, gv.z, gv.w}, oo[4] = {ov.x, ov.y, ov.z, ov.w};
+            uint32_t m = 0xF;
+            if (thr) m = keep_bits4(seed, (uint64_t)i4, thr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float g1 = ((m >> k) & 1u) ? gg[k] * (thr ? inv_keep : 1.f) : 0.f;
+                const float yp = oo[k] * scv[k] + shv[k];
+                const float g2 = yp > 0.f ? g1 : 0.f;
+                const float xh = (oo[k] - muv[k]) * isv[k];
+                s0[k] += g2;
+                s1[k] += g2 * xh;
+            }
+        }
+    }
+    // reduce over row phases (rpi ≤ 2 for H = 512; general rpi via loop)
+    __shared__ __attribute__((aligned(16))) float red_all[256][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { red_all[t][k] = s0[k]; red_all[t][4 + k] = s1[k]; }
+    __syncthreads();
+    (void)red;
+    if (t < H4) {
+        float a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
+        for (int q = 0; q < rpi; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a0[k] += red_all[q * H4 + t][k];
+                a1[k] += red_all[q * H4 + t][4 + k];
+            }
+        float* dst = part + (int64_t)lb * 2 * H;
+        *reinterpret_cast<float4*>(dst + c) = make_float4(a0[0], a0[1], a0[2], a0[3]);
+        *reinterpret_cast<float4*>(dst + H + c) = make_float4(a1[0], a1[1], a1[2], a1[3]);
+    }
+}
+
+// Backward pass 2: one wave per row (H <= 512, NV float4 per lane).
+template <int NV>
+__global__ __launch_bounds__(256) void k_sage_bwd_rows(
+    const float* __restrict__ g, const float* __restrict__ o, const float* __restrict__ nrm,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sum_g2,
+    const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
+    int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
+    float* __restrict__ gskip, float* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t r0 = (int64_t)lb * rows_per_block;
+    const int64_t r1 = min(n_rows, r0 + rows_per_block);
+    const int H4 = H / 4;
+    const bool bn = (mean != nullptr);
+    const float invn = 1.f / (float)(n_rows > 0 ? n_rows : 1);
+    int cpos[NV];
+    bool cok[NV];
+    float scv[NV][4], shv[NV][4], kA[NV][4], kB[NV][4], kC[NV][4], muv[NV][4], isv[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        cpos[v] = (lane + 64 * v) * 4;
+        cok[v] = cpos[v] < H;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = cok[v] ? cpos[v] + k : 0;
+            scv[v][k] = scale ? scale[c] : 1.f;
+            shv[v][k] = shift ? shift[c] : 0.f;
+            if (bn) {
+                // do = gamma*invstd/N * (N*g2 - sum_g2 - xhat*sum_g2xhat)
+                const float gi = (gamma ? gamma[c] : 1.f) * invstd[c];
+                kA[v][k] = gi;
+                kB[v][k] = gi * sum_g2[c] * invn;
+                kC[v][k] = gi * sum_g2xhat[c] * invn;
+                muv[v][k] = mean[c];
+                isv[v][k] = invstd[c];
+            } else {
+                kA[v][k] = 1.f; kB[v][k] = 0.f; kC[v][k] = 0.f; muv[v][k] = 0.f; isv[v][k] = 0.f;
+            }
+        }
+    }
+    float db[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) db[v][k] = 0.f;
+
+    for (int64_t r = r0 + wave; r < r1; r += 4) {
+        float ov[NV][4], dov[NV][4], g1v[NV][4];
+        float dot = 0.f;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (!cok[v]) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ov[v][k] = dov[v][k] = g1v[v][k] = 0.f;
+                continue;
+            }
+            const int64_t i4 = r * H4 + (cpos[v] >> 2);
+            const float4 gv = reinterpret_cast<const float4*>(g)[i4];
+            const float4 o4 = reinterpret_cast<const float4*>(o)[i4];
+            const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+            ov[v][0] = o4.x; ov[v][1] = o4.y; ov[v][2] = o4.z; ov[v][3] = o4.w;
+            uint32_t m = 0xF;
+            if (thr) m = keep_bits4(seed, (uint64_t)i4, thr);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float g1 = ((m >> k) & 1u) ? gg[k] * (thr ? inv_keep : 1.f) : 0.f;
+                g1v[v][k] = g1;
+                const float yp = ov[v][k] * scv[v][k] + shv[v][k];
+                const float g2 = yp > 0.f ? g1 : 0.f;
+                float d;
+                if (bn) {
+                    const float xh = (ov[v][k] - muv[v][k]) * isv[v][k];
+                    d = kA[v][k] * g2 - kB[v][k] - xh * kC[v][k];
+                } else {
+                    d = g2;
+                }
+                dov[v][k] = d;
+                dot += ov[v][k] * d;
+            }
+        }
+        dot = group_sum(dot, kWave);
+        const float n = nrm[r];
+        const bool through = n >= 1e-12f;
+        const float rn = through ? 1.f / n : 1e12f;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (!cok[v]) continue;
+            float out[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                out[k] = through ? (dov[v][k] - ov[v][k] * dot) * rn : dov[v][k] * rn;
+                db[v][k] += out[k];
+            }
+            *reinterpret_cast<float4*>(dh + r * lddh + cpos[v]) = make_float4(out[0], out[1], out[2], out[3]);
+            if (skip)
+                *reinterpret_cast<float4*>(gskip + r * H + cpos[v]) =
+                    make_float4(g1v[v][0], g1v[v][1], g1v[v][2], g1v[v][3]);
+        }
+    }
+    __shared__ __attribute__((aligned(16))) float red[4][512];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+        if (cok[v])
+#pragma unroll
+            for (int k = 0; k < 4; ++k) red[wave][cpos[v] + k] = db[v][k];
+    __syncthreads();
+    float* dst = part + (int64_t)lb * 2 * H;
+    for (int c = threadIdx.x; c < H; c += 256) {
+        dst[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+        dst[H + c] = 0.f;
+    }
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace bgnn
+
+using namespace bgnn;
+
+extern "C" int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H, float* out0, float* out1,
+                                    int32_t accumulate, void* stream) {
+    BGNN_REQUIRE(partial && H > 0 && n_slots >= 0, "reduce_partials: bad args");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_reduce_partials, dim3((H + 63) / 64), dim3(256), 0, s, partial, n_slots, H, out0, out1,
+                       accumulate);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_bn_finalize(const float* bn_partial, int32_t n_slots, int32_t H, int64_t count,
+                                const float* gamma, const float* beta, float eps, float momentum,
+                                float* running_mean, float* running_var, float* mean, float* invstd, float* scale,
+                                float* shift, void* stream) {
+    BGNN_REQUIRE(bn_partial && H > 0 && count > 0 && mean && invstd && scale && shift, "bn_finalize: bad args");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_bn_finalize, dim3((H + 63) / 64), dim3(256), 0, s, bn_partial, n_slots, H, count, gamma,
+                       beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_bn_eval_coeffs(int32_t H, const float* gamma, const float* beta, float eps,
+                                   const float* running_mean, const float* running_var, float* scale, float* shift,
+                                   void* stream) {
+    BGNN_REQUIRE(H > 0 && running_mean && running_var && scale && shift, "bn_eval_coeffs: bad args");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_bn_eval, dim3((H + 255) / 256), dim3(256), 0, s, H, gamma, beta, eps, running_mean,
+                       running_var, scale, shift);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_sage_apply(const float* o, const float* scale, const float* shift, const float* x_prev,
+                               int32_t skip, float p, uint64_t seed, int64_t n_rows, int32_t H, float* x_next,
+                               void* stream) {
+    BGNN_REQUIRE(H > 0 && H % 4 == 0, "sage_apply: H must be a multiple of 4");
+    BGNN_REQUIRE(p >= 0.f && p < 1.f, "sage_apply: dropout p must be in [0, 1)");
+    BGNN_REQUIRE((scale == nullptr) == (shift == nullptr), "sage_apply: scale/shift must both be set or NULL");
+    BGNN_REQUIRE(!skip || x_prev, "sage_apply: skip requires x_prev");
+    BGNN_REQUIRE(al16(o) && al16(x_next) && (!x_prev || al16(x_prev)) && (!scale || (al16(scale) && al16(shift))),
+                 "sage_apply: pointers must be 16-byte aligned");
+    if (n_rows == 0) return BGNN_OK;
+    hipStream_t s = as_stream(stream);
+    const int64_t n4 = n_rows * (H / 4);
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    const uint32_t thr = dropout_threshold(p);
+    const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
+    hipLaunchKernelGGL(k_sage_apply, dim3((unsigned)blocks), dim3(256), 0, s, (const float4*)o, scale, shift,
+                       (const float4*)x_prev, skip, thr, inv_keep, seed, n4, H / 4, (float4*)x_next);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int32_t bgnn_rows_slots(int64_t n_rows) {
+    int64_t rpb = 0;
+    return (int32_t)rows_grid(n_rows, 4, &rpb);
+}
+
+extern "C" int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, const float* shift,
+                                   const float* mean, const float* invstd, float p, uint64_t seed, int64_t n_rows,
+                                   int32_t H, float* partial2, void* stream) {
+    BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 1024, "sage_bwd_stats: H=%d unsupported", H);
+    BGNN_REQUIRE(g && o && scale && shift && mean && invstd && partial2, "sage_bwd_stats: null pointer");
+    BGNN_REQUIRE(al16(g) && al16(o) && al16(scale) && al16(shift) && al16(mean) && al16(invstd) && al16(partial2),
+                 "sage_bwd_stats: pointers must be 16-byte aligned");
+    hipStream_t s = as_stream(stream);
+    int64_t rpb = 0;
+    const int64_t blocks = rows_grid(n_rows, 4, &rpb);
+    const uint32_t thr = dropout_threshold(p);
+    const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
+    hipLaunchKernelGGL(k_sage_bwd_stats, dim3((unsigned)blocks), dim3(256), 0, s, g, o, scale, shift, mean, invstd,
+                       thr, inv_keep, seed, n_rows, H, rpb, partial2);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm, const float* scale,
+                                  const float* shift, const float* gamma, const float* mean, const float* invstd,
+                                  const float* sum_g2, const float* sum_g2xhat, float p, uint64_t seed,
+                                  int32_t skip, int64_t n_rows, int32_t H, float* dh, int64_t lddh, float* gskip,
+                                  float* partial_db, void* stream) {
+    BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 512, "sage_bwd_rows: H=%d unsupported", H);
+    BGNN_REQUIRE(lddh >= H && lddh % 4 == 0, "sage_bwd_rows: bad lddh");
+    BGNN_REQUIRE(!skip || gskip, "sage_bwd_rows: skip requires gskip");
+    BGNN_REQUIRE(!mean || (invstd && sum_g2 && sum_g2xhat), "sage_bwd_rows: BN stats incomplete");
+    BGNN_REQUIRE(al16(g) && al16(o) && al16(dh) && (!gskip || al16(gskip)) && al16(partial_db),
+                 "sage_bwd_rows: pointers must be 16-byte aligned");
+    hipStream_t s = as_stream(stream);
+    int64_t rpb = 0;
+    const int64_t blocks = rows_grid(n_rows, 4, &rpb);
+    const uint32_t thr = dropout_threshold(p);
+    const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
+    if (H > 256)
+        hipLaunchKernelGGL(k_sage_bwd_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
+                           gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
+                           lddh, gskip, partial_db);
+    else
+        hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
+                           gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
+                           lddh, gskip, partial_db);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}

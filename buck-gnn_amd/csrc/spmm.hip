@@ -1,0 +1,608 @@
+// CSR segment-reduce kernels: SAGEConv neighbour aggregation (sum/mean/max),
+// its transpose (backward), global_mean_pool / scatter_mean / scatter_add, and
+// the fused SAGE forward epilogue (bias + lin_r term + L2 normalize + BatchNorm
+// statistics).
+//
+// Semantics follow PyG's SAGEConv as used at Models/BuckGNN.py:113-180,434:
+// target = edge_index[1], AGG over in-edges, empty segments give 0 (sum, mean,
+// max). The data layout is row-major [rows, H] fp32.
+//
+// Mapping to CDNA4 (MI355X): one 64-lane wavefront owns one destination row
+// (H = 512 fp32 = 2 KiB = two 1 KiB coalesced float4 wave-loads per neighbour).
+// Neighbour rows are gathered in batches of 8 (16 x 16-B loads in flight per
+// lane). A workgroup (4 waves) owns a contiguous range of rows, and the block
+// index is remapped so that every XCD works on a contiguous slice of the graph:
+// mesh neighbours (i±1, i±n, i±n±1; GraphCreate.py:334-350) are then L2 hits
+// and HBM sees each source row about once. Rows whose degree exceeds `chunk`
+// (super nodes, VirtualEdgeCreate.py:106-111) are skipped here and reduced by
+// `chunk`-edge pieces in k_seg_chunk, then combined in chunk order
+// (k_seg_combine) — deterministic, no atomics.
+#include "common.h"
+
+namespace bgnn {
+
+enum : int { OP_SUM = 0, OP_MEAN = 1, OP_MAX = 2, OP_MEANT = 3, OP_MAXT = 4 };
+enum : int { EPI_PLAIN = 0, EPI_SAGE = 1 };
+
+struct SegArgs {
+    // structure
+    const int32_t* rowptr;
+    const int32_t* col;
+    const int32_t* heavy_row;
+    const int32_t* heavy_chunk0;
+    const int32_t* chunk_heavy;
+    int64_t n_rows;
+    int32_t n_heavy, n_chunks, chunk;
+    int32_t H;
+    int64_t rows_per_block;
+    // data
+    const float* x;     int64_t ldx;
+    float* out;         int64_t ldo;
+    int32_t* arg;       // MAX: [n_rows, H] (ld = H)
+    float* partial;     // [n_chunks, H]
+    int32_t* partial_arg;
+    // transpose helpers
+    const int32_t* fwd_rowptr;  // MEANT
+    const int32_t* perm_t;      // MAXT
+    const int32_t* arg_in;      // MAXT: forward arg [n_fwd_rows, H]
+    // SAGE epilogue
+    const float* zr;    int64_t ldzr;   // lin_r term rows (z + H)
+    const float* bias;
+    float* nrm;
+    float* bn_partial;  // [slots, 2, H]
+    int32_t light_slots;
+};
+
+template <int VEC>
+struct Vec {
+    float f[VEC];
+};
+
+template <int VEC>
+__device__ __forceinline__ Vec<VEC> ld(const float* p) {
+    Vec<VEC> v;
+    if constexpr (VEC == 4) {
+        const float4 q = *reinterpret_cast<const float4*>(p);
+        v.f[0] = q.x; v.f[1] = q.y; v.f[2] = q.z; v.f[3] = q.w;
+    } else {
+        v.f[0] = *p;
+    }
+    return v;
+}
+
+template <int VEC>
+__device__ __forceinline__ void st(float* p, const Vec<VEC>& v) {
+    if constexpr (VEC == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(v.f[0], v.f[1], v.f[2], v.f[3]);
+    } else {
+        *p = v.f[0];
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void ldi(const int32_t* p, int32_t (&o)[VEC]) {
+    if constexpr (VEC == 4) {
+        const int4 q = *reinterpret_cast<const int4*>(p);
+        o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.w;
+    } else {
+        o[0] = *p;
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void sti(int32_t* p, const int32_t (&o)[VEC]) {
+    if constexpr (VEC == 4) {
+        *reinterpret_cast<int4*>(p) = make_int4(o[0], o[1], o[2], o[3]);
+    } else {
+        *p = o[0];
+    }
+}
+
+// Per-lane accumulator for NV vectors of VEC floats.
+template <int VEC, int NV, int OP>
+struct Acc {
+    float a[NV][VEC];
+    int32_t g[(OP == OP_MAX) ? NV : 1][(OP == OP_MAX) ? VEC : 1];
+
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                a[v][k] = (OP == OP_MAX) ? -INFINITY : 0.f;
+                if constexpr (OP == OP_MAX) g[v][k] = -1;
+            }
+    }
+};
+
+// Gather-accumulate the edges [e0, e1) of one row into acc. cols are shared by
+// the lanes of the row (wave-uniform when LPR == 64). `cpos[v]` = column offset
+// of this lane's v-th vector, `cok[v]` = whether it is inside H.
+template <int VEC, int NV, int OP, int U>
+__device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>& acc, int32_t e,
+                                             int32_t nvalid, const int (&cpos)[NV],
+                                             const bool (&cok)[NV]) {
+    int32_t j[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int32_t eu = e + (u < nvalid ? u : 0);
+        j[u] = A.col[eu];
+        w[u] = 1.f;
+        if constexpr (OP == OP_MEANT) {
+            const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
+            w[u] = 1.f / (float)(d > 0 ? d : 1);
+        }
+    }
+    Vec<VEC> val[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (cok[v]) val[u][v] = ld<VEC>(A.x + (int64_t)j[u] * A.ldx + cpos[v]);
+            else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) val[u][v].f[k] = 0.f;
+            }
+        }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool ok = u < nvalid;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if constexpr (OP == OP_MAXT) {
+                int32_t ga[VEC];
+                if (cok[v]) ldi<VEC>(A.arg_in + (int64_t)j[u] * A.H + cpos[v], ga);
+                else {
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) ga[k] = -2;
+                }
+                const int32_t pe = A.perm_t[e + (u < nvalid ? u : 0)];
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    acc.a[v][k] += (ok && ga[k] == pe) ? val[u][v].f[k] : 0.f;
+            } else if constexpr (OP == OP_MAX) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const bool better = ok && (val[u][v].f[k] > acc.a[v][k]);
+                    acc.a[v][k] = better ? val[u][v].f[k] : acc.a[v][k];
+                    acc.g[v][k] = better ? (e + u) : acc.g[v][k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) acc.a[v][k] += ok ? val[u][v].f[k] * w[u] : 0.f;
+            }
+        }
+    }
+}
+
+template <int VEC, int NV, int OP>
+__device__ __forceinline__ void gather_range(const SegArgs& A, Acc<VEC, NV, OP>& acc, int32_t beg,
+                                             int32_t end, const int (&cpos)[NV],
+                                             const bool (&cok)[NV]) {
+    int32_t e = beg;
+    for (; e + 8 <= end; e += 8) gather_batch<VEC, NV, OP, 8>(A, acc, e, 8, cpos, cok);
+    const int32_t rem = end - e;
+    if (rem > 4) gather_batch<VEC, NV, OP, 8>(A, acc, e, rem, cpos, cok);
+    else if (rem > 0) gather_batch<VEC, NV, OP, 4>(A, acc, e, rem, cpos, cok);
+}
+
+// Finish a plain reduction and store it (row r of out).
+template <int VEC, int NV, int OP>
+__device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& acc, int64_t r,
+                                            int32_t deg, const int (&cpos)[NV],
+                                            const bool (&cok)[NV]) {
+    const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        if (!cok[v]) continue;
+        Vec<VEC> o;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            float t = acc.a[v][k];
+            if constexpr (OP == OP_MAX) t = (deg > 0) ? t : 0.f;
+            o.f[k] = t * sc;
+        }
+        st<VEC>(A.out + r * A.ldo + cpos[v], o);
+        if constexpr (OP == OP_MAX) {
+            if (A.arg) {
+                int32_t gi[VEC];
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) gi[k] = deg > 0 ? acc.g[v][k] : -1;
+                sti<VEC>(A.arg + r * A.H + cpos[v], gi);
+            }
+        }
+    }
+}
+
+// Fused SAGE epilogue for one row held by a full wave (LPR == 64, VEC == 4):
+// h = acc*scale + z_r[r] + b; o = h / max(||h||, 1e-12); BN partial sums.
+template <int NV, int OP>
+__device__ __forceinline__ void store_sage(const SegArgs& A, Acc<4, NV, OP>& acc, int64_t r,
+                                           int32_t deg, const int (&cpos)[NV], const bool (&cok)[NV],
+                                           float (&bs)[NV][4], float (&bq)[NV][4]) {
+    const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
+    float h[NV][4];
+    float ss = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        if (cok[v]) {
+            const Vec<4> zr = ld<4>(A.zr + r * A.ldzr + cpos[v]);
+            const Vec<4> b = ld<4>(A.bias + cpos[v]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                h[v][k] = acc.a[v][k] * sc + zr.f[k] + b.f[k];
+                ss += h[v][k] * h[v][k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[v][k] = 0.f;
+        }
+    }
+    ss = group_sum(ss, kWave);
+    const float n = sqrtf(ss);
+    const float d = fmaxf(n, 1e-12f);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        if (!cok[v]) continue;
+        Vec<4> o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o.f[k] = h[v][k] / d;
+            bs[v][k] += o.f[k];
+            bq[v][k] += o.f[k] * o.f[k];
+        }
+        st<4>(A.out + r * A.ldo + cpos[v], o);
+    }
+    if ((threadIdx.x & 63) == 0) A.nrm[r] = n;
+}
+
+template <int VEC, int NV, int LPR>
+__device__ __forceinline__ void lane_cols(int cb, int lir, int H, int (&cpos)[NV], bool (&cok)[NV]) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        cpos[v] = cb + (lir + LPR * v) * VEC;
+        cok[v] = cpos[v] < H;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Light rows: deg <= chunk. Grid: (blocks, column tiles). 256 threads.
+template <int VEC, int NV, int LPR, int OP, int EPI>
+__global__ __launch_bounds__(256) void k_seg_light(SegArgs A) {
+    constexpr int RPW = kWave / LPR;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sub = lane / LPR, lir = lane % LPR;
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t r_begin = (int64_t)lb * A.rows_per_block;
+    const int64_t r_end = min(A.n_rows, r_begin + A.rows_per_block);
+    const int cb = blockIdx.y * (LPR * VEC * NV);
+    int cpos[NV];
+    bool cok[NV];
+    lane_cols<VEC, NV, LPR>(cb, lir, A.H, cpos, cok);
+
+    float bs[NV][4], bq[NV][4];
+    if constexpr (EPI == EPI_SAGE) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bs[v][k] = bq[v][k] = 0.f;
+    }
+
+    for (int64_t rb = r_begin + (int64_t)wave * RPW; rb < r_end; rb += 4 * RPW) {
+        const int64_t r = (RPW == 1) ? rb : rb + sub;
+        if (RPW > 1 && r >= r_end) continue;
+        const int32_t beg = A.rowptr[r], end = A.rowptr[r + 1];
+        const int32_t deg = end - beg;
+        if (deg > A.chunk) continue;  // heavy row: k_seg_chunk + k_seg_combine
+        Acc<VEC, NV, OP> acc;
+        acc.init();
+        gather_range<VEC, NV, OP>(A, acc, beg, end, cpos, cok);
+        if constexpr (EPI == EPI_SAGE) {
+            store_sage<NV, OP>(A, *reinterpret_cast<Acc<4, NV, OP>*>(&acc), r, deg, cpos, cok, bs, bq);
+        } else {
+            store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok);
+        }
+    }
+
+    if constexpr (EPI == EPI_SAGE) {
+        // block-reduce the BatchNorm partial sums over the 4 waves -> slot lb
+        __shared__ __attribute__((aligned(16))) float red[4][2][512];
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (cok[v])
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    red[wave][0][cpos[v] + k] = bs[v][k];
+                    red[wave][1][cpos[v] + k] = bq[v][k];
+                }
+        __syncthreads();
+        float* dst = A.bn_partial + (int64_t)lb * 2 * A.H;
+        for (int c = threadIdx.x; c < A.H; c += 256) {
+            dst[c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+            dst[A.H + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+        }
+    }
+}
+
+// Heavy chunks: one wave per chunk -> partial[c, :]. 256 threads (4 chunks).
+template <int VEC, int NV, int LPR, int OP>
+__global__ __launch_bounds__(256) void k_seg_chunk(SegArgs A) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * 4 + wave;
+    if (c >= A.n_chunks) return;
+    const int cb = blockIdx.y * (LPR * VEC * NV);
+    const int lir = lane % LPR;
+    if (lane / LPR != 0) return;  // one row per chunk: extra row-groups idle
+    int cpos[NV];
+    bool cok[NV];
+    lane_cols<VEC, NV, LPR>(cb, lir, A.H, cpos, cok);
+    const int32_t h = A.chunk_heavy[c];
+    const int32_t r = A.heavy_row[h];
+    const int32_t k = (int32_t)(c - A.heavy_chunk0[h]);
+    const int32_t beg = A.rowptr[r] + k * A.chunk;
+    const int32_t end = min(beg + A.chunk, A.rowptr[r + 1]);
+    Acc<VEC, NV, OP> acc;
+    acc.init();
+    gather_range<VEC, NV, OP>(A, acc, beg, end, cpos, cok);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        if (!cok[v]) continue;
+        Vec<VEC> o;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o.f[q] = acc.a[v][q];
+        st<VEC>(A.partial + c * A.H + cpos[v], o);
+        if constexpr (OP == OP_MAX) sti<VEC>(A.partial_arg + c * A.H + cpos[v], acc.g[v]);
+    }
+}
+
+// Combine heavy rows: one wave (64 threads) per heavy row, chunks in order.
+template <int VEC, int NV, int LPR, int OP, int EPI>
+__global__ __launch_bounds__(64) void k_seg_combine(SegArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int h = blockIdx.x;
+    if (h >= A.n_heavy) return;
+    if (lane / LPR != 0) return;
+    const int cb = blockIdx.y * (LPR * VEC * NV);
+    const int lir = lane % LPR;
+    int cpos[NV];
+    bool cok[NV];
+    lane_cols<VEC, NV, LPR>(cb, lir, A.H, cpos, cok);
+    const int64_t r = A.heavy_row[h];
+    const int32_t deg = A.rowptr[r + 1] - A.rowptr[r];
+    const int32_t c0 = A.heavy_chunk0[h], c1 = A.heavy_chunk0[h + 1];
+    Acc<VEC, NV, OP> acc;
+    acc.init();
+    for (int32_t c = c0; c < c1; ++c) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (!cok[v]) continue;
+            const Vec<VEC> p = ld<VEC>(A.partial + (int64_t)c * A.H + cpos[v]);
+            if constexpr (OP == OP_MAX) {
+                int32_t pa[VEC];
+                ldi<VEC>(A.partial_arg + (int64_t)c * A.H + cpos[v], pa);
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                    const bool better = p.f[q] > acc.a[v][q];
+                    acc.a[v][q] = better ? p.f[q] : acc.a[v][q];
+                    acc.g[v][q] = better ? pa[q] : acc.g[v][q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) acc.a[v][q] += p.f[q];
+            }
+        }
+    }
+    if constexpr (EPI == EPI_SAGE) {
+        float bs[NV][4], bq[NV][4];
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bs[v][k] = bq[v][k] = 0.f;
+        store_sage<NV, OP>(A, *reinterpret_cast<Acc<4, NV, OP>*>(&acc), r, deg, cpos, cok, bs, bq);
+        float* dst = A.bn_partial + (int64_t)(A.light_slots + h) * 2 * A.H;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (cok[v]) {
+                Vec<4> s1, s2;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { s1.f[k] = bs[v][k]; s2.f[k] = bq[v][k]; }
+                st<4>(dst + cpos[v], s1);
+                st<4>(dst + A.H + cpos[v], s2);
+            }
+    } else {
+        store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok);
+    }
+}
+
+// ---------------------------------------------------------------------------
+constexpr int kMaxLightBlocks = 1024;
+
+struct Geometry {
+    int vec, nv, lpr, ctiles;
+};
+
+inline int pow2ceil(int x) {
+    int p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+inline Geometry pick_geometry(int H, bool aligned16) {
+    Geometry g;
+    if (aligned16 && H % 4 == 0) {
+        g.vec = 4;
+        const int nv4 = H / 4;
+        if (nv4 >= 128) { g.lpr = 64; g.nv = 2; }
+        else if (nv4 > 64) { g.lpr = 64; g.nv = 2; }
+        else { g.lpr = pow2ceil(nv4 < 16 ? 16 : nv4); g.nv = 1; }
+        g.ctiles = (H + g.lpr * 4 * g.nv - 1) / (g.lpr * 4 * g.nv);
+    } else {
+        g.vec = 1;
+        g.nv = 1;
+        g.lpr = pow2ceil(H < 16 ? 16 : (H > 64 ? 64 : H));
+        g.ctiles = (H + g.lpr - 1) / g.lpr;
+    }
+    return g;
+}
+
+inline int64_t light_grid(int64_t n_rows, int rows_per_wave, int max_blocks, int64_t* rpb) {
+    const int64_t per_block = 4 * rows_per_wave;
+    int64_t blocks = (n_rows + per_block - 1) / per_block;
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks < 1) blocks = 1;
+    *rpb = (n_rows + blocks - 1) / blocks;
+    return blocks;
+}
+
+template <int VEC, int NV, int LPR, int OP, int EPI>
+int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* blocks_out) {
+    int64_t rpb = 0;
+    const int64_t blocks = light_grid(A.n_rows, kWave / LPR, max_blocks, &rpb);
+    A.rows_per_block = rpb;
+    if (blocks_out) *blocks_out = blocks;
+    A.light_slots = (int32_t)blocks;
+    if (A.n_rows > 0) {
+        hipLaunchKernelGGL((k_seg_light<VEC, NV, LPR, OP, EPI>), dim3((unsigned)blocks, ctiles), dim3(256),
+                           0, s, A);
+        BGNN_CHECK_LAUNCH();
+    }
+    if (A.n_chunks > 0) {
+        constexpr int COP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MAXT ? OP_MAXT : (OP == OP_MEANT ? OP_MEANT : OP_SUM));
+        hipLaunchKernelGGL((k_seg_chunk<VEC, NV, LPR, COP>), dim3((A.n_chunks + 3) / 4, ctiles), dim3(256), 0, s,
+                           A);
+        BGNN_CHECK_LAUNCH();
+        constexpr int MOP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MEAN ? OP_MEAN : OP_SUM);
+        hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles), dim3(64), 0, s, A);
+        BGNN_CHECK_LAUNCH();
+    }
+    return BGNN_OK;
+}
+
+template <int OP>
+int dispatch_plain(SegArgs A, const Geometry& g, hipStream_t s) {
+#define BGNN_PLAIN(V, N, L)                                                              \
+    if (g.vec == V && g.nv == N && g.lpr == L)                                           \
+        return launch_all<V, N, L, OP, EPI_PLAIN>(A, g.ctiles, 2048, s, nullptr);
+    BGNN_PLAIN(4, 2, 64)
+    BGNN_PLAIN(4, 1, 64)
+    BGNN_PLAIN(4, 1, 32)
+    BGNN_PLAIN(4, 1, 16)
+    BGNN_PLAIN(1, 1, 64)
+    BGNN_PLAIN(1, 1, 32)
+    BGNN_PLAIN(1, 1, 16)
+#undef BGNN_PLAIN
+    return fail(BGNN_E_UNSUPPORTED, "spmm: no kernel for vec=%d nv=%d lpr=%d", g.vec, g.nv, g.lpr);
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+inline SegArgs args_from_csr(const bgnn_csr_t* c) {
+    SegArgs A{};
+    A.rowptr = c->rowptr;
+    A.col = c->col;
+    A.heavy_row = c->heavy_row;
+    A.heavy_chunk0 = c->heavy_chunk0;
+    A.chunk_heavy = c->chunk_heavy;
+    A.n_rows = c->n_rows;
+    A.n_heavy = c->n_heavy;
+    A.n_chunks = c->n_chunks;
+    A.chunk = c->chunk > 0 ? c->chunk : 0x7fffffff;
+    return A;
+}
+
+}  // namespace bgnn
+
+using namespace bgnn;
+
+extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H, int32_t reduce,
+                             float* out, int64_t ldo, int32_t* arg, float* partial, void* stream) {
+    BGNN_REQUIRE(csr && csr->rowptr, "spmm_fwd: null csr");
+    BGNN_REQUIRE(H > 0 && ldx >= H && ldo >= H, "spmm_fwd: bad H/ld");
+    BGNN_REQUIRE(reduce >= 0 && reduce <= 2, "spmm_fwd: bad reduce %d", reduce);
+    BGNN_REQUIRE(csr->n_chunks == 0 || partial, "spmm_fwd: partial scratch required for heavy rows");
+    SegArgs A = args_from_csr(csr);
+    A.H = H;
+    A.x = x; A.ldx = ldx;
+    A.out = out; A.ldo = ldo;
+    A.arg = arg;
+    A.partial = partial;
+    A.partial_arg = partial ? reinterpret_cast<int32_t*>(partial + (int64_t)csr->n_chunks * H) : nullptr;
+    const bool al = aligned16(x) && aligned16(out) && ldx % 4 == 0 && ldo % 4 == 0 &&
+                    (!partial || aligned16(partial)) && (!arg || aligned16(arg));
+    const Geometry g = pick_geometry(H, al);
+    hipStream_t s = as_stream(stream);
+    switch (reduce) {
+        case BGNN_REDUCE_SUM: return dispatch_plain<OP_SUM>(A, g, s);
+        case BGNN_REDUCE_MEAN: return dispatch_plain<OP_MEAN>(A, g, s);
+        default: return dispatch_plain<OP_MAX>(A, g, s);
+    }
+}
+
+extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                             const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                             float* gx, int64_t ldgx, float* partial, void* stream) {
+    BGNN_REQUIRE(csr_t && csr_t->rowptr, "spmm_bwd: null csr");
+    BGNN_REQUIRE(H > 0 && ldg >= H && ldgx >= H, "spmm_bwd: bad H/ld");
+    BGNN_REQUIRE(csr_t->n_chunks == 0 || partial, "spmm_bwd: partial scratch required");
+    SegArgs A = args_from_csr(csr_t);
+    A.H = H;
+    A.x = g; A.ldx = ldg;
+    A.out = gx; A.ldo = ldgx;
+    A.partial = partial;
+    A.fwd_rowptr = fwd_rowptr;
+    A.perm_t = perm_t;
+    A.arg_in = arg;
+    const bool al = aligned16(g) && aligned16(gx) && ldg % 4 == 0 && ldgx % 4 == 0 &&
+                    (!partial || aligned16(partial)) && (!arg || aligned16(arg));
+    const Geometry geo = pick_geometry(H, al);
+    hipStream_t s = as_stream(stream);
+    switch (reduce) {
+        case BGNN_REDUCE_SUM: return dispatch_plain<OP_SUM>(A, geo, s);
+        case BGNN_REDUCE_MEAN:
+            BGNN_REQUIRE(fwd_rowptr, "spmm_bwd(mean): fwd_rowptr required");
+            return dispatch_plain<OP_MEANT>(A, geo, s);
+        default:
+            BGNN_REQUIRE(perm_t && arg, "spmm_bwd(max): perm_t and arg required");
+            return dispatch_plain<OP_MAXT>(A, geo, s);
+    }
+}
+
+extern "C" int32_t bgnn_sage_fwd_slots(int64_t n_rows) {
+    int64_t rpb = 0;
+    return (int32_t)light_grid(n_rows, 1, kMaxLightBlocks, &rpb);
+}
+
+extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* z, int64_t ldz, const float* bias, int32_t H,
+                             int32_t reduce, float* o, float* nrm, float* bn_partial, float* partial,
+                             void* stream) {
+    BGNN_REQUIRE(csr && csr->rowptr, "sage_fwd: null csr");
+    BGNN_REQUIRE(H > 0 && H <= 512 && H % 4 == 0, "sage_fwd: H=%d unsupported (need H%%4==0, H<=512)", H);
+    BGNN_REQUIRE(ldz >= 2 * H && ldz % 4 == 0, "sage_fwd: ldz=%lld must be >= 2H and a multiple of 4",
+                 (long long)ldz);
+    BGNN_REQUIRE(reduce == BGNN_REDUCE_SUM || reduce == BGNN_REDUCE_MEAN, "sage_fwd: reduce must be sum/mean");
+    BGNN_REQUIRE(aligned16(z) && aligned16(o) && aligned16(bias) && aligned16(bn_partial) &&
+                     (!partial || aligned16(partial)),
+                 "sage_fwd: pointers must be 16-byte aligned");
+    BGNN_REQUIRE(csr->n_chunks == 0 || partial, "sage_fwd: partial scratch required for heavy rows");
+    SegArgs A = args_from_csr(csr);
+    A.H = H;
+    A.x = z; A.ldx = ldz;
+    A.zr = z + H; A.ldzr = ldz;
+    A.bias = bias;
+    A.out = o; A.ldo = H;
+    A.nrm = nrm;
+    A.bn_partial = bn_partial;
+    A.partial = partial;
+    hipStream_t s = as_stream(stream);
+    int64_t blocks = 0;
+    if (H > 256) {
+        return reduce == BGNN_REDUCE_SUM
+                   ? launch_all<4, 2, 64, OP_SUM, EPI_SAGE>(A, 1, kMaxLightBlocks, s, &blocks)
+                   : launch_all<4, 2, 64, OP_MEAN, EPI_SAGE>(A, 1, kMaxLightBlocks, s, &blocks);
+    }
+    return reduce == BGNN_REDUCE_SUM ? launch_all<4, 1, 64, OP_SUM, EPI_SAGE>(A, 1, kMaxLightBlocks, s, &blocks)
+                                     : launch_all<4, 1, 64, OP_MEAN, EPI_SAGE>(A, 1, kMaxLightBlocks, s, &blocks);
+}

@@ -1,0 +1,207 @@
+/*
+ * bgnn.h — C-ABI of libbgnn.so, the MI355X (gfx950) kernels behind buck-gnn's
+ * GraphSAGE message-passing hot path.
+ *
+ * The reference (omerkurt-okt/buck-gnn) is pure Python; its hot path calls into
+ * third-party PyG / torch_scatter ops. Each entry point below replaces the
+ * arithmetic of one of those calls:
+ *
+ *   bgnn_graph_build / bgnn_heavy_plan  ← the edge_index preprocessing PyG's
+ *       propagate() implies for `SAGEConv(x, edge_index)` (flow='source_to_target':
+ *       edge_index[0] = source j, edge_index[1] = target i), called at
+ *       Models/BuckGNN.py:342,393,434,449,463; edge_index is produced at
+ *       Dataset_Preparation/GraphCreate.py:417-422 (both directions, int64).
+ *   bgnn_spmm_fwd / bgnn_spmm_bwd  ← SAGEConv's neighbour aggregation
+ *       (aggr='add'|'sum'|'mean'|'max', Models/BuckGNN.py:118,130,145,160,175),
+ *       global_mean_pool (Models/BuckGNN.py:274) and torch_scatter.scatter_add /
+ *       scatter_mean (Models/BuckGNN.py:561,605).
+ *   bgnn_sage_fwd_*, bgnn_bn_*, bgnn_sage_bwd_*  ← the fused layer of
+ *       Models/BuckGNN.py:430-444: SAGEConv(normalize=True) → BatchNorm1d → ReLU →
+ *       skip (0<i<L-1) → Dropout, and its autograd backward.
+ *   bgnn_gemm_f32  ← lin_l / lin_r of SAGEConv (dense fp32 linear, MFMA).
+ *
+ * Conventions (all functions):
+ *   - every pointer is a DEVICE pointer unless named host_*;
+ *   - `stream` is a hipStream_t passed as void*; the library never uses the
+ *     default stream and never allocates device memory: scratch comes from the
+ *     caller through (ws, ws_bytes);
+ *   - return 0 on success, otherwise a hipError_t or a BGNN_E* code; the message
+ *     is available from bgnn_last_error_string() (per calling thread);
+ *   - no C++ exception crosses this boundary.
+ */
+#ifndef BGNN_H
+#define BGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BGNN_ABI_VERSION 1
+
+#define BGNN_OK 0
+#define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
+#define BGNN_E_WS 1002        /* workspace too small                             */
+#define BGNN_E_UNSUPPORTED 1003
+
+/* reduction selector, PyG aggr= names: 'add' == 'sum' */
+#define BGNN_REDUCE_SUM 0
+#define BGNN_REDUCE_MEAN 1
+#define BGNN_REDUCE_MAX 2
+
+int bgnn_abi_version(void);
+const char* bgnn_last_error_string(void);
+
+/* ------------------------------------------------------------------------
+ * Graph structure. A CSR over destination rows plus the split plan for rows
+ * whose in-degree exceeds `chunk` (super nodes: VirtualEdgeCreate.py:106-111).
+ * Rows with deg > chunk are reduced in chunks of `chunk` edges by separate
+ * waves into a partial buffer and combined in chunk order (deterministic).
+ * ---------------------------------------------------------------------- */
+typedef struct bgnn_csr {
+    const int32_t* rowptr;       /* [n_rows + 1]                               */
+    const int32_t* col;          /* [nnz]  source row of each entry            */
+    const int32_t* heavy_row;    /* [n_heavy] row id of each heavy row         */
+    const int32_t* heavy_chunk0; /* [n_heavy + 1] first chunk of each heavy row*/
+    const int32_t* chunk_heavy;  /* [n_chunks] heavy index owning each chunk   */
+    int64_t n_rows;
+    int64_t nnz;
+    int32_t n_heavy;
+    int32_t n_chunks;
+    int32_t chunk;               /* edges per chunk; rows with deg > chunk are heavy */
+    int32_t _pad;
+} bgnn_csr_t;
+
+/* Workspace for bgnn_graph_build (bytes). */
+size_t bgnn_graph_build_ws_bytes(int64_t num_edges, int64_t num_nodes);
+
+/* Sort a COO edge_index [2, E] (int64, row 0 = source, row 1 = target) into
+ *   forward CSR (rows = targets):   rowptr[N+1], col[E] = sources,
+ *   transpose CSR (rows = sources): rowptr_t[N+1], col_t[E] = targets,
+ *                                   perm_t[E] = forward-CSR position of the edge.
+ * Both sorts are stable, so entries of a row keep edge_index order.
+ * `host_status[0]` receives 0, or 1 if an index was outside [0, N); the call
+ * synchronises the stream only when host_status != NULL. */
+int bgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                     int32_t* rowptr, int32_t* col,
+                     int32_t* rowptr_t, int32_t* col_t, int32_t* perm_t,
+                     void* ws, size_t ws_bytes, int32_t* host_status, void* stream);
+
+/* CSR over segments given a sorted-or-unsorted index vector (global_mean_pool's
+ * `batch`, torch_scatter's `index`): row r lists the positions i with index[i]==r,
+ * in increasing i. Same workspace rule as bgnn_graph_build with E = n. */
+int bgnn_index_csr_build(const int64_t* index, int64_t n, int64_t num_rows,
+                         int32_t* rowptr, int32_t* col,
+                         void* ws, size_t ws_bytes, int32_t* host_status, void* stream);
+
+/* Heavy-row plan for a CSR (rows with deg > chunk). Outputs are device arrays
+ * sized for the worst case: heavy_row[n_rows], heavy_chunk0[n_rows+1],
+ * chunk_heavy[2 * (nnz / chunk) + 2]. host_counts[0] = n_heavy, [1] = n_chunks
+ * (synchronises the stream). */
+size_t bgnn_heavy_plan_ws_bytes(int64_t n_rows);
+int bgnn_heavy_plan(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t chunk,
+                    int32_t* heavy_row, int32_t* heavy_chunk0, int32_t* chunk_heavy,
+                    void* ws, size_t ws_bytes, int32_t* host_counts, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Generic segment reduce (SpMM with a 0/1 or 1/deg matrix):
+ *   out[r, :] = REDUCE_{e in row r} x[col[e], :]
+ * H columns, row strides ldx / ldo in elements. For MEAN the sum is divided by
+ * max(deg, 1); empty rows give 0 for every reduce (PyG semantics).
+ * MAX writes the CSR position of the winning entry to arg[r, c] (first maximum
+ * in CSR order; -1 for empty rows) when arg != NULL.
+ * `partial` is scratch of n_chunks * H floats (+ n_chunks * H int32 for MAX).
+ * ---------------------------------------------------------------------- */
+int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H,
+                  int32_t reduce, float* out, int64_t ldo, int32_t* arg,
+                  float* partial, void* stream);
+
+/* Backward of bgnn_spmm_fwd through the transpose CSR (rows = sources):
+ *   SUM : gx[j] = sum_{q in rowT j} g[col_t[q]]
+ *   MEAN: gx[j] = sum_{q in rowT j} g[col_t[q]] / max(deg_fwd(col_t[q]), 1)
+ *   MAX : gx[j, c] = sum_{q in rowT j, arg[col_t[q], c] == perm_t[q]} g[col_t[q], c]
+ * `fwd_rowptr` is the forward CSR's rowptr (for MEAN degrees); `perm_t` and `arg`
+ * are needed for MAX only. Deterministic (gather form, no atomics). */
+int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                  const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                  float* gx, int64_t ldgx, float* partial, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused SAGE layer (Models/BuckGNN.py:430-444, transform-first order):
+ *   z = x · [W_l ; W_r]^T                   (bgnn_gemm_f32, [N, 2H], ld = ldz)
+ *   h_i = AGG_{j->i} z_l[j] + z_r[i] + b_l   (SUM or MEAN)
+ *   o_i = h_i / max(||h_i||_2, 1e-12)        (SAGEConv normalize=True)
+ *   BatchNorm statistics of o (train mode) as per-block partial sums.
+ * Outputs: o [N, H], nrm [N] = ||h_i||, bn_partial [n_slots, 2, H] with
+ *   n_slots = bgnn_sage_fwd_slots(N) + n_heavy.
+ * ---------------------------------------------------------------------- */
+int32_t bgnn_sage_fwd_slots(int64_t n_rows);
+int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* z, int64_t ldz, const float* bias,
+                  int32_t H, int32_t reduce, float* o, float* nrm,
+                  float* bn_partial, float* partial, void* stream);
+
+/* BatchNorm1d finalize (train): sums the partials in fp64, writes
+ *   mean[H], invstd[H], scale = gamma*invstd, shift = beta - mean*scale,
+ *   running_mean/var updated in place with `momentum` (unbiased var), as
+ *   torch.nn.BatchNorm1d does. gamma/beta may be NULL (affine=False -> 1/0).
+ * Eval mode: bgnn_bn_eval_coeffs computes scale/shift from running stats. */
+int bgnn_bn_finalize(const float* bn_partial, int32_t n_slots, int32_t H, int64_t count,
+                     const float* gamma, const float* beta, float eps, float momentum,
+                     float* running_mean, float* running_var,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+int bgnn_bn_eval_coeffs(int32_t H, const float* gamma, const float* beta, float eps,
+                        const float* running_mean, const float* running_var,
+                        float* scale, float* shift, void* stream);
+
+/* x_next = Dropout_p( ReLU(o*scale + shift) + (skip ? x_prev : 0) ).
+ * scale/shift NULL => identity (no BatchNorm, the *_Shared variant).
+ * The dropout mask is a counter-based hash of (seed, element index): keep with
+ * probability 1-p, scaled by 1/(1-p); p == 0 disables dropout. */
+int bgnn_sage_apply(const float* o, const float* scale, const float* shift,
+                    const float* x_prev, int32_t skip, float p, uint64_t seed,
+                    int64_t n_rows, int32_t H, float* x_next, void* stream);
+
+/* Backward pass 1: BatchNorm statistics of the incoming gradient g (= dL/dx_next):
+ *   g2 = relu'(o*scale+shift) * dropout'(g);  partial sums of g2 and g2*xhat. */
+int32_t bgnn_rows_slots(int64_t n_rows);
+int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, const float* shift,
+                        const float* mean, const float* invstd, float p, uint64_t seed,
+                        int64_t n_rows, int32_t H, float* partial2, void* stream);
+
+/* Reduce [n_slots, 2, H] partials (fp64) into out0[H], out1[H] (either may be NULL;
+ * accumulate=1 adds into the outputs). */
+int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
+                         float* out0, float* out1, int32_t accumulate, void* stream);
+
+/* Backward pass 2 (row-wise): BatchNorm input-gradient, then the L2-normalize
+ * backward, giving dh [N, H] (ld = lddh). If skip, writes dropout'(g) into
+ * gskip [N, H] (the skip branch's gradient, the initial value of dL/dx_prev).
+ * Partial sums of dh (for db_l) go to partial_db [slots, 2, H] (second half 0).
+ * sum_g2 / sum_g2xhat are the reduced stats of pass 1 (NULL when BatchNorm is off). */
+int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
+                       const float* scale, const float* shift, const float* gamma,
+                       const float* mean, const float* invstd,
+                       const float* sum_g2, const float* sum_g2xhat,
+                       float p, uint64_t seed, int32_t skip,
+                       int64_t n_rows, int32_t H, float* dh, int64_t lddh,
+                       float* gskip, float* partial_db, void* stream);
+
+/* ------------------------------------------------------------------------
+ * fp32 GEMM on the gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain):
+ *   C[M,N] = alpha * op(A)[M,K] · op(B)[K,N] + beta * C
+ * trans_a = 0: A is [M,K] row-major (lda >= K); 1: A is [K,M] row-major (lda >= M).
+ * trans_b = 0: B is [K,N] row-major (ldb >= N);  1: B is [N,K] row-major (ldb >= K).
+ * C is [M,N] row-major (ldc >= N). `ws` is scratch for split-K (may be NULL when
+ * bgnn_gemm_ws_bytes() returns 0 for the shape).
+ * ---------------------------------------------------------------------- */
+size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b);
+int bgnn_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                  float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
+                  float beta, float* C, int64_t ldc, void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BGNN_H */

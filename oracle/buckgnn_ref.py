@@ -1,0 +1,119 @@
+"""ORACLE (test infrastructure only): CPU restatement of BuckGNN's SAGE forward and
+train step, in functional form over a state dict with the reference's key names.
+
+Follows, line for line in meaning:
+  encoder            Models/BuckGNN.py:41-74   (h<=128: F->64->h; h>=256: F->64->128->h)
+  decoder            Models/BuckGNN.py:55-65,85-100
+  SAGE layer loops   Models/BuckGNN.py:338-352 (Shared, no BN), :389-403 (sum),
+                     :430-444 (add), :445-458 (mean), :459-471 (max)
+  pooling 'mean'     Models/BuckGNN.py:273-274 (global_mean_pool incl. super node)
+  pooling super*     Models/BuckGNN.py:248-271,277-293
+  loss               Utils/Losses.py:755-761 on Normalizer.py:207-215 denormalised values
+  step               TRAIN_FINAL.py:190 (Adam lr, wd), :253-298 (fwd, loss, zero_grad, bwd, step)
+The SAGEConv arithmetic is oracle.pyg_ref (gather -> index_add -> lin_l + lin_r -> normalize).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor
+
+from .pyg_ref import global_mean_pool, sage_aggregate
+
+SAGE = {  # model_name -> (ModuleList attribute, aggr, batchnorm)
+    "GraphSage_sumAggr": ("sage_blocks_sum", "sum", True),
+    "GraphSage_addAggr": ("sage_blocks_add", "add", True),
+    "GraphSage_meanAggr": ("sage_blocks_mean", "mean", True),
+    "GraphSage_maxAggr": ("sage_blocks_max", "max", True),
+    "GraphSage_addAggr_Shared": ("shared_graphsage_block", "add", False),
+}
+
+
+def _mlp(sd: Dict[str, Tensor], prefix: str, x: Tensor) -> Tensor:
+    idx = sorted({int(k[len(prefix) + 1:].split(".")[0]) for k in sd if k.startswith(prefix + ".")})
+    for n, i in enumerate(idx):
+        x = F.linear(x, sd[f"{prefix}.{i}.weight"], sd[f"{prefix}.{i}.bias"])
+        if n < len(idx) - 1:
+            x = F.relu(x)
+    return x
+
+
+def sage_conv(sd, pre, x, edge_index, aggr):
+    agg = sage_aggregate(x, edge_index, aggr)
+    out = F.linear(agg, sd[pre + ".lin_l.weight"], sd[pre + ".lin_l.bias"]) + F.linear(x, sd[pre + ".lin_r.weight"])
+    return F.normalize(out, p=2.0, dim=-1)
+
+
+def super_index(batch: Optional[Tensor], n: int) -> Tensor:
+    if batch is None:
+        return torch.tensor([n - 1])
+    last = [i for i in range(n - 1) if batch[i] != batch[i + 1]] + [n - 1]
+    return torch.tensor(last)
+
+
+def forward(sd: Dict[str, Tensor], model_name: str, x: Tensor, edge_index: Tensor, batch: Optional[Tensor],
+            training: bool, pooling: str = "mean", dropout: float = 0.0, num_layers: int = 6,
+            bn_momentum: float = 0.1, bn_eps: float = 1e-5, return_nodes: bool = False):
+    attr, aggr, use_bn = SAGE[model_name]
+    x = _mlp(sd, "node_encoder", x)
+    for i in range(num_layers):
+        x_prev = x
+        pre = attr if model_name.endswith("_Shared") else f"{attr}.{i}"
+        x = sage_conv(sd, pre, x, edge_index, aggr)
+        if use_bn:
+            b = f"batch_norms.{i}"
+            x = F.batch_norm(x, sd[b + ".running_mean"], sd[b + ".running_var"], sd[b + ".weight"],
+                             sd[b + ".bias"], training, bn_momentum, bn_eps)
+        x = F.relu(x)
+        if 0 < i < num_layers - 1:
+            x = x + x_prev
+        x = F.dropout(x, dropout, training)
+    nodes = x
+    if pooling == "mean":
+        pooled = global_mean_pool(x, batch)
+    else:
+        sup = super_index(batch, x.size(0))
+        keep = torch.ones(x.size(0), dtype=torch.bool)
+        keep[sup] = False
+        real = torch.nonzero(keep).flatten()
+        rb = batch[real] if batch is not None else torch.zeros(real.numel(), dtype=torch.long)
+        if pooling == "mean_no_super":
+            pooled = global_mean_pool(x[real], rb)
+        elif pooling == "supernode_only":
+            pooled = x[sup]
+        elif pooling == "supernode_with_pooling":
+            pooled = torch.cat([global_mean_pool(x[real], rb), x[sup]], 1)
+        else:
+            raise ValueError(pooling)
+    pred = _mlp(sd, "decoder", pooled).squeeze()
+    return (pred, nodes) if return_nodes else pred
+
+
+def relative_error_loss(pred: Tensor, target: Tensor, eps: float = 1e-8) -> Tensor:
+    return torch.mean(torch.abs(pred - target) / (torch.abs(target) + eps))
+
+
+class TrainStep:
+    """fwd + RelativeErrorLoss + bwd + Adam over the used parameters (CPU)."""
+
+    def __init__(self, sd: Dict[str, Tensor], model_name: str, lr: float = 1e-2, weight_decay: float = 1e-8,
+                 dropout: float = 0.1, pooling: str = "mean", num_layers: int = 6):
+        self.sd = {k: v.detach().clone() for k, v in sd.items()}
+        self.params = []
+        for k, v in self.sd.items():
+            if v.is_floating_point() and not k.endswith(("running_mean", "running_var")):
+                v.requires_grad_(True)
+                self.params.append(v)
+        self.model_name, self.dropout, self.pooling, self.num_layers = model_name, dropout, pooling, num_layers
+        self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay)
+
+    def __call__(self, x, edge_index, batch, y):
+        pred = forward(self.sd, self.model_name, x, edge_index, batch, True, self.pooling, self.dropout,
+                       self.num_layers)
+        loss = relative_error_loss(pred, y)
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()

@@ -1,0 +1,138 @@
+"""ORACLE (test infrastructure only): CPU restatement of the PyG / torch_scatter ops
+buck-gnn calls (Models/BuckGNN.py:3-6; Utils/Losses.py:4).
+
+Everything is the textbook gather -> scatter formulation PyG's MessagePassing
+uses on the CPU: messages x_j = x.index_select(0, edge_index[0]) and an
+index_add_ / scatter_reduce_ into edge_index[1]. No fused or reordered math.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+
+# ----------------------------------------------------------------------------- scatter
+def scatter(src: Tensor, index: Tensor, dim_size: int, reduce: str) -> Tensor:
+    """Segment reduce along dim 0 (torch_scatter / PyG utils.scatter semantics):
+    sum, mean (sum / max(count, 1)), max (empty segments -> 0)."""
+    out_shape = (dim_size,) + tuple(src.shape[1:])
+    if reduce in ("sum", "add"):
+        return src.new_zeros(out_shape).index_add_(0, index, src)
+    if reduce == "mean":
+        s = src.new_zeros(out_shape).index_add_(0, index, src)
+        cnt = torch.zeros(dim_size, dtype=src.dtype).index_add_(0, index, torch.ones(index.numel(), dtype=src.dtype))
+        return s / cnt.clamp_min(1).view(-1, *([1] * (src.dim() - 1)))
+    if reduce == "max":
+        idx = index.view(-1, *([1] * (src.dim() - 1))).expand_as(src)
+        return src.new_zeros(out_shape).scatter_reduce_(0, idx, src, reduce="amax", include_self=False)
+    raise ValueError(reduce)
+
+
+def scatter_add(src, index, dim=0, out=None, dim_size=None):
+    n = dim_size if dim_size is not None else (int(index.max()) + 1 if index.numel() else 0)
+    return scatter(src, index, n, "sum")
+
+
+def scatter_mean(src, index, dim=0, out=None, dim_size=None):
+    n = dim_size if dim_size is not None else (int(index.max()) + 1 if index.numel() else 0)
+    return scatter(src, index, n, "mean")
+
+
+# ----------------------------------------------------------------------------- pooling
+def _pool(x: Tensor, batch: Optional[Tensor], size: Optional[int], reduce: str) -> Tensor:
+    if batch is None:
+        kd = x.dim() == 2
+        if reduce == "mean":
+            return x.mean(dim=-2, keepdim=kd)
+        if reduce == "sum":
+            return x.sum(dim=-2, keepdim=kd)
+        return x.max(dim=-2, keepdim=kd)[0]
+    n = size if size is not None else (int(batch.max()) + 1 if batch.numel() else 0)
+    return scatter(x, batch, n, reduce)
+
+
+def global_mean_pool(x, batch, size=None):
+    return _pool(x, batch, size, "mean")
+
+
+def global_add_pool(x, batch, size=None):
+    return _pool(x, batch, size, "sum")
+
+
+def global_max_pool(x, batch, size=None):
+    return _pool(x, batch, size, "max")
+
+
+# ----------------------------------------------------------------------------- SAGEConv
+class Linear(nn.Linear):
+    def reset_parameters(self):
+        bound = math.sqrt(6.0 / (6.0 * self.in_features)) if self.in_features else 0.0
+        with torch.no_grad():
+            self.weight.uniform_(-bound, bound)
+            if self.bias is not None:
+                b = 1.0 / math.sqrt(self.in_features) if self.in_features else 0.0
+                self.bias.uniform_(-b, b)
+
+
+def sage_aggregate(x: Tensor, edge_index: Tensor, aggr: str) -> Tensor:
+    """AGG_{j: (j -> i)} x_j with j = edge_index[0], i = edge_index[1]."""
+    msg = x.index_select(0, edge_index[0])
+    return scatter(msg, edge_index[1], x.size(0), "sum" if aggr == "add" else aggr)
+
+
+class SAGEConv(nn.Module):
+    def __init__(self, in_channels, out_channels, aggr="mean", normalize=False, root_weight=True,
+                 project=False, bias=True, **kw):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.aggr, self.normalize, self.root_weight, self.project = aggr, normalize, root_weight, project
+        if project:
+            self.lin = Linear(in_channels, in_channels, bias=True)
+        self.lin_l = Linear(in_channels, out_channels, bias=bias)
+        if root_weight:
+            self.lin_r = Linear(in_channels, out_channels, bias=False)
+
+    def forward(self, x, edge_index, size=None):
+        x_src = x
+        if self.project:
+            x_src = F.relu(self.lin(x_src))
+        out = self.lin_l(sage_aggregate(x_src, edge_index, self.aggr))
+        if self.root_weight:
+            out = out + self.lin_r(x)
+        if self.normalize:
+            out = F.normalize(out, p=2.0, dim=-1)
+        return out
+
+
+class SAGPooling(nn.Module):
+    def __init__(self, *a, **k):
+        super().__init__()
+        raise NotImplementedError("SAGPooling is outside the oracle's scope")
+
+
+# ----------------------------------------------------------------------------- batching
+class Data:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def collate(graphs: Sequence[dict]) -> dict:
+    """PyG Batch.from_data_list restated: x/edge_attr/y concatenated, edge_index offset
+    by the running node count, batch = graph id per node."""
+    xs, eis, eas, ys, bs = [], [], [], [], []
+    off = 0
+    for g, d in enumerate(graphs):
+        n = d["x"].shape[0]
+        xs.append(torch.as_tensor(d["x"]))
+        eis.append(torch.as_tensor(d["edge_index"]) + off)
+        if d.get("edge_attr") is not None:
+            eas.append(torch.as_tensor(d["edge_attr"]))
+        ys.append(torch.as_tensor(d["y"]).reshape(-1))
+        bs.append(torch.full((n,), g, dtype=torch.long))
+        off += n
+    return {"x": torch.cat(xs), "edge_index": torch.cat(eis, 1),
+            "edge_attr": torch.cat(eas) if eas else None, "y": torch.cat(ys), "batch": torch.cat(bs)}

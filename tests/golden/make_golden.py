@@ -1,0 +1,142 @@
+#!/usr/bin/env python
+"""Generate tests/golden/*.npz from the REFERENCE's own Models/BuckGNN.py.
+
+Runs only in the build container, where /root/reference exists. The reference
+model class is imported unchanged; the third-party ops it imports
+(torch_geometric.nn.SAGEConv, global_mean_pool, torch_scatter.scatter_mean, ...)
+are supplied by the oracle's CPU restatement (oracle/shim.py), because PyG is not
+installed. Nothing from /root/reference is written into the
+repository: each fixture holds only data — inputs, the weight-recipe seed, and the
+reference's outputs (prediction, loss, gradients or gradient checksums, BatchNorm
+running statistics, pooled features, eval-mode prediction).
+
+    python tests/golden/make_golden.py [--out tests/golden]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+sys.path.insert(0, HERE)
+
+from recipe import grad_checksum, make_weights, meta_to_array  # noqa: E402
+
+CASES = [
+    # name, model_name, hidden, pooling, graphs [(n, super_node, seed)], full_grads
+    ("add_h64", "GraphSage_addAggr", 64, "mean", [(5, False, 1), (6, False, 2), (4, False, 3)], True),
+    ("sum_h64", "GraphSage_sumAggr", 64, "mean", [(5, False, 1), (6, False, 2), (4, False, 3)], True),
+    ("mean_h64", "GraphSage_meanAggr", 64, "mean", [(5, False, 1), (6, False, 2), (4, False, 3)], True),
+    ("max_h64", "GraphSage_maxAggr", 64, "mean", [(5, False, 1), (6, False, 2), (4, False, 3)], True),
+    ("shared_h64", "GraphSage_addAggr_Shared", 64, "mean", [(5, False, 1), (6, False, 2), (4, False, 3)], True),
+    ("add_super_h64", "GraphSage_addAggr", 64, "mean", [(5, True, 4), (7, True, 5)], True),
+    ("add_super_nosuper_h64", "GraphSage_addAggr", 64, "mean_no_super", [(5, True, 4), (7, True, 5)], True),
+    ("add_super_only_h64", "GraphSage_addAggr", 64, "supernode_only", [(5, True, 4), (7, True, 5)], True),
+    ("add_super_withpool_h64", "GraphSage_addAggr", 64, "supernode_with_pooling", [(5, True, 4), (7, True, 5)],
+     True),
+    ("add_single_h64", "GraphSage_addAggr", 64, "mean", [(6, False, 7)], True),
+    ("add_super_h512", "GraphSage_addAggr", 512, "mean", [(5, True, 8), (4, True, 9)], False),
+    ("mean_h512", "GraphSage_meanAggr", 512, "mean", [(5, False, 10), (4, False, 11)], False),
+    ("shared_h512", "GraphSage_addAggr_Shared", 512, "mean", [(6, False, 12)], False),
+    ("add_h256", "GraphSage_addAggr", 256, "mean", [(5, False, 13), (5, True, 14)], False),
+    ("ea_gnn_h64", "EA_GNN", 64, "mean", [(4, False, 15), (5, False, 16)], False),
+]
+
+
+def build_inputs(graphs):
+    from bgnn.synthetic import make_mesh_graph
+    from oracle.pyg_ref import collate
+
+    ds = []
+    for n, sup, seed in graphs:
+        d = make_mesh_graph(n, seed, super_node=sup)
+        ds.append({"x": d.x.numpy(), "edge_index": d.edge_index.numpy(), "edge_attr": d.edge_attr.numpy(),
+                   "y": d.y.numpy()})
+    return collate(ds)
+
+
+def run_case(BuckGNN, case):
+    name, model_name, h, pooling, graphs, full = case
+    torch.manual_seed(0)
+    model = BuckGNN(num_node_features=16, num_edge_features=5, hidden_channels=h, num_layers=6,
+                    pooling_layer=pooling, prediction_type="buckling", dropout_rate=0.0, model_name=model_name)
+    sd = model.state_dict()
+    shapes = {k: tuple(v.shape) for k, v in sd.items()}
+    seed = 1000 + h
+    w = make_weights(shapes, seed)
+    model.load_state_dict({k: torch.from_numpy(w[k]) if k in w else sd[k] for k in sd})
+    b = build_inputs(graphs)
+    single = len(graphs) == 1
+    batch = None if single else b["batch"]
+    captured = {}
+    model.decoder.register_forward_pre_hook(lambda m, inp: captured.__setitem__("pooled", inp[0].detach().clone()))
+    model.train()
+    pred, _ = model(b["x"], b["edge_index"], b["edge_attr"], batch)
+    y = b["y"] if not single else b["y"][0]
+    loss = torch.mean(torch.abs(pred - y) / (torch.abs(y) + 1e-8))   # RelativeErrorLoss, Losses.py:755-761
+    model.zero_grad(set_to_none=True)
+    loss.backward()
+    out = {
+        "meta": meta_to_array({"name": name, "model_name": model_name, "hidden": h, "pooling": pooling,
+                               "weight_seed": seed, "num_layers": 6, "single_graph": single,
+                               "graphs": graphs}),
+        "x": b["x"].numpy(), "edge_index": b["edge_index"].numpy(), "edge_attr": b["edge_attr"].numpy(),
+        "batch": b["batch"].numpy(), "y": b["y"].numpy(),
+        "pred_train": pred.detach().numpy().reshape(-1), "loss_train": np.array(loss.item()),
+        "pooled_train": captured["pooled"].numpy(),
+    }
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.numpy()
+        if full:
+            out["grad/" + k] = g
+        else:
+            out["gradsum/" + k] = grad_checksum(g)
+    for k, v in model.state_dict().items():
+        if "running_" in k:
+            out["state/" + k] = v.numpy()
+    model.eval()
+    with torch.no_grad():
+        pe, _ = model(b["x"], b["edge_index"], b["edge_attr"], batch)
+    out["pred_eval"] = pe.numpy().reshape(-1)
+    out["pooled_eval"] = captured["pooled"].numpy()
+    return name, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=HERE)
+    args = ap.parse_args()
+    if not os.path.isdir(os.path.join(REF, "Models")):
+        print("reference not present; nothing to do")
+        return 0
+    from oracle import shim
+    shim.install()
+    sys.path.insert(0, REF)
+    try:
+        from Models.BuckGNN import BuckGNN  # the reference's model class, unchanged
+    finally:
+        sys.path.remove(REF)
+    total = 0
+    for case in CASES:
+        name, out = run_case(BuckGNN, case)
+        path = os.path.join(args.out, f"{name}.npz")
+        np.savez_compressed(path, **out)
+        total += os.path.getsize(path)
+        print(f"{name}: pred={out['pred_train']} loss={float(out['loss_train']):.6f} -> {path}")
+    print(f"total fixture bytes: {total}")
+    shim.uninstall()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,98 @@
+"""GPU: the fused SAGE layer (bgnn.fused.SageLayerFn) against the CPU oracle
+composition SAGEConv(normalize) -> BatchNorm1d -> ReLU -> skip -> Dropout
+(Models/BuckGNN.py:430-444), forward and every gradient."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from bgnn import fused
+from bgnn.graph import Graph
+from bgnn import synthetic as S
+from oracle import pyg_ref as P
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-4, atol=1e-4)
+
+
+def make_params(H, seed):
+    g = torch.Generator().manual_seed(seed)
+    return dict(
+        w_l=torch.randn(H, H, generator=g) / H ** 0.5, b_l=0.1 * torch.randn(H, generator=g),
+        w_r=torch.randn(H, H, generator=g) / H ** 0.5, gamma=1 + 0.1 * torch.randn(H, generator=g),
+        beta=0.1 * torch.randn(H, generator=g), rm=0.1 * torch.randn(H, generator=g),
+        rv=1 + 0.2 * torch.rand(H, generator=g))
+
+
+def oracle_layer(x, ei, p, aggr, bn, training, skip, mask=None, keep_scale=1.0):
+    t = {k: v.double().clone().requires_grad_(k not in ("rm", "rv")) for k, v in p.items()}
+    xc = x.double().clone().requires_grad_(True)
+    agg = P.sage_aggregate(xc, ei, aggr)
+    h = agg @ t["w_l"].t() + t["b_l"] + xc @ t["w_r"].t()
+    o = F.normalize(h, p=2.0, dim=-1)
+    if bn:
+        o = F.batch_norm(o, t["rm"], t["rv"], t["gamma"], t["beta"], training, 0.1, 1e-5)
+    y = F.relu(o)
+    if skip:
+        y = y + xc
+    if mask is not None:
+        y = y * mask.double() * keep_scale
+    return y, xc, t
+
+
+@pytest.mark.parametrize("aggr,red", [("sum", 0), ("mean", 1)])
+@pytest.mark.parametrize("bn,training", [(True, True), (True, False), (False, True)])
+@pytest.mark.parametrize("skip", [False, True])
+@pytest.mark.parametrize("H", [64, 512])
+def test_fused_layer_matches_oracle(dev, aggr, red, bn, training, skip, H):
+    b = S.make_batch(9, 3, super_node=True)
+    n = b.num_nodes
+    torch.manual_seed(H)
+    x = torch.randn(n, H)
+    p = make_params(H, 7)
+    graph = Graph.build(b.edge_index.to(dev), n, chunk=16)
+    d = {k: v.to(dev).requires_grad_(k not in ("rm", "rv")) for k, v in p.items()}
+    rm, rv = d["rm"].detach().clone(), d["rv"].detach().clone()
+    xd = x.to(dev).requires_grad_(True)
+    cfg = fused.LayerConfig(red, bn, training, 0.1, 1e-5, skip, 0.0, 123)
+    out = fused.SageLayerFn.apply(xd, d["w_l"], d["b_l"], d["w_r"], d["gamma"] if bn else None,
+                                  d["beta"] if bn else None, rm if bn else None, rv if bn else None, graph, cfg)
+    up = torch.randn_like(out)
+    out.backward(up)
+    ro, xc, t = oracle_layer(x, b.edge_index, p, aggr, bn, training, skip)
+    ro.backward(up.cpu().double())
+    torch.testing.assert_close(out.detach().cpu(), ro.float(), **TOL)
+    torch.testing.assert_close(xd.grad.cpu(), xc.grad.float(), **TOL)
+    for k in ("w_l", "b_l", "w_r") + (("gamma", "beta") if bn else ()):
+        torch.testing.assert_close(d[k].grad.cpu(), t[k].grad.float(), **TOL, msg=k)
+    if bn and training:
+        torch.testing.assert_close(rm.cpu(), t["rm"].detach().float(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(rv.cpu(), t["rv"].detach().float(), rtol=1e-5, atol=1e-6)
+
+
+def test_dropout_mask_fraction_and_backward_consistency(dev):
+    H = 512
+    b = S.make_batch(12, 2)
+    n = b.num_nodes
+    torch.manual_seed(0)
+    x = torch.randn(n, H)
+    p = make_params(H, 3)
+    graph = Graph.build(b.edge_index.to(dev), n)
+    d = {k: v.to(dev).requires_grad_(k not in ("rm", "rv")) for k, v in p.items()}
+    xd = x.to(dev).requires_grad_(True)
+    drop = 0.25
+    cfg = fused.LayerConfig(0, True, True, 0.1, 1e-5, True, drop, 987654321)
+    out = fused.SageLayerFn.apply(xd, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"], d["rm"].detach().clone(),
+                                  d["rv"].detach().clone(), graph, cfg)
+    y0, _, _ = oracle_layer(x, b.edge_index, p, "sum", True, True, True)
+    keep = out.detach().cpu() != 0
+    nz = y0.detach().abs() > 1e-6
+    frac = 1 - keep[nz].float().mean().item()
+    assert abs(frac - drop) < 0.01, frac
+    torch.testing.assert_close(out.detach().cpu()[keep], (y0.detach()[keep] / (1 - drop)).float(), **TOL)
+    up = torch.randn_like(out)
+    out.backward(up)
+    ro, xc, t = oracle_layer(x, b.edge_index, p, "sum", True, True, True, mask=keep, keep_scale=1 / (1 - drop))
+    ro.backward(up.cpu().double())
+    torch.testing.assert_close(xd.grad.cpu(), xc.grad.float(), **TOL)
+    torch.testing.assert_close(d["w_l"].grad.cpu(), t["w_l"].grad.float(), **TOL)

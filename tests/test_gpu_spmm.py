@@ -1,0 +1,125 @@
+"""GPU: neighbour aggregation (sum/mean/max, forward + backward), pooling and scatter
+against the CPU oracle (oracle.pyg_ref). Tolerance 1e-4 abs/rel in fp32 (BASELINE north star)."""
+import numpy as np
+import pytest
+import torch
+
+import bgnn
+from bgnn.graph import Graph, SegmentIndex
+from bgnn import synthetic as S
+from oracle import pyg_ref as P
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-4, atol=1e-4)
+
+
+def oracle_agg(x, ei, reduce, g):
+    xc = x.detach().cpu().double().requires_grad_(True)
+    out = P.sage_aggregate(xc, ei.cpu(), reduce)
+    out.backward(g.cpu().double())
+    return out.float(), xc.grad.float()
+
+
+def run_agg(x, ei, n, reduce, chunk, dev):
+    g = Graph.build(ei.to(dev), n, chunk=chunk)
+    xd = x.to(dev).requires_grad_(True)
+    out = bgnn.aggregate(xd, g, reduce)
+    up = torch.randn_like(out)
+    out.backward(up)
+    ro, rg = oracle_agg(x, ei, reduce, up)
+    torch.testing.assert_close(out.detach().cpu(), ro, **TOL)
+    torch.testing.assert_close(xd.grad.cpu(), rg, **TOL)
+
+
+GRAPHS = {
+    "mesh": lambda: S.make_batch(12, 2),
+    "super": lambda: S.make_batch(15, 2, super_node=True),
+}
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("H", [1, 3, 16, 64, 100, 128, 256, 512, 700, 1024])
+def test_aggregate_matches_oracle_random_graph(dev, reduce, H):
+    torch.manual_seed(H)
+    n, E = 257, 3000
+    ei = torch.randint(0, n, (2, E))
+    x = torch.randn(n, H)
+    run_agg(x, ei, n, reduce, chunk=16, dev=dev)
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("kind", ["mesh", "super"])
+@pytest.mark.parametrize("chunk", [4, 64])
+def test_aggregate_meshes(dev, reduce, kind, chunk):
+    b = GRAPHS[kind]()
+    torch.manual_seed(1)
+    x = torch.randn(b.num_nodes, 512)
+    run_agg(x, b.edge_index, b.num_nodes, reduce, chunk, dev)
+
+
+def test_aggregate_is_deterministic(dev):
+    b = S.make_batch(30, 2, super_node=True)
+    g = Graph.build(b.edge_index.to(dev), b.num_nodes, chunk=16)
+    x = torch.randn(b.num_nodes, 512, device=dev)
+    a1 = bgnn.aggregate(x, g, "sum")
+    a2 = bgnn.aggregate(x, g, "sum")
+    assert torch.equal(a1, a2)
+
+
+def test_aggregate_empty_graph_gives_zero(dev):
+    g = Graph.build(torch.zeros(2, 0, dtype=torch.long, device=dev), 5)
+    for r in ("sum", "mean", "max"):
+        assert torch.equal(bgnn.aggregate(torch.randn(5, 8, device=dev), g, r), torch.zeros(5, 8, device=dev))
+
+
+@pytest.mark.parametrize("reduce", ["mean", "sum", "max"])
+def test_global_pool_matches_oracle(dev, reduce):
+    torch.manual_seed(0)
+    batch = torch.tensor([0] * 40 + [1] * 300 + [3] * 7)     # graph 2 empty
+    x = torch.randn(batch.numel(), 512)
+    fn = {"mean": bgnn.global_mean_pool, "sum": bgnn.global_add_pool, "max": bgnn.global_max_pool}[reduce]
+    rf = {"mean": P.global_mean_pool, "sum": P.global_add_pool, "max": P.global_max_pool}[reduce]
+    xd = x.to(dev).requires_grad_(True)
+    out = fn(xd, batch.to(dev))
+    up = torch.randn_like(out)
+    out.backward(up)
+    xc = x.double().requires_grad_(True)
+    ro = rf(xc, batch)
+    ro.backward(up.cpu().double())
+    torch.testing.assert_close(out.detach().cpu(), ro.float(), **TOL)
+    torch.testing.assert_close(xd.grad.cpu(), xc.grad.float(), **TOL)
+
+
+def test_scatter_unsorted_index(dev):
+    torch.manual_seed(0)
+    idx = torch.randint(0, 9, (500,))
+    src = torch.randn(500, 33)
+    for fn, rf in ((bgnn.scatter_mean, P.scatter_mean), (bgnn.scatter_add, P.scatter_add)):
+        out = fn(src.to(dev), idx.to(dev), dim=0, dim_size=12)
+        torch.testing.assert_close(out.cpu(), rf(src, idx, dim_size=12), **TOL)
+
+
+def test_full_size_cfg3_properties(dev):
+    """Full cfg3 batch (super nodes of in-degree 5,041): sum aggregation is linear and
+    its transpose is the adjoint: <A x, y> == <x, A^T y> (size-independent checks)."""
+    b = S.make_config_batch("cfg3")
+    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    assert g.fwd.plan.n_heavy == 16
+    torch.manual_seed(0)
+    x = torch.randn(b.num_nodes, 512, device=dev, dtype=torch.float32)
+    y = torch.randn(b.num_nodes, 512, device=dev, dtype=torch.float32)
+    ax = bgnn.aggregate(x, g, "sum")
+    ax2 = bgnn.aggregate(2 * x, g, "sum")
+    torch.testing.assert_close(ax2, 2 * ax, rtol=0, atol=0)
+    xd = x.clone().requires_grad_(True)
+    bgnn.aggregate(xd, g, "sum").backward(y)
+    lhs = (ax.double() * y.double()).sum()
+    rhs = (x.double() * xd.grad.double()).sum()
+    assert abs(float(lhs - rhs)) <= 1e-6 * float(ax.double().abs().sum() * y.double().abs().max())
+    # super node rows against an independent fp64 torch sum
+    s = b.ptr[1:] - 1
+    ei = b.edge_index.to(dev)
+    for r in s[:2].tolist():
+        nb = ei[0][ei[1] == r]
+        ref = x.double()[nb].sum(0)
+        torch.testing.assert_close(ax[r].double(), ref, rtol=1e-5, atol=1e-4)

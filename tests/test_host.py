@@ -1,0 +1,119 @@
+"""Host-side logic (CPU only): synthetic inputs, PyG-compatible containers and
+collation, the PyG shim, BuckGNN module/state-dict layout, and 'no CPU fallback'."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import bgnn
+from bgnn import synthetic as S
+from oracle import pyg_ref as P
+
+REF = "/root/reference"
+
+
+def test_mesh_config_sizes_match_survey():
+    # per-graph node/edge counts of cfg1/cfg2/cfg3
+    g1 = S.make_mesh_graph(45, 0)
+    assert (g1.num_nodes, g1.num_edges) == (2025, 17752)
+    g2 = S.make_mesh_graph(71, 0)
+    assert (g2.num_nodes, g2.num_edges) == (5041, 44742)
+    g3 = S.make_mesh_graph(71, 0, super_node=True)
+    assert (g3.num_nodes, g3.num_edges) == (5042, 49562)
+
+
+def test_mesh_graph_structure():
+    g = S.make_mesh_graph(6, 3)
+    ei = g.edge_index.numpy()
+    # both directions, interleaved (GraphCreate.py:420-422)
+    assert np.array_equal(ei[0, 0::2], ei[1, 1::2]) and np.array_equal(ei[1, 0::2], ei[0, 1::2])
+    pairs = {tuple(sorted(p)) for p in ei.T.tolist()}
+    assert len(pairs) * 2 == ei.shape[1]            # no duplicate undirected edges
+    assert all(a != b for a, b in pairs)            # no self loops
+    assert g.x.shape == (36, 16) and float(g.x[:, -1].abs().sum()) == 0.0
+    assert g.edge_attr.shape == (ei.shape[1], 5)
+    gs = S.make_mesh_graph(6, 3, super_node=True)
+    s = gs.num_nodes - 1
+    deg_s = int((gs.edge_index[1] == s).sum())
+    assert deg_s == 36 and float(gs.x[s, -1]) == 1.0
+
+
+def test_batch_collation_matches_oracle():
+    ds = [S.make_mesh_graph(n, seed) for n, seed in ((4, 1), (5, 2), (3, 3))]
+    b = bgnn.Batch.from_data_list(ds)
+    ref = P.collate([{"x": d.x, "edge_index": d.edge_index, "edge_attr": d.edge_attr, "y": d.y} for d in ds])
+    for k in ("x", "edge_index", "edge_attr", "y", "batch"):
+        assert torch.equal(getattr(b, k), ref[k]), k
+    assert b.num_graphs == 3 and b.ptr.tolist() == [0, 16, 41, 50]
+    assert b.num_node_features == 16 and b.num_edge_features == 5
+    loader = bgnn.DataLoader(ds, batch_size=2, shuffle=False)
+    batches = list(loader)
+    assert [bb.num_graphs for bb in batches] == [2, 1]
+
+
+def test_data_attributes_and_clone():
+    d = bgnn.Data(x=torch.zeros(3, 2), edge_index=torch.tensor([[0], [1]]), file_path="a.bdf",
+                  mode_shapes=torch.ones(3, 3))
+    c = d.clone()
+    c.x[0, 0] = 5
+    assert float(d.x[0, 0]) == 0.0
+    assert d.file_path == "a.bdf" and d.num_nodes == 3 and d.edge_attr is None
+    b = bgnn.Batch.from_data_list([d, d])
+    assert b.file_path == ["a.bdf", "a.bdf"] and b.mode_shapes.shape == (6, 3)
+
+
+@pytest.mark.parametrize("fn", [
+    lambda: bgnn.aggregate(torch.zeros(3, 4), None),
+    lambda: bgnn.Graph.build(torch.zeros(2, 3, dtype=torch.long), 3),
+    lambda: bgnn.SAGEConv(4, 4, aggr="sum")(torch.zeros(3, 4), torch.zeros(2, 3, dtype=torch.long)),
+    lambda: bgnn.global_mean_pool(torch.zeros(3, 4), torch.zeros(3, dtype=torch.long)),
+])
+def test_no_cpu_fallback(fn):
+    with pytest.raises((RuntimeError, AttributeError)):
+        fn()
+
+
+VARIANTS = ["GraphSage_addAggr", "GraphSage_sumAggr", "GraphSage_meanAggr", "GraphSage_maxAggr",
+            "GraphSage_addAggr_Shared", "EA_GNN", "EA_GNN_Shared", "GraphSAGE_MLP"]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference not present")
+@pytest.mark.parametrize("hidden", [64, 512])
+@pytest.mark.parametrize("name", VARIANTS)
+def test_state_dict_layout_matches_reference(name, hidden):
+    """The reference's BuckGNN (imported unchanged through bgnn's PyG shim) and bgnn.BuckGNN
+    have identical state-dict keys and shapes, so checkpoints load both ways."""
+    bgnn.install_pyg_shim()
+    sys.path.insert(0, REF)
+    try:
+        from Models.BuckGNN import BuckGNN as RefBuckGNN
+    finally:
+        sys.path.remove(REF)
+    kw = dict(hidden_channels=hidden, num_layers=6, pooling_layer="mean", dropout_rate=0.1, model_name=name)
+    ref = RefBuckGNN(16, 5, **kw).state_dict()
+    mine = bgnn.BuckGNN(16, 5, **kw).state_dict()
+    assert list(ref.keys()) == list(mine.keys())
+    for k in ref:
+        assert ref[k].shape == mine[k].shape, k
+    bgnn.BuckGNN(16, 5, **kw).load_state_dict(ref)
+    bgnn.uninstall_pyg_shim()
+
+
+def test_reference_defects_reproduced():
+    m = bgnn.BuckGNN(16, 5, hidden_channels=64, model_name="GraphSage_MLP")
+    with pytest.raises(AttributeError):
+        m(torch.zeros(4, 16), torch.zeros(2, 0, dtype=torch.long), None)
+    # hidden in (128, 256): no encoder is built (Models/BuckGNN.py:41,67)
+    m2 = bgnn.BuckGNN(16, 5, hidden_channels=192, model_name="GraphSage_addAggr")
+    assert not hasattr(m2, "node_encoder")
+
+
+def test_super_node_index_vectorised():
+    from bgnn.buckgnn import super_node_index
+    from oracle.buckgnn_ref import super_index
+
+    b = torch.tensor([0, 0, 0, 1, 1, 2, 2, 2, 2])
+    assert super_node_index(b, 9, "cpu").tolist() == super_index(b, 9).tolist() == [2, 4, 8]
+    assert super_node_index(None, 5, "cpu").tolist() == [4]
