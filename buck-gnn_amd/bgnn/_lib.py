@@ -47,6 +47,7 @@ class CsrStruct(ctypes.Structure):
 SIGNATURES = {
     "bgnn_abi_version": (c_i32, []),
     "bgnn_last_error_string": (ctypes.c_char_p, []),
+    "bgnn_set_tuning": (c_i32, [c_i32, c_i32]),
     "bgnn_graph_build_ws_bytes": (c_sz, [c_i64, c_i64]),
     "bgnn_graph_build": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p]),
     "bgnn_index_csr_build": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_sz, c_p, c_p]),
@@ -67,6 +68,7 @@ SIGNATURES = {
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
                                    c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
+    "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,
                               c_p, c_sz, c_p]),
 }

@@ -31,108 +31,114 @@ struct GemmArgs {
     int split;
 };
 
-constexpr int GBM = 128, GBN = 128, GBK = 16;
-
-template <int T>  // T = 1: operand is K-contiguous in global memory (needs transpose into LDS)
-struct OpLayout {
-    static constexpr int PAD = T ? 2 : 4;
+// LDS row pad (floats): a K-contiguous operand is transposed by scalar ds_write_b32
+// into a [BK][R + PAD] image; PAD is chosen so one wave's 32-lane store groups hit 32
+// distinct banks (4*(R+PAD) = 8 mod 32 for BK = 16, 4 mod 32 for BK = 32). An
+// R-contiguous operand is stored as float4 rows, kept 16-B aligned.
+template <int KCONTIG, int BK>
+struct Pad {
+    static constexpr int value = KCONTIG ? (BK == 16 ? 2 : 1) : 4;
 };
 
-// Load one BK x 128 slice of an operand into registers (2 float4 per thread).
+// Load one BK x R slice of an operand into registers (NL float4 per thread).
 //   KCONTIG = 1: element (r, k) at P[r * ld + k]  (r = m or n, k contiguous)
 //   KCONTIG = 0: element (r, k) at P[k * ld + r]  (r contiguous)
-template <int KCONTIG>
-__device__ __forceinline__ void load_slice(const float* __restrict__ P, int64_t ld, int64_t R, int64_t r0,
-                                           int64_t k0, int64_t kend, bool vec_ok, float (&reg)[2][4]) {
+template <int KCONTIG, int R, int BK>
+__device__ __forceinline__ void load_slice(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0,
+                                           int64_t k0, int64_t kend, bool vec_ok, float (&reg)[R * BK / 1024][4]) {
+    constexpr int NL = R * BK / 1024;
     const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NL; ++i) {
         const int idx = t + 256 * i;
         if constexpr (KCONTIG) {
-            const int r = idx >> 2, kq = idx & 3;
+            const int r = idx / (BK / 4), kq = idx % (BK / 4);
             const int64_t gr = r0 + r, gk = k0 + kq * 4;
-            if (vec_ok && gr < R && gk + 3 < kend) {
+            if (vec_ok && gr < Rlim && gk + 3 < kend) {
                 const float4 v = *reinterpret_cast<const float4*>(P + gr * ld + gk);
                 reg[i][0] = v.x; reg[i][1] = v.y; reg[i][2] = v.z; reg[i][3] = v.w;
             } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    reg[i][q] = (gr < R && gk + q < kend) ? P[gr * ld + gk + q] : 0.f;
+                for (int q = 0; q < 4; ++q) reg[i][q] = (gr < Rlim && gk + q < kend) ? P[gr * ld + gk + q] : 0.f;
             }
         } else {
-            const int kr = idx >> 5, rq = idx & 31;
+            const int kr = idx / (R / 4), rq = idx % (R / 4);
             const int64_t gk = k0 + kr, gr = r0 + rq * 4;
-            if (vec_ok && gk < kend && gr + 3 < R) {
+            if (vec_ok && gk < kend && gr + 3 < Rlim) {
                 const float4 v = *reinterpret_cast<const float4*>(P + gk * ld + gr);
                 reg[i][0] = v.x; reg[i][1] = v.y; reg[i][2] = v.z; reg[i][3] = v.w;
             } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    reg[i][q] = (gk < kend && gr + q < R) ? P[gk * ld + gr + q] : 0.f;
+                for (int q = 0; q < 4; ++q) reg[i][q] = (gk < kend && gr + q < Rlim) ? P[gk * ld + gr + q] : 0.f;
             }
         }
     }
 }
 
-template <int KCONTIG, int LDS_LD>
-__device__ __forceinline__ void store_slice(float* __restrict__ S, const float (&reg)[2][4]) {
+template <int KCONTIG, int R, int BK, int LDS_LD>
+__device__ __forceinline__ void store_slice(float* __restrict__ S, const float (&reg)[R * BK / 1024][4]) {
+    constexpr int NL = R * BK / 1024;
     const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NL; ++i) {
         const int idx = t + 256 * i;
         if constexpr (KCONTIG) {
-            const int r = idx >> 2, kq = idx & 3;
+            const int r = idx / (BK / 4), kq = idx % (BK / 4);
 #pragma unroll
             for (int q = 0; q < 4; ++q) S[(kq * 4 + q) * LDS_LD + r] = reg[i][q];
         } else {
-            const int kr = idx >> 5, rq = idx & 31;
+            const int kr = idx / (R / 4), rq = idx % (R / 4);
             *reinterpret_cast<float4*>(S + kr * LDS_LD + rq * 4) =
                 make_float4(reg[i][0], reg[i][1], reg[i][2], reg[i][3]);
         }
     }
 }
 
+// C tile BM x BN per 256-thread workgroup; the 4 waves form a WM x WN grid, each wave
+// owns (BM/WM) x (BN/WN) = TM x TN MFMA tiles of 32x32.
 // TA: 0 -> A is [M,K] (K-contiguous), 1 -> A is [K,M].
 // TB: 0 -> B is [K,N] (N-contiguous), 1 -> B is [N,K] (K-contiguous).
-template <int TA, int TB>
+template <int TA, int TB, int BM, int BN, int BK, int WM, int WN>
 __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
+    static_assert(WM * WN == 4, "4 waves per workgroup");
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
-    constexpr int LDA_S = GBM + OpLayout<AK>::PAD;
-    constexpr int LDB_S = GBN + OpLayout<BKc>::PAD;
-    __shared__ __attribute__((aligned(16))) float As[2][GBK * LDA_S];
-    __shared__ __attribute__((aligned(16))) float Bs[2][GBK * LDB_S];
+    constexpr int LDA_S = BM + Pad<AK, BK>::value;
+    constexpr int LDB_S = BN + Pad<BKc, BK>::value;
+    __shared__ __attribute__((aligned(16))) float As[2][BK * LDA_S];
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK * LDB_S];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int64_t ntn = (g.N + GBN - 1) / GBN;
-    const int64_t ntm = (g.M + GBM - 1) / GBM;
+    const int wm = wave / WN, wn = wave % WN;
+    const int64_t ntn = (g.N + BN - 1) / BN;
+    const int64_t ntm = (g.M + BM - 1) / BM;
     const int tiles = (int)(ntm * ntn);
     const int lt = xcd_remap(blockIdx.x, tiles);
     const int64_t tm = lt / ntn, tn = lt % ntn;
-    const int64_t m0 = tm * GBM, n0 = tn * GBN;
+    const int64_t m0 = tm * BM, n0 = tn * BN;
     const int64_t kb = (int64_t)blockIdx.y * g.kchunk;
     const int64_t ke = min(g.K, kb + g.kchunk);
 
     const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % 4 == 0);
     const bool b_vec = (((uintptr_t)g.B & 15) == 0) && (g.ldb % 4 == 0);
 
-    floatx16 acc[2][2];
+    floatx16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float ra[2][4], rb[2][4];
-    const int64_t nk = (ke > kb) ? (ke - kb + GBK - 1) / GBK : 0;
+    float ra[BM * BK / 1024][4], rb[BN * BK / 1024][4];
+    const int64_t nk = (ke > kb) ? (ke - kb + BK - 1) / BK : 0;
     if (nk > 0) {
-        load_slice<AK>(g.A, g.lda, g.M, m0, kb, ke, a_vec, ra);
-        load_slice<BKc>(g.B, g.ldb, g.N, n0, kb, ke, b_vec, rb);
-        store_slice<AK, LDA_S>(As[0], ra);
-        store_slice<BKc, LDB_S>(Bs[0], rb);
+        load_slice<AK, BM, BK>(g.A, g.lda, g.M, m0, kb, ke, a_vec, ra);
+        load_slice<BKc, BN, BK>(g.B, g.ldb, g.N, n0, kb, ke, b_vec, rb);
+        store_slice<AK, BM, BK, LDA_S>(As[0], ra);
+        store_slice<BKc, BN, BK, LDB_S>(Bs[0], rb);
     }
     __syncthreads();
 
@@ -141,27 +147,29 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
         const int cur = kt & 1;
         const bool more = kt + 1 < nk;
         if (more) {
-            const int64_t k0 = kb + (kt + 1) * GBK;
-            load_slice<AK>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
-            load_slice<BKc>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
+            const int64_t k0 = kb + (kt + 1) * BK;
+            load_slice<AK, BM, BK>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
+            load_slice<BKc, BN, BK>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
         }
-        const float* as = As[cur];
-        const float* bs = Bs[cur];
+        const float* as = As[cur] + wm * (BM / WM) + li;
+        const float* bs = Bs[cur] + wn * (BN / WN) + li;
 #pragma unroll
-        for (int kk = 0; kk < GBK / 2; ++kk) {
+        for (int kk = 0; kk < BK / 2; ++kk) {
             const int kr = 2 * kk + lk;
-            const float a0 = as[kr * LDA_S + wm * 64 + li];
-            const float a1 = as[kr * LDA_S + wm * 64 + 32 + li];
-            const float b0 = bs[kr * LDB_S + wn * 64 + li];
-            const float b1 = bs[kr * LDB_S + wn * 64 + 32 + li];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            float a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) a[i] = as[kr * LDA_S + i * 32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b[j] = bs[kr * LDB_S + j * 32];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         if (more) {
-            store_slice<AK, LDA_S>(As[cur ^ 1], ra);
-            store_slice<BKc, LDB_S>(Bs[cur ^ 1], rb);
+            store_slice<AK, BM, BK, LDA_S>(As[cur ^ 1], ra);
+            store_slice<BKc, BN, BK, LDB_S>(Bs[cur ^ 1], rb);
         }
         __syncthreads();
     }
@@ -170,14 +178,14 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
     float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)blockIdx.y * g.M * g.N : g.C;
     const int64_t ldd = g.split > 1 ? g.N : g.ldc;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int64_t col = n0 + wn * 64 + j * 32 + li;
+        for (int j = 0; j < TN; ++j) {
+            const int64_t col = n0 + wn * (BN / WN) + j * 32 + li;
             if (col >= g.N) continue;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+                const int64_t row = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
                 if (row >= g.M) continue;
                 float v = acc[i][j][r];
                 if (g.split > 1) {
@@ -206,8 +214,23 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
     }
 }
 
-inline int choose_split(int64_t M, int64_t N, int64_t K) {
-    const int64_t tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+struct GemmCfg {
+    int bm, bn, bk;
+};
+// tile configurations (index = BGNN_TUNE_GEMM_CFG value)
+constexpr GemmCfg kCfgs[] = {{128, 128, 16}, {128, 128, 32}, {256, 128, 16}, {128, 256, 16}};
+constexpr int kNumCfgs = 4;
+static int g_gemm_cfg = -1;   // -1 = automatic
+
+inline int pick_cfg(int64_t M, int64_t N, int64_t K, int ta, int tb) {
+    (void)K; (void)ta; (void)tb;
+    if (g_gemm_cfg >= 0) return g_gemm_cfg;
+    (void)M; (void)N;
+    return 0;
+}
+
+inline int choose_split(int64_t M, int64_t N, int64_t K, const GemmCfg& c) {
+    const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     if (tiles >= 512 || K < 4 * 256) return 1;
     int64_t s = (1024 + tiles - 1) / tiles;
     const int64_t smax = K / 256;   // keep >= 256 of K per slice
@@ -216,13 +239,28 @@ inline int choose_split(int64_t M, int64_t N, int64_t K) {
     return s < 1 ? 1 : (int)s;
 }
 
+template <int TA, int TB>
+void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    switch (cfg) {
+        case 1: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 128, 32, 2, 2>), grid, dim3(256), 0, s, g); break;
+        case 2: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
+        case 3: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
+        default: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 128, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
+    }
+}
+
 }  // namespace bgnn
 
 using namespace bgnn;
 
+extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
+    BGNN_REQUIRE(cfg >= -1 && cfg < kNumCfgs, "gemm: config %d out of range", cfg);
+    g_gemm_cfg = cfg;
+    return BGNN_OK;
+}
+
 extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb) {
-    (void)ta; (void)tb;
-    const int s = choose_split(M, N, K);
+    const int s = choose_split(M, N, K, kCfgs[pick_cfg(M, N, K, ta, tb)]);
     return s > 1 ? (size_t)s * (size_t)M * (size_t)N * sizeof(float) : 0;
 }
 
@@ -235,23 +273,22 @@ extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64
     BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm: bad ldb");
     BGNN_REQUIRE(ldc >= N || M == 0, "gemm: bad ldc");
     if (M == 0 || N == 0) return BGNN_OK;
-    const int64_t tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+    const int cfg = pick_cfg(M, N, K, ta, tb);
+    const GemmCfg& c = kCfgs[cfg];
+    const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
     hipStream_t s = as_stream(stream);
-    int split = choose_split(M, N, K);
+    int split = choose_split(M, N, K, c);
     if (split > 1 && (ws == nullptr || ws_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
     GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split};
     int64_t kc = (K + split - 1) / split;
-    kc = (kc + GBK - 1) / GBK * GBK;
-    g.kchunk = kc > 0 ? kc : GBK;
+    kc = (kc + c.bk - 1) / c.bk * c.bk;
+    g.kchunk = kc > 0 ? kc : c.bk;
     dim3 grid((unsigned)tiles, split);
-#define BGNN_G(TA, TB)                                                                          \
-    if (ta == TA && tb == TB) hipLaunchKernelGGL((k_gemm_f32<TA, TB>), grid, dim3(256), 0, s, g);
-    BGNN_G(0, 0)
-    BGNN_G(0, 1)
-    BGNN_G(1, 0)
-    BGNN_G(1, 1)
-#undef BGNN_G
+    if (ta == 0 && tb == 0) launch_cfg<0, 0>(cfg, grid, s, g);
+    else if (ta == 0 && tb == 1) launch_cfg<0, 1>(cfg, grid, s, g);
+    else if (ta == 1 && tb == 0) launch_cfg<1, 0>(cfg, grid, s, g);
+    else launch_cfg<1, 1>(cfg, grid, s, g);
     BGNN_CHECK_LAUNCH();
     if (split > 1) {
         int64_t blocks = (M * N + 255) / 256;

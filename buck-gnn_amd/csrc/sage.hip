@@ -21,16 +21,48 @@ inline int64_t rows_grid(int64_t n_rows, int rows_per_block_min, int64_t* rpb) {
 }
 
 // ---------------------------------------------------------------------------
-// Reduce [n_slots, 2, H] partials; one thread per (channel, slot-phase).
-__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int n_slots, int H,
-                                                         float* __restrict__ out0, float* __restrict__ out1,
+// Stage 1 of every partial-slot reduction: [n_slots, 2H] -> kGroups group sums,
+// written IN PLACE into the first slot of each group's range (a thread reads its
+// whole column range before writing that column, and no other thread touches it).
+// Coalesced: a block covers 256 consecutive of the 2H columns for one group.
+constexpr int kGroups = 16;
+
+__global__ __launch_bounds__(256) void k_slots_stage1(float* __restrict__ part, int n_slots, int W, int per) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    const int g = blockIdx.y;
+    if (c >= W) return;
+    const int s0 = g * per, s1 = min(n_slots, s0 + per);
+    if (s0 >= s1) return;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int s = s0;
+    for (; s + 8 <= s1; s += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(s + u) * W + c];
+    }
+    for (; s < s1; ++s) acc[0] += part[(int64_t)s * W + c];
+    part[(int64_t)s0 * W + c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// Launch stage 1; returns the slot stride the stage-2 kernels must use.
+inline int slots_stage1(float* part, int n_slots, int H, hipStream_t s) {
+    if (n_slots <= kGroups) return 1;
+    const int per = (n_slots + kGroups - 1) / kGroups;
+    hipLaunchKernelGGL(k_slots_stage1, dim3((2 * H + 255) / 256, kGroups), dim3(256), 0, s, part, n_slots, 2 * H,
+                       per);
+    return per;
+}
+
+// ---------------------------------------------------------------------------
+// Reduce [n_slots, 2, H] partials (slots taken every `stride`); one thread per (channel, slot-phase).
+__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int n_slots, int stride,
+                                                         int H, float* __restrict__ out0, float* __restrict__ out1,
                                                          int accumulate) {
     __shared__ double red[4][2][64];
     const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
     double s0 = 0.0, s1 = 0.0;
     if (c < H)
-        for (int sl = ph; sl < n_slots; sl += 4) {
+        for (int sl = ph * stride; sl < n_slots; sl += 4 * stride) {
             s0 += (double)part[(int64_t)sl * 2 * H + c];
             s1 += (double)part[(int64_t)sl * 2 * H + H + c];
         }
@@ -47,7 +79,7 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
 
 // BatchNorm1d finalize (train mode), torch semantics: biased var for
 // normalisation, unbiased var for running_var, momentum update.
-__global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ part, int n_slots, int H,
+__global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ part, int n_slots, int stride, int H,
                                                      int64_t count, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps, float momentum,
                                                      float* __restrict__ rmean, float* __restrict__ rvar,
@@ -58,7 +90,7 @@ __global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ p
     const int c = blockIdx.x * 64 + cl;
     double s0 = 0.0, s1 = 0.0;
     if (c < H)
-        for (int sl = ph; sl < n_slots; sl += 4) {
+        for (int sl = ph * stride; sl < n_slots; sl += 4 * stride) {
             s0 += (double)part[(int64_t)sl * 2 * H + c];
             s1 += (double)part[(int64_t)sl * 2 * H + H + c];
         }
@@ -320,8 +352,10 @@ extern "C" int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32
                                     int32_t accumulate, void* stream) {
     BGNN_REQUIRE(partial && H > 0 && n_slots >= 0, "reduce_partials: bad args");
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(k_reduce_partials, dim3((H + 63) / 64), dim3(256), 0, s, partial, n_slots, H, out0, out1,
-                       accumulate);
+    const int stride = slots_stage1(const_cast<float*>(partial), n_slots, H, s);
+    BGNN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_reduce_partials, dim3((H + 63) / 64), dim3(256), 0, s, partial, n_slots, stride, H, out0,
+                       out1, accumulate);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
@@ -332,8 +366,10 @@ extern "C" int bgnn_bn_finalize(const float* bn_partial, int32_t n_slots, int32_
                                 float* shift, void* stream) {
     BGNN_REQUIRE(bn_partial && H > 0 && count > 0 && mean && invstd && scale && shift, "bn_finalize: bad args");
     hipStream_t s = as_stream(stream);
-    hipLaunchKernelGGL(k_bn_finalize, dim3((H + 63) / 64), dim3(256), 0, s, bn_partial, n_slots, H, count, gamma,
-                       beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+    const int stride = slots_stage1(const_cast<float*>(bn_partial), n_slots, H, s);
+    BGNN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_bn_finalize, dim3((H + 63) / 64), dim3(256), 0, s, bn_partial, n_slots, stride, H, count,
+                       gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

@@ -418,7 +418,195 @@ __global__ __launch_bounds__(64) void k_seg_combine(SegArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// XCD sweep kernel (one full row per wave, LPR = 64, VEC = 4): the production
+// light-row kernel for H >= 256.
+//
+// Row assignment: the grid (a multiple of 8 blocks) is split into the 8 groups
+// of blocks that share an XCD under round-robin dispatch (b % 8). Group x owns
+// the contiguous row region [x*N/8, (x+1)*N/8) and its 4*G/8 waves sweep that
+// region together: wave q takes rows lo + q, lo + q + W, lo + q + 2W, ... So at
+// any moment an XCD works on a ~W-row front and its mesh neighbourhood
+// (±n rows), which stays in that XCD's 4 MiB L2, instead of G/8 scattered row
+// ranges whose union far exceeds it. (Placement affects speed only.)
+//
+// Latency: rowptr of all rows of a wave is fetched with one vector load (lane l
+// holds row t0+l); a row's col indices are one vector load (lane k = k-th
+// neighbour, deg <= chunk <= 64) issued one row ahead; up to U neighbours are
+// gathered in a single batch, so a light row costs about one memory round trip.
+struct Sweep {
+    int64_t lo, first;
+    int W, T;
+};
+
+__device__ __forceinline__ Sweep sweep_rows(int64_t n_rows, int wave) {
+    Sweep s;
+    const int G = gridDim.x;                 // multiple of 8
+    const int x = blockIdx.x & 7, i = blockIdx.x >> 3;
+    const int64_t lo = n_rows * x / kNumXcd, hi = n_rows * (x + 1) / kNumXcd;
+    s.W = 4 * (G >> 3);
+    s.lo = lo;
+    s.first = lo + i * 4 + wave;
+    s.T = s.first < hi ? (int)((hi - s.first + s.W - 1) / s.W) : 0;
+    return s;
+}
+
+template <int NV, int OP, int U>
+__device__ __forceinline__ void sweep_gather(const SegArgs& A, Acc<4, NV, OP>& acc, int32_t cur, int32_t beg,
+                                             int32_t deg, int32_t e0, const int (&cpos)[NV], const bool (&cok)[NV]) {
+    const int nvalid = min(U, deg - e0);
+    int32_t j[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int slot = (u < nvalid) ? e0 + u : e0;   // masked slots re-read the first row (L1 hit)
+        j[u] = __builtin_amdgcn_readlane(cur, slot);
+        w[u] = 1.f;
+        if constexpr (OP == OP_MEANT) {
+            const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
+            w[u] = 1.f / (float)(d > 0 ? d : 1);
+        }
+    }
+    Vec<4> val[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) val[u][v] = ld<4>(A.x + (int64_t)j[u] * A.ldx + (cok[v] ? cpos[v] : 0));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool ok = u < nvalid;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if constexpr (OP == OP_MAXT) {
+                int32_t ga[4];
+                ldi<4>(A.arg_in + (int64_t)j[u] * A.H + (cok[v] ? cpos[v] : 0), ga);
+                const int32_t pe = A.perm_t[beg + e0 + (ok ? u : 0)];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc.a[v][k] += (ok && ga[k] == pe) ? val[u][v].f[k] : 0.f;
+            } else if constexpr (OP == OP_MAX) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool better = ok && (val[u][v].f[k] > acc.a[v][k]);
+                    acc.a[v][k] = better ? val[u][v].f[k] : acc.a[v][k];
+                    acc.g[v][k] = better ? (beg + e0 + u) : acc.g[v][k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc.a[v][k] += ok ? val[u][v].f[k] * w[u] : 0.f;
+            }
+        }
+    }
+}
+
+template <int NV, int OP, int EPI, int U>
+__global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Sweep sw = sweep_rows(A.n_rows, wave);
+    const int cb = blockIdx.y * (64 * 4 * NV);
+    int cpos[NV];
+    bool cok[NV];
+    lane_cols<4, NV, 64>(cb, lane, A.H, cpos, cok);
+    float bs[NV][4], bq[NV][4];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bs[v][k] = bq[v][k] = 0.f;
+    Vec<4> bias[NV];
+    if constexpr (EPI == EPI_SAGE) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) bias[v] = ld<4>(A.bias + (cok[v] ? cpos[v] : 0));
+    }
+    const int32_t chunk = A.chunk;
+
+    for (int t0 = 0; t0 < sw.T; t0 += 64) {
+        const int nrow = min(64, sw.T - t0);
+        int32_t rp_lo = 0, rp_hi = 0;
+        if (lane < nrow) {
+            const int64_t rl = sw.first + (int64_t)sw.W * (t0 + lane);
+            rp_lo = A.rowptr[rl];
+            rp_hi = A.rowptr[rl + 1];
+        }
+        int32_t nb = __builtin_amdgcn_readlane(rp_lo, 0), ndeg = __builtin_amdgcn_readlane(rp_hi, 0) - nb;
+        int32_t cv = (lane < ndeg && ndeg <= chunk) ? A.col[nb + lane] : 0;
+        for (int k = 0; k < nrow; ++k) {
+            const int64_t r = sw.first + (int64_t)sw.W * (t0 + k);
+            const int32_t beg = nb, deg = ndeg;
+            const int32_t cur = cv;
+            if (k + 1 < nrow) {   // prefetch the next row's neighbour list
+                nb = __builtin_amdgcn_readlane(rp_lo, k + 1);
+                ndeg = __builtin_amdgcn_readlane(rp_hi, k + 1) - nb;
+                cv = (lane < ndeg && ndeg <= chunk) ? A.col[nb + lane] : 0;
+            }
+            if (deg > chunk) continue;   // heavy row: k_seg_chunk + k_seg_combine
+            Acc<4, NV, OP> acc;
+            acc.init();
+            Vec<4> zr[NV];
+            if (deg > 0) sweep_gather<NV, OP, U>(A, acc, cur, beg, deg, 0, cpos, cok);
+            if constexpr (EPI == EPI_SAGE) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) zr[v] = ld<4>(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
+            }
+            for (int e0 = U; e0 < deg; e0 += U) sweep_gather<NV, OP, U>(A, acc, cur, beg, deg, e0, cpos, cok);
+            if constexpr (EPI == EPI_SAGE) {
+                const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
+                float h[NV][4];
+                float ss = 0.f;
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        h[v][q] = cok[v] ? acc.a[v][q] * sc + zr[v].f[q] + bias[v].f[q] : 0.f;
+                        ss += h[v][q] * h[v][q];
+                    }
+                ss = group_sum(ss, kWave);
+                const float n = sqrtf(ss);
+                const float d = fmaxf(n, 1e-12f);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    if (!cok[v]) continue;
+                    Vec<4> o;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        o.f[q] = h[v][q] / d;
+                        bs[v][q] += o.f[q];
+                        bq[v][q] += o.f[q] * o.f[q];
+                    }
+                    st<4>(A.out + r * A.ldo + cpos[v], o);
+                }
+                if (lane == 0) A.nrm[r] = n;
+            } else {
+                store_plain<4, NV, OP>(A, acc, r, deg, cpos, cok);
+            }
+        }
+    }
+
+    if constexpr (EPI == EPI_SAGE) {
+        __shared__ __attribute__((aligned(16))) float red[4][2][512];
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (cok[v])
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    red[wave][0][cpos[v] + k] = bs[v][k];
+                    red[wave][1][cpos[v] + k] = bq[v][k];
+                }
+        __syncthreads();
+        float* dst = A.bn_partial + (int64_t)blockIdx.x * 2 * A.H;
+        for (int c = threadIdx.x; c < A.H; c += 256) {
+            dst[c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+            dst[A.H + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 constexpr int kMaxLightBlocks = 1024;
+
+// Tuning knobs (process-wide; defaults are the production choice; see bgnn_set_tuning).
+static int g_seg_kernel = 0;     // 0 = sweep kernel where applicable, 1 = blocked kernel
+static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
+static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto:
+                                 // 8 with the SAGE epilogue (register-bound), 12 otherwise)
 
 struct Geometry {
     int vec, nv, lpr, ctiles;
@@ -457,16 +645,47 @@ inline int64_t light_grid(int64_t n_rows, int rows_per_wave, int max_blocks, int
     return blocks;
 }
 
+inline int64_t sweep_grid(int64_t n_rows) {
+    int64_t want = (n_rows + 3) / 4;                 // at most one row per wave
+    int64_t blocks = g_seg_blocks;
+    if (want < blocks) blocks = want;
+    blocks = (blocks + 7) / 8 * 8;
+    return blocks < 8 ? 8 : blocks;
+}
+
 template <int VEC, int NV, int LPR, int OP, int EPI>
 int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* blocks_out) {
     int64_t rpb = 0;
-    const int64_t blocks = light_grid(A.n_rows, kWave / LPR, max_blocks, &rpb);
+    // the sweep kernel needs one row per wave and every light row's list in one vector load
+    const bool sweep = (VEC == 4 && LPR == 64 && g_seg_kernel == 0 && A.chunk <= 64);
+    int64_t blocks;
+    if (sweep || EPI == EPI_SAGE) {   // SAGE: slot count = bgnn_sage_fwd_slots() for either kernel
+        blocks = sweep_grid(A.n_rows);
+        rpb = (A.n_rows + blocks - 1) / blocks;
+    } else {
+        blocks = light_grid(A.n_rows, kWave / LPR, max_blocks, &rpb);
+    }
     A.rows_per_block = rpb;
     if (blocks_out) *blocks_out = blocks;
     A.light_slots = (int32_t)blocks;
     if (A.n_rows > 0) {
-        hipLaunchKernelGGL((k_seg_light<VEC, NV, LPR, OP, EPI>), dim3((unsigned)blocks, ctiles), dim3(256),
-                           0, s, A);
+        if constexpr (VEC == 4 && LPR == 64) {
+            if (sweep) {
+                const int u = g_seg_u ? g_seg_u : (EPI == EPI_SAGE ? 8 : 12);
+                if (u == 8)
+                    hipLaunchKernelGGL((k_seg_sweep<NV, OP, EPI, 8>), dim3((unsigned)blocks, ctiles), dim3(256), 0,
+                                       s, A);
+                else
+                    hipLaunchKernelGGL((k_seg_sweep<NV, OP, EPI, 12>), dim3((unsigned)blocks, ctiles), dim3(256), 0,
+                                       s, A);
+            } else {
+                hipLaunchKernelGGL((k_seg_light<VEC, NV, LPR, OP, EPI>), dim3((unsigned)blocks, ctiles), dim3(256),
+                                   0, s, A);
+            }
+        } else {
+            hipLaunchKernelGGL((k_seg_light<VEC, NV, LPR, OP, EPI>), dim3((unsigned)blocks, ctiles), dim3(256), 0,
+                               s, A);
+        }
         BGNN_CHECK_LAUNCH();
     }
     if (A.n_chunks > 0) {
@@ -570,9 +789,21 @@ extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, con
     }
 }
 
-extern "C" int32_t bgnn_sage_fwd_slots(int64_t n_rows) {
-    int64_t rpb = 0;
-    return (int32_t)light_grid(n_rows, 1, kMaxLightBlocks, &rpb);
+extern "C" int32_t bgnn_sage_fwd_slots(int64_t n_rows) { return (int32_t)sweep_grid(n_rows); }
+
+extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
+    switch (knob) {
+        case BGNN_TUNE_SEG_KERNEL: g_seg_kernel = value ? 1 : 0; return BGNN_OK;
+        case BGNN_TUNE_SEG_BLOCKS:
+            BGNN_REQUIRE(value >= 8 && value <= 65536, "set_tuning: blocks out of range");
+            g_seg_blocks = value;
+            return BGNN_OK;
+        case BGNN_TUNE_SEG_U:
+            BGNN_REQUIRE(value == 0 || value == 8 || value == 12, "set_tuning: U must be 0 (auto), 8 or 12");
+            g_seg_u = value;
+            return BGNN_OK;
+        default: return fail(BGNN_E_ARG, "set_tuning: unknown knob %d", knob);
+    }
 }
 
 extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* z, int64_t ldz, const float* bias, int32_t H,

@@ -54,6 +54,14 @@ extern "C" {
 int bgnn_abi_version(void);
 const char* bgnn_last_error_string(void);
 
+/* Process-wide tuning knobs for A/B measurement (tools/, tests). The defaults are
+ * the production choice; results are identical for every setting, only speed
+ * changes. Not thread-safe against concurrent launches. */
+#define BGNN_TUNE_SEG_KERNEL 1   /* 0 = XCD-sweep light-row kernel (default), 1 = blocked */
+#define BGNN_TUNE_SEG_BLOCKS 2   /* sweep grid in blocks (default 1024)                   */
+#define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (default), 8, 12 */
+int bgnn_set_tuning(int32_t knob, int32_t value);
+
 /* ------------------------------------------------------------------------
  * Graph structure. A CSR over destination rows plus the split plan for rows
  * whose in-degree exceeds `chunk` (super nodes: VirtualEdgeCreate.py:106-111).
@@ -171,7 +179,8 @@ int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, cons
                         int64_t n_rows, int32_t H, float* partial2, void* stream);
 
 /* Reduce [n_slots, 2, H] partials (fp64) into out0[H], out1[H] (either may be NULL;
- * accumulate=1 adds into the outputs). */
+ * accumulate=1 adds into the outputs). The partial buffer is used as scratch and
+ * its contents are undefined afterwards (also for bgnn_bn_finalize). */
 int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
                          float* out0, float* out1, int32_t accumulate, void* stream);
 
@@ -197,6 +206,9 @@ int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
  * bgnn_gemm_ws_bytes() returns 0 for the shape).
  * ---------------------------------------------------------------------- */
 size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b);
+/* Force a tile configuration (tuning/tests; -1 = automatic, the default). Results are
+ * identical up to the split-K partition; only speed changes. */
+int bgnn_gemm_set_cfg(int32_t cfg);
 int bgnn_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
                   float beta, float* C, int64_t ldc, void* ws, size_t ws_bytes, void* stream);

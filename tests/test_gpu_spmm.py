@@ -123,3 +123,22 @@ def test_full_size_cfg3_properties(dev):
         nb = ei[0][ei[1] == r]
         ref = x.double()[nb].sum(0)
         torch.testing.assert_close(ax[r].double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("knobs", [(1, 0), (0, 8), (0, 12)], ids=["blocked", "sweep8", "sweep12"])
+def test_kernel_variants_bit_identical(dev, knobs):
+    """Every light-row kernel variant (tuning knobs) gives bit-identical aggregation results."""
+    from bgnn import _lib
+    b = S.make_batch(25, 3, super_node=True)
+    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    torch.manual_seed(3)
+    x = torch.randn(b.num_nodes, 512, device=dev)
+    ref = {r: bgnn.aggregate(x, g, r) for r in ("sum", "mean", "max")}
+    try:
+        _lib.call("bgnn_set_tuning", 1, knobs[0])
+        _lib.call("bgnn_set_tuning", 3, knobs[1])
+        for r in ("sum", "mean", "max"):
+            assert torch.equal(bgnn.aggregate(x, g, r), ref[r]), r
+    finally:
+        _lib.call("bgnn_set_tuning", 1, 0)
+        _lib.call("bgnn_set_tuning", 3, 0)

@@ -1,0 +1,106 @@
+#!/usr/bin/env python
+"""A/B the aggregation kernel variants on cfg2/cfg3 in ONE process (interleaved rounds,
+median of per-launch HIP-event times), checking that every variant gives bit-identical
+results. Usage: python tools/tune_agg.py [--config cfg2] [--rounds 20]"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+
+import torch  # noqa: E402
+
+from bgnn import _lib, synthetic  # noqa: E402
+from bgnn.graph import Graph  # noqa: E402
+
+KNOB = {"kernel": 1, "blocks": 2, "u": 3}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--variants", default="blocked,sweep8,sweep12,sweep12_b2048,sweep8_b2048,sweep12_b512")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    b = synthetic.make_config_batch(args.config)
+    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    N, E, H = b.num_nodes, b.num_edges, 512
+    torch.manual_seed(0)
+    z = torch.randn(N, 2 * H, device=dev)
+    bias = torch.randn(H, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def set_variant(v):
+        kern, u, blocks = 0, 12, 1024
+        if v == "blocked":
+            kern = 1
+        else:
+            parts = v.split("_")
+            u = int(parts[0][5:])
+            if len(parts) > 1:
+                blocks = int(parts[1][1:])
+        _lib.call("bgnn_set_tuning", KNOB["kernel"], kern)
+        _lib.call("bgnn_set_tuning", KNOB["u"], u)
+        _lib.call("bgnn_set_tuning", KNOB["blocks"], blocks)
+
+    def run_fwd():
+        slots = _lib.query("bgnn_sage_fwd_slots", N) + g.fwd.plan.n_heavy
+        o = torch.empty(N, H, device=dev)
+        nrm = torch.empty(N, device=dev)
+        bnp = torch.empty(slots, 2, H, device=dev)
+        part = torch.empty(max(g.fwd.plan.n_chunks, 1) * H, device=dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.call("bgnn_sage_fwd", g.fwd.ref(), z.data_ptr(), z.stride(0), bias.data_ptr(), H, 0, o.data_ptr(),
+                  nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
+        e1.record()
+        return (e0, e1), (o, nrm, bnp.sum(0))
+
+    def run_bwd():
+        gx = torch.empty(N, 2 * H, device=dev)
+        part = torch.empty(max(g.bwd.plan.n_chunks, 1) * H, device=dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _lib.call("bgnn_spmm_bwd", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), z[:, H:].data_ptr(),
+                  z.stride(0), H, 0, None, gx.data_ptr(), gx.stride(0), part.data_ptr(), s)
+        e1.record()
+        return (e0, e1), (gx[:, :H],)
+
+    variants = args.variants.split(",")
+    times = {(v, k): [] for v in variants for k in ("fwd", "bwd")}
+    ref = {}
+    for rnd in range(args.rounds + 2):
+        for v in variants:
+            set_variant(v)
+            for k, fn in (("fwd", run_fwd), ("bwd", run_bwd)):
+                ev, outs = fn()
+                torch.cuda.synchronize()
+                if rnd >= 2:
+                    times[(v, k)].append(ev[0].elapsed_time(ev[1]))
+                if rnd == 0:
+                    if k not in ref:
+                        ref[k] = [t.clone() for t in outs]
+                    else:
+                        for a, bb in zip(ref[k], outs):
+                            if not torch.equal(a, bb):
+                                print(f"MISMATCH {v} {k}: max diff {(a - bb).abs().max().item()}")
+    set_variant("sweep12")
+    fwd_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
+    bwd_bytes = 2 * N * H * 4 + 4 * E + 4 * (N + 1)
+    res = {}
+    for v in variants:
+        f = statistics.median(times[(v, "fwd")])
+        bw = statistics.median(times[(v, "bwd")])
+        res[v] = {"fwd_us": round(f * 1e3, 1), "fwd_GBs": round(fwd_bytes / f / 1e6, 1),
+                  "bwd_us": round(bw * 1e3, 1), "bwd_GBs": round(bwd_bytes / bw / 1e6, 1)}
+        print(f"{v:16s} fwd {f*1e3:8.1f} us {fwd_bytes/f/1e6:8.1f} GB/s | bwd {bw*1e3:8.1f} us "
+              f"{bwd_bytes/bw/1e6:8.1f} GB/s")
+    print(json.dumps({"config": args.config, "N": N, "E": E, "results": res}))
+
+
+if __name__ == "__main__":
+    main()
