@@ -20,7 +20,7 @@ from typing import Optional
 import torch
 from torch import Tensor, nn
 
-from .fused import sage_layer
+from .fused import mlp, sage_layer
 from .graph import Graph, SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
@@ -225,7 +225,10 @@ class BuckGNN(nn.Module):
             is_real_node = x[:, -1] == 0 if x.size(1) > 0 else torch.ones(x.size(0), dtype=torch.bool,
                                                                            device=x.device)
             real_node_batch = batch[is_real_node] if batch is not None else None
-        x = self.node_encoder(x)
+        if self._fused_ok(x) and x.size(0) >= 1024:
+            x = mlp(self.node_encoder, x)        # encoder GEMMs with fused bias+ReLU epilogues
+        else:
+            x = self.node_encoder(x)
         if name == "EA_GNN_Shared":
             e = self.edge_encoder(edge_attr)
             for i in range(self.num_layers):

@@ -52,8 +52,8 @@ class _timed:
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool, trans_b: bool, out: torch.Tensor = None,
-         beta: float = 0.0, alpha: float = 1.0) -> torch.Tensor:
-    """C = alpha * op(a) @ op(b) + beta * C (fp32, row-major operands, unit column stride)."""
+         beta: float = 0.0, alpha: float = 1.0, bias: torch.Tensor = None, relu: bool = False) -> torch.Tensor:
+    """C = act(alpha * op(a) @ op(b) + beta * C + bias) (fp32, row-major operands, unit column stride)."""
     M = a.size(1) if trans_a else a.size(0)
     K = a.size(0) if trans_a else a.size(1)
     N = b.size(0) if trans_b else b.size(1)
@@ -72,16 +72,67 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool, trans_b: bool, out: to
                 out.mul_(alpha)
         else:
             out.mul_(beta).addmm_(ra, rb, alpha=alpha)
+        if bias is not None:
+            out.add_(bias)
+        if relu:
+            out.relu_()
         return out
     for t, nm in ((a, "A"), (b, "B"), (out, "C")):
         if t.stride(1) != 1:
             raise ValueError(f"gemm: {nm} must have unit column stride")
     ws_bytes = _lib.query("bgnn_gemm_ws_bytes", M, N, K, int(trans_a), int(trans_b))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=a.device) if ws_bytes else None
-    _lib.call("bgnn_gemm_f32", int(trans_a), int(trans_b), M, N, K, float(alpha), a.data_ptr(), a.stride(0),
+    _lib.call("bgnn_gemm_f32_ex", int(trans_a), int(trans_b), M, N, K, float(alpha), a.data_ptr(), a.stride(0),
               b.data_ptr(), b.stride(0), float(beta), out.data_ptr(), out.stride(0),
-              None if ws is None else ws.data_ptr(), ws_bytes, _stream())
+              None if bias is None else bias.data_ptr(), int(relu), None if ws is None else ws.data_ptr(),
+              ws_bytes, _stream())
     return out
+
+
+class LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b) on bgnn_gemm_f32_ex (bias + ReLU fused in the GEMM epilogue);
+    backward: dgrad and wgrad GEMMs on the same kernel (Models/BuckGNN.py:67-74 encoder)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu: bool):
+        x = x.contiguous()
+        y = gemm(x, weight.contiguous(), trans_a=False, trans_b=True, bias=bias, relu=relu)
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device))
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, y = ctx.saved_tensors
+        g = g.contiguous()
+        if ctx.relu:
+            g = g * (y > 0)
+        dx = gemm(g, weight.contiguous(), trans_a=False, trans_b=False) if ctx.needs_input_grad[0] else None
+        dw = gemm(g, x, trans_a=True, trans_b=False)
+        db = g.sum(0) if ctx.has_bias else None
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, relu: bool = False) -> torch.Tensor:
+    return LinearFn.apply(x, weight, bias, relu)
+
+
+def mlp(seq: torch.nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """Run an nn.Sequential of Linear/ReLU through bgnn GEMMs, fusing each ReLU into the
+    preceding Linear's epilogue (same parameters, same result as seq(x))."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, torch.nn.Linear):
+            fuse = i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.ReLU)
+            x = linear(x, m.weight, m.bias, fuse)
+            i += 2 if fuse else 1
+        else:
+            x = m(x)
+            i += 1
+    return x
 
 
 def _ptr(t):

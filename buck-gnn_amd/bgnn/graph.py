@@ -134,6 +134,7 @@ class SegmentIndex:
     num_rows: int
     fwd: Csr          # rows = segments (graphs), col = positions
     bwd: Csr          # rows = positions, exactly one entry: its segment
+    index: Optional[torch.Tensor] = field(default=None, repr=False)   # int64 [n]
 
     @staticmethod
     def build(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK,
@@ -158,7 +159,7 @@ class SegmentIndex:
         empty = Plan(torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
                      torch.zeros(1, dtype=torch.int32, device=dev), 0, 0, chunk)
         bwd = Csr(rowptr_t, col_t if n > 0 else torch.zeros(1, dtype=torch.int32, device=dev), n, n, empty)
-        return SegmentIndex(n, R, fwd, bwd)
+        return SegmentIndex(n, R, fwd, bwd, idx)
 
 
 class _Cache:

@@ -105,7 +105,13 @@ class _SegmentReduce(torch.autograd.Function):
             slot = torch.empty(seg.n, dtype=torch.int32, device=g.device)
             slot[seg.fwd.col[:seg.n].long()] = torch.arange(seg.n, dtype=torch.int32, device=g.device)
             return spmm_bwd(seg.bwd, slot, seg.fwd.rowptr, g, 2, arg, seg.n), None, None
-        return spmm_bwd(seg.bwd, None, seg.fwd.rowptr, g, r, None, seg.n), None, None
+        # sum / mean: every position receives its segment's gradient row (a broadcast;
+        # one HBM write of the output, no gather structure needed)
+        g = g.contiguous()
+        if r == 1:
+            cnt = seg.fwd.degree().clamp_min(1).to(g.dtype)
+            g = g / cnt.unsqueeze(1)
+        return g.index_select(0, seg.index), None, None
 
 
 def segment_reduce(src: torch.Tensor, seg: SegmentIndex, reduce: str = "sum") -> torch.Tensor:

@@ -29,6 +29,8 @@ struct GemmArgs {
     float alpha, beta;
     int64_t kchunk;   // K range per split-K slice (multiple of BK)
     int split;
+    const float* bias;   // epilogue: + bias[col] (may be NULL)
+    int relu;            // epilogue: max(., 0)
 };
 
 // LDS row pad (floats): a K-contiguous operand is transposed by scalar ds_write_b32
@@ -43,15 +45,21 @@ struct Pad {
 // Load one BK x R slice of an operand into registers (NL float4 per thread).
 //   KCONTIG = 1: element (r, k) at P[r * ld + k]  (r = m or n, k contiguous)
 //   KCONTIG = 0: element (r, k) at P[k * ld + r]  (r contiguous)
-template <int KCONTIG, int R, int BK>
+template <int KCONTIG, int R, int BK, int NT, bool FULL = false>
 __device__ __forceinline__ void load_slice(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0,
-                                           int64_t k0, int64_t kend, bool vec_ok, float (&reg)[R * BK / 1024][4]) {
-    constexpr int NL = R * BK / 1024;
+                                           int64_t k0, int64_t kend, bool vec_ok, float (&reg)[R * BK / 4 / NT][4]) {
+    constexpr int NL = R * BK / 4 / NT;
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-        const int idx = t + 256 * i;
-        if constexpr (KCONTIG) {
+        const int idx = t + NT * i;
+        if constexpr (FULL) {   // interior tile, aligned, whole slice in range: no guards
+            const int r = KCONTIG ? idx / (BK / 4) : (idx % (R / 4)) * 4;
+            const int k = KCONTIG ? (idx % (BK / 4)) * 4 : idx / (R / 4);
+            const float* src = KCONTIG ? P + (r0 + r) * ld + (k0 + k) : P + (k0 + k) * ld + (r0 + r);
+            const float4 v = *reinterpret_cast<const float4*>(src);
+            reg[i][0] = v.x; reg[i][1] = v.y; reg[i][2] = v.z; reg[i][3] = v.w;
+        } else if constexpr (KCONTIG) {
             const int r = idx / (BK / 4), kq = idx % (BK / 4);
             const int64_t gr = r0 + r, gk = k0 + kq * 4;
             if (vec_ok && gr < Rlim && gk + 3 < kend) {
@@ -75,13 +83,13 @@ __device__ __forceinline__ void load_slice(const float* __restrict__ P, int64_t 
     }
 }
 
-template <int KCONTIG, int R, int BK, int LDS_LD>
-__device__ __forceinline__ void store_slice(float* __restrict__ S, const float (&reg)[R * BK / 1024][4]) {
-    constexpr int NL = R * BK / 1024;
+template <int KCONTIG, int R, int BK, int LDS_LD, int NT>
+__device__ __forceinline__ void store_slice(float* __restrict__ S, const float (&reg)[R * BK / 4 / NT][4]) {
+    constexpr int NL = R * BK / 4 / NT;
     const int t = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-        const int idx = t + 256 * i;
+        const int idx = t + NT * i;
         if constexpr (KCONTIG) {
             const int r = idx / (BK / 4), kq = idx % (BK / 4);
 #pragma unroll
@@ -94,13 +102,13 @@ __device__ __forceinline__ void store_slice(float* __restrict__ S, const float (
     }
 }
 
-// C tile BM x BN per 256-thread workgroup; the 4 waves form a WM x WN grid, each wave
-// owns (BM/WM) x (BN/WN) = TM x TN MFMA tiles of 32x32.
+// C tile BM x BN per workgroup of WM x WN waves; each wave owns (BM/WM) x (BN/WN)
+// = TM x TN MFMA tiles of 32x32.
 // TA: 0 -> A is [M,K] (K-contiguous), 1 -> A is [K,M].
 // TB: 0 -> B is [K,N] (N-contiguous), 1 -> B is [N,K] (K-contiguous).
-template <int TA, int TB, int BM, int BN, int BK, int WM, int WN>
-__global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
-    static_assert(WM * WN == 4, "4 waves per workgroup");
+template <int TA, int TB, int BM, int BN, int BK, int WM, int WN, int ABL = 0>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
+    constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
@@ -132,46 +140,62 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float ra[BM * BK / 1024][4], rb[BN * BK / 1024][4];
+    float ra[BM * BK / 4 / NT][4], rb[BN * BK / 4 / NT][4];
     const int64_t nk = (ke > kb) ? (ke - kb + BK - 1) / BK : 0;
+    // interior tile with whole, aligned K slices: unguarded loads (uniform branch)
+    const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % BK == 0);
+    auto load_ab = [&](int64_t k0) {
+        if (full) {
+            load_slice<AK, BM, BK, NT, true>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
+            load_slice<BKc, BN, BK, NT, true>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
+        } else {
+            load_slice<AK, BM, BK, NT>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
+            load_slice<BKc, BN, BK, NT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
+        }
+    };
+    // Pipeline (guide T14 order): slice t+1 is written to LDS right AFTER the barrier that
+    // frees its buffer, slice t+2 is loaded into registers immediately, then slice t is
+    // multiplied; the LDS-write latency and the global-load latency both hide under the MFMAs.
     if (nk > 0) {
-        load_slice<AK, BM, BK>(g.A, g.lda, g.M, m0, kb, ke, a_vec, ra);
-        load_slice<BKc, BN, BK>(g.B, g.ldb, g.N, n0, kb, ke, b_vec, rb);
-        store_slice<AK, BM, BK, LDA_S>(As[0], ra);
-        store_slice<BKc, BN, BK, LDB_S>(Bs[0], rb);
+        load_ab(kb);
+        store_slice<AK, BM, BK, LDA_S, NT>(As[0], ra);
+        store_slice<BKc, BN, BK, LDB_S, NT>(Bs[0], rb);
+        if (nk > 1 && ABL == 0) load_ab(kb + BK);
     }
     __syncthreads();
 
     const int li = lane & 31, lk = lane >> 5;
     for (int64_t kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        const bool more = kt + 1 < nk;
-        if (more) {
-            const int64_t k0 = kb + (kt + 1) * BK;
-            load_slice<AK, BM, BK>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
-            load_slice<BKc, BN, BK>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
+        if (kt + 1 < nk && ABL <= 1) {
+            store_slice<AK, BM, BK, LDA_S, NT>(As[cur ^ 1], ra);
+            store_slice<BKc, BN, BK, LDB_S, NT>(Bs[cur ^ 1], rb);
         }
+        if (kt + 2 < nk && ABL == 0) load_ab(kb + (kt + 2) * BK);
         const float* as = As[cur] + wm * (BM / WM) + li;
         const float* bs = Bs[cur] + wn * (BN / WN) + li;
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
             const int kr = 2 * kk + lk;
             float a[TM], b[TN];
+            if constexpr (ABL >= 3) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i) a[i] = as[kr * LDA_S + i * 32];
+                for (int i = 0; i < TM; ++i) a[i] = ra[0][i & 3] + (float)kk;
 #pragma unroll
-            for (int j = 0; j < TN; ++j) b[j] = bs[kr * LDB_S + j * 32];
+                for (int j = 0; j < TN; ++j) b[j] = rb[0][j & 3];
+            } else {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) a[i] = as[kr * LDA_S + i * 32];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) b[j] = bs[kr * LDB_S + j * 32];
+            }
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
-        if (more) {
-            store_slice<AK, BM, BK, LDA_S>(As[cur ^ 1], ra);
-            store_slice<BKc, BN, BK, LDB_S>(Bs[cur ^ 1], rb);
-        }
-        __syncthreads();
+        if constexpr (ABL <= 1) __syncthreads();
     }
 
     // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -193,6 +217,8 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
                 } else {
                     v *= g.alpha;
                     if (g.beta != 0.f) v += g.beta * dst[row * ldd + col];
+                    if (g.bias) v += g.bias[col];
+                    if (g.relu) v = fmaxf(v, 0.f);
                     dst[row * ldd + col] = v;
                 }
             }
@@ -201,7 +227,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(GemmArgs g) {
 
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ ws, int split, int64_t M,
                                                        int64_t N, float alpha, float beta, float* __restrict__ C,
-                                                       int64_t ldc) {
+                                                       int64_t ldc, const float* __restrict__ bias, int relu) {
     const int64_t total = M * N;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -210,29 +236,47 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
         const int64_t r = i / N, c = i % N;
         float v = alpha * s;
         if (beta != 0.f) v += beta * C[r * ldc + c];
+        if (bias) v += bias[c];
+        if (relu) v = fmaxf(v, 0.f);
         C[r * ldc + c] = v;
     }
 }
 
 struct GemmCfg {
-    int bm, bn, bk;
+    int bm, bn, bk, waves, blocks_per_cu;
 };
-// tile configurations (index = BGNN_TUNE_GEMM_CFG value)
-constexpr GemmCfg kCfgs[] = {{128, 128, 16}, {128, 128, 32}, {256, 128, 16}, {128, 256, 16}};
-constexpr int kNumCfgs = 4;
+// tile configurations (index = bgnn_gemm_set_cfg value)
+constexpr GemmCfg kCfgs[] = {
+    {128, 128, 16, 4, 3},   // 0: 2x2 waves of 64x64
+    {256, 256, 16, 8, 1},   // 1: 2x4 waves of 128x64 (2 waves/SIMD)
+    {256, 256, 16, 4, 1},   // 2: 2x2 waves of 128x128 (1 wave/SIMD)
+    {256, 128, 16, 8, 1},   // 3: 4x2 waves of 64x64
+    {256, 128, 16, 4, 1},   // 4: 2x2 waves of 128x64
+    {128, 256, 16, 8, 1},   // 5: 2x4 waves of 64x64
+    {128, 256, 32, 8, 1},   // 6: as 5, BK = 32
+    {256, 256, 32, 8, 1},   // 7: as 1, BK = 32
+    {256, 128, 32, 8, 1},   // 8: as 3, BK = 32
+};
+constexpr int kNumCfgs = 9;
 static int g_gemm_cfg = -1;   // -1 = automatic
+static int g_gemm_abl = 0;    // ablation (measurement only)
 
+// Measured on MI355X (tools/tune_gemm.py, SAGE layer shapes): 256x128 tiles of 8 waves for
+// the tall GEMMs (fwd 118 TF, dgrad 118 TF), 256x256 tiles of 8 waves + split-K for the
+// short-and-deep weight gradient (125 TF); small problems keep the 128x128 tile.
 inline int pick_cfg(int64_t M, int64_t N, int64_t K, int ta, int tb) {
-    (void)K; (void)ta; (void)tb;
+    (void)ta; (void)tb;
     if (g_gemm_cfg >= 0) return g_gemm_cfg;
-    (void)M; (void)N;
+    if (M >= 256 && N >= 256 && K >= 8192 && M * N <= (int64_t)4096 * 4096) return 1;
+    if (M >= 4096 && N >= 128) return 3;
     return 0;
 }
 
 inline int choose_split(int64_t M, int64_t N, int64_t K, const GemmCfg& c) {
     const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
-    if (tiles >= 512 || K < 4 * 256) return 1;
-    int64_t s = (1024 + tiles - 1) / tiles;
+    const int64_t slots = 256 * c.blocks_per_cu;          // resident workgroups on the chip
+    if (tiles >= slots / 2 || K < 4 * 256) return 1;
+    int64_t s = (slots + tiles - 1) / tiles;
     const int64_t smax = K / 256;   // keep >= 256 of K per slice
     if (s > smax) s = smax;
     if (s > 64) s = 64;
@@ -242,9 +286,19 @@ inline int choose_split(int64_t M, int64_t N, int64_t K, const GemmCfg& c) {
 template <int TA, int TB>
 void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     switch (cfg) {
-        case 1: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 128, 32, 2, 2>), grid, dim3(256), 0, s, g); break;
-        case 2: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
-        case 3: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
+        case 1: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 256, 16, 2, 4>), grid, dim3(512), 0, s, g); break;
+        case 2: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 256, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
+        case 3: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 16, 4, 2>), grid, dim3(512), 0, s, g); break;
+        case 4: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
+        case 5:
+            if (g_gemm_abl == 1) hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4, 1>), grid, dim3(512), 0, s, g);
+            else if (g_gemm_abl == 2) hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4, 2>), grid, dim3(512), 0, s, g);
+            else if (g_gemm_abl == 3) hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4, 3>), grid, dim3(512), 0, s, g);
+            else hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4>), grid, dim3(512), 0, s, g);
+            break;
+        case 6: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 32, 2, 4>), grid, dim3(512), 0, s, g); break;
+        case 7: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 256, 32, 2, 4>), grid, dim3(512), 0, s, g); break;
+        case 8: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 32, 4, 2>), grid, dim3(512), 0, s, g); break;
         default: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 128, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
     }
 }
@@ -254,8 +308,9 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 using namespace bgnn;
 
 extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
-    BGNN_REQUIRE(cfg >= -1 && cfg < kNumCfgs, "gemm: config %d out of range", cfg);
-    g_gemm_cfg = cfg;
+    BGNN_REQUIRE(cfg >= -1 && cfg < kNumCfgs + 300, "gemm: config %d out of range", cfg);
+    g_gemm_abl = cfg / 100;
+    g_gemm_cfg = cfg % 100;
     return BGNN_OK;
 }
 
@@ -264,9 +319,10 @@ extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta
     return s > 1 ? (size_t)s * (size_t)M * (size_t)N * sizeof(float) : 0;
 }
 
-extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
-                             int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, void* ws,
-                             size_t ws_bytes, void* stream) {
+extern "C" int bgnn_gemm_f32_ex(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
+                                const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                                int64_t ldc, const float* bias, int32_t relu, void* ws, size_t ws_bytes,
+                                void* stream) {
     BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
     BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
     BGNN_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M) || M == 0 || K == 0, "gemm: bad lda");
@@ -280,7 +336,7 @@ extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64
     hipStream_t s = as_stream(stream);
     int split = choose_split(M, N, K, c);
     if (split > 1 && (ws == nullptr || ws_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
-    GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split};
+    GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu};
     int64_t kc = (K + split - 1) / split;
     kc = (kc + c.bk - 1) / c.bk * c.bk;
     g.kchunk = kc > 0 ? kc : c.bk;
@@ -294,8 +350,14 @@ extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64
         int64_t blocks = (M * N + 255) / 256;
         if (blocks > 4096) blocks = 4096;
         hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, split, M, N,
-                           alpha, beta, C, ldc);
+                           alpha, beta, C, ldc, bias, relu);
         BGNN_CHECK_LAUNCH();
     }
     return BGNN_OK;
+}
+
+extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                             int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, void* ws,
+                             size_t ws_bytes, void* stream) {
+    return bgnn_gemm_f32_ex(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr, 0, ws, ws_bytes, stream);
 }

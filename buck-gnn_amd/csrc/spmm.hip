@@ -375,6 +375,7 @@ __global__ __launch_bounds__(64) void k_seg_combine(SegArgs A) {
     const int32_t c0 = A.heavy_chunk0[h], c1 = A.heavy_chunk0[h + 1];
     Acc<VEC, NV, OP> acc;
     acc.init();
+#pragma unroll 8
     for (int32_t c = c0; c < c1; ++c) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {

@@ -212,6 +212,12 @@ int bgnn_gemm_set_cfg(int32_t cfg);
 int bgnn_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
                   float beta, float* C, int64_t ldc, void* ws, size_t ws_bytes, void* stream);
+/* Same with a fused epilogue: C = act(alpha*op(A)op(B) + beta*C + bias[col]),
+ * act = ReLU when relu != 0 (nn.Linear + ReLU of the node encoder, Models/BuckGNN.py:67-74). */
+int bgnn_gemm_f32_ex(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                     float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
+                     float beta, float* C, int64_t ldc, const float* bias, int32_t relu,
+                     void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }
