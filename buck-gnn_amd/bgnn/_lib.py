@@ -52,7 +52,7 @@ SIGNATURES = {
     "bgnn_graph_build": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p]),
     "bgnn_index_csr_build": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_sz, c_p, c_p]),
     "bgnn_heavy_plan_ws_bytes": (c_sz, [c_i64]),
-    "bgnn_heavy_plan": (c_i32, [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p, c_p]),
+    "bgnn_heavy_plan": (c_i32, [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
                               c_p, c_p]),

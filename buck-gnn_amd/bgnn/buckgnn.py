@@ -25,6 +25,9 @@ from .graph import Graph, SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
 
+# run the node encoder on bgnn GEMMs (fused bias+ReLU) instead of torch nn.Linear
+FUSED_ENCODER = False
+
 _SAGE_VARIANTS = {
     # model_name: (ModuleList attribute, aggr, has BatchNorm)
     "GraphSage_sumAggr": ("sage_blocks_sum", "sum", True),
@@ -225,7 +228,7 @@ class BuckGNN(nn.Module):
             is_real_node = x[:, -1] == 0 if x.size(1) > 0 else torch.ones(x.size(0), dtype=torch.bool,
                                                                            device=x.device)
             real_node_batch = batch[is_real_node] if batch is not None else None
-        if self._fused_ok(x) and x.size(0) >= 1024:
+        if self._fused_ok(x) and x.size(0) >= 1024 and FUSED_ENCODER:
             x = mlp(self.node_encoder, x)        # encoder GEMMs with fused bias+ReLU epilogues
         else:
             x = self.node_encoder(x)

@@ -39,7 +39,8 @@ def require_cuda(*tensors: torch.Tensor, what: str = "bgnn") -> None:
 
 @dataclass
 class Plan:
-    """Heavy-row split plan of one CSR (rows with deg > chunk)."""
+    """Heavy-row split plan of one CSR (rows with deg > chunk). n_heavy / n_chunks are
+    filled on the host after the (single, batched) device->host copy of the counts."""
 
     heavy_row: torch.Tensor
     heavy_chunk0: torch.Tensor
@@ -49,18 +50,26 @@ class Plan:
     chunk: int
 
 
-def make_plan(rowptr: torch.Tensor, n_rows: int, nnz: int, chunk: int = DEFAULT_CHUNK) -> Plan:
+def enqueue_plan(rowptr: torch.Tensor, n_rows: int, nnz: int, counts: torch.Tensor,
+                 chunk: int = DEFAULT_CHUNK) -> Plan:
+    """Launch bgnn_heavy_plan; its two counts land in `counts` (device int32[2])."""
     dev = rowptr.device
     heavy_row = torch.empty(max(n_rows, 1), dtype=torch.int32, device=dev)
     heavy_chunk0 = torch.empty(max(n_rows, 1) + 1, dtype=torch.int32, device=dev)
     # sum over heavy rows of ceil(deg/chunk) <= nnz/chunk + n_heavy <= 2*nnz/chunk
     chunk_heavy = torch.empty(2 * (nnz // chunk) + 2, dtype=torch.int32, device=dev)
     ws = torch.empty(_lib.query("bgnn_heavy_plan_ws_bytes", n_rows), dtype=torch.uint8, device=dev)
-    counts = (ctypes.c_int32 * 2)()
     _lib.call("bgnn_heavy_plan", rowptr.data_ptr(), n_rows, nnz, chunk, heavy_row.data_ptr(),
-              heavy_chunk0.data_ptr(), chunk_heavy.data_ptr(), ws.data_ptr(), ws.numel(),
-              ctypes.cast(counts, ctypes.c_void_p), _stream())
-    return Plan(heavy_row, heavy_chunk0, chunk_heavy, int(counts[0]), int(counts[1]), chunk)
+              heavy_chunk0.data_ptr(), chunk_heavy.data_ptr(), counts.data_ptr(), ws.data_ptr(), ws.numel(),
+              _stream())
+    return Plan(heavy_row, heavy_chunk0, chunk_heavy, -1, -1, chunk)
+
+
+def make_plan(rowptr: torch.Tensor, n_rows: int, nnz: int, chunk: int = DEFAULT_CHUNK) -> Plan:
+    counts = torch.empty(2, dtype=torch.int32, device=rowptr.device)
+    p = enqueue_plan(rowptr, n_rows, nnz, counts, chunk)
+    p.n_heavy, p.n_chunks = counts.tolist()
+    return p
 
 
 @dataclass
@@ -75,6 +84,7 @@ class Csr:
     def struct(self) -> _lib.CsrStruct:
         if self._struct is None:
             p = self.plan
+            assert p.n_heavy >= 0, "plan counts not resolved (call resolve())"
             self._struct = _lib.CsrStruct(
                 self.rowptr.data_ptr(), self.col.data_ptr(), p.heavy_row.data_ptr(),
                 p.heavy_chunk0.data_ptr(), p.chunk_heavy.data_ptr(), self.n_rows, self.nnz,
@@ -98,10 +108,11 @@ class Graph:
     bwd: Csr
     perm_t: torch.Tensor
     edge_index: Optional[torch.Tensor] = field(default=None, repr=False)
+    meta: Optional[torch.Tensor] = field(default=None, repr=False)   # device int32[5]: status, counts
 
     @staticmethod
-    def build(edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK,
-              check: bool = True) -> "Graph":
+    def enqueue(edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK) -> "Graph":
+        """Launch every build kernel without any host synchronisation; call resolve(meta_host)."""
         require_cuda(edge_index, what="Graph.build")
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError(f"edge_index must have shape [2, E], got {tuple(edge_index.shape)}")
@@ -109,21 +120,31 @@ class Graph:
         E = ei.size(1)
         N = int(num_nodes)
         dev = ei.device
+        meta = torch.zeros(5, dtype=torch.int32, device=dev)
         rowptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
         rowptr_t = torch.empty(N + 1, dtype=torch.int32, device=dev)
         col = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
         col_t = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
         perm_t = torch.empty(max(E, 1), dtype=torch.int32, device=dev)
         ws = torch.empty(_lib.query("bgnn_graph_build_ws_bytes", E, N), dtype=torch.uint8, device=dev)
-        status = (ctypes.c_int32 * 1)(0)
         _lib.call("bgnn_graph_build", ei.data_ptr(), E, N, rowptr.data_ptr(), col.data_ptr(),
                   rowptr_t.data_ptr(), col_t.data_ptr(), perm_t.data_ptr(), ws.data_ptr(), ws.numel(),
-                  ctypes.cast(status, ctypes.c_void_p) if check else None, _stream())
-        if check and status[0] != 0:
-            raise IndexError(f"edge_index contains indices outside [0, {N})")
-        fwd = Csr(rowptr, col, N, E, make_plan(rowptr, N, E, chunk))
-        bwd = Csr(rowptr_t, col_t, N, E, make_plan(rowptr_t, N, E, chunk))
-        return Graph(N, E, fwd, bwd, perm_t, edge_index)
+                  meta.data_ptr(), _stream())
+        fwd = Csr(rowptr, col, N, E, enqueue_plan(rowptr, N, E, meta[1:3], chunk))
+        bwd = Csr(rowptr_t, col_t, N, E, enqueue_plan(rowptr_t, N, E, meta[3:5], chunk))
+        return Graph(N, E, fwd, bwd, perm_t, edge_index, meta)
+
+    def resolve(self, meta_host) -> "Graph":
+        if int(meta_host[0]) != 0:
+            raise IndexError(f"edge_index contains indices outside [0, {self.num_nodes})")
+        self.fwd.plan.n_heavy, self.fwd.plan.n_chunks = int(meta_host[1]), int(meta_host[2])
+        self.bwd.plan.n_heavy, self.bwd.plan.n_chunks = int(meta_host[3]), int(meta_host[4])
+        return self
+
+    @staticmethod
+    def build(edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK) -> "Graph":
+        g = Graph.enqueue(edge_index, num_nodes, chunk)
+        return g.resolve(g.meta.tolist())
 
 
 @dataclass
@@ -135,31 +156,39 @@ class SegmentIndex:
     fwd: Csr          # rows = segments (graphs), col = positions
     bwd: Csr          # rows = positions, exactly one entry: its segment
     index: Optional[torch.Tensor] = field(default=None, repr=False)   # int64 [n]
+    meta: Optional[torch.Tensor] = field(default=None, repr=False)    # device int32[3]
 
     @staticmethod
-    def build(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK,
-              check: bool = True) -> "SegmentIndex":
+    def enqueue(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK) -> "SegmentIndex":
         require_cuda(index, what="SegmentIndex.build")
         idx = index.to(torch.int64).contiguous().view(-1)
         n = idx.numel()
         R = int(num_rows)
         dev = idx.device
+        meta = torch.zeros(3, dtype=torch.int32, device=dev)
         rowptr = torch.empty(R + 1, dtype=torch.int32, device=dev)
         col = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         ws = torch.empty(_lib.query("bgnn_graph_build_ws_bytes", n, R), dtype=torch.uint8, device=dev)
-        status = (ctypes.c_int32 * 1)(0)
         _lib.call("bgnn_index_csr_build", idx.data_ptr(), n, R, rowptr.data_ptr(), col.data_ptr(),
-                  ws.data_ptr(), ws.numel(), ctypes.cast(status, ctypes.c_void_p) if check else None,
-                  _stream())
-        if check and status[0] != 0:
-            raise IndexError(f"index contains values outside [0, {R})")
-        fwd = Csr(rowptr, col, R, n, make_plan(rowptr, R, n, chunk))
+                  ws.data_ptr(), ws.numel(), meta.data_ptr(), _stream())
+        fwd = Csr(rowptr, col, R, n, enqueue_plan(rowptr, R, n, meta[1:3], chunk))
         rowptr_t = torch.arange(n + 1, dtype=torch.int32, device=dev)
         col_t = idx.to(torch.int32)
         empty = Plan(torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
                      torch.zeros(1, dtype=torch.int32, device=dev), 0, 0, chunk)
         bwd = Csr(rowptr_t, col_t if n > 0 else torch.zeros(1, dtype=torch.int32, device=dev), n, n, empty)
-        return SegmentIndex(n, R, fwd, bwd, idx)
+        return SegmentIndex(n, R, fwd, bwd, idx, meta)
+
+    def resolve(self, meta_host) -> "SegmentIndex":
+        if int(meta_host[0]) != 0:
+            raise IndexError(f"index contains values outside [0, {self.num_rows})")
+        self.fwd.plan.n_heavy, self.fwd.plan.n_chunks = int(meta_host[1]), int(meta_host[2])
+        return self
+
+    @staticmethod
+    def build(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK) -> "SegmentIndex":
+        s = SegmentIndex.enqueue(index, num_rows, chunk)
+        return s.resolve(s.meta.tolist())
 
 
 class _Cache:
@@ -180,6 +209,17 @@ class _Cache:
         self.items.insert(0, (t, ver, key, val))
         del self.items[self.size:]
         return val
+
+    def peek(self, t: torch.Tensor, key):
+        ver = t._version
+        for tt, v, k, val in self.items:
+            if tt is t and v == ver and k == key:
+                return val
+        return None
+
+    def put(self, t: torch.Tensor, key, val):
+        self.items.insert(0, (t, t._version, key, val))
+        del self.items[self.size:]
 
     def clear(self):
         self.items.clear()
@@ -202,3 +242,35 @@ def segments_for(index: torch.Tensor, num_rows: int, chunk: int = DEFAULT_CHUNK)
 def clear_caches() -> None:
     _graph_cache.clear()
     _index_cache.clear()
+
+
+def prepare(edge_index: torch.Tensor, num_nodes: int, batch: Optional[torch.Tensor] = None,
+            num_graphs: Optional[int] = None, chunk: int = DEFAULT_CHUNK):
+    """Build (or fetch from cache) the graph structure of a mini-batch and the segment
+    structure of its `batch` vector with ONE host synchronisation for all status words and
+    plan counts, and register them in the caches used by SAGEConv / BuckGNN / pooling."""
+    key = (int(num_nodes), chunk)
+    g = _graph_cache.peek(edge_index, key)
+    s = None
+    pending = []
+    if g is None:
+        g = Graph.enqueue(edge_index, num_nodes, chunk)
+        pending.append(g)
+    if batch is not None:
+        s = _index_cache.peek(batch, ("batch",))
+        if s is None:
+            n = num_graphs if num_graphs is not None else int(batch.max().item()) + 1
+            s = SegmentIndex.enqueue(batch, n, chunk)
+            pending.append(s)
+    if pending:
+        host = torch.cat([p.meta for p in pending]).tolist()
+        off = 0
+        for p in pending:
+            k = p.meta.numel()
+            p.resolve(host[off:off + k])
+            off += k
+        if pending[0] is g:
+            _graph_cache.put(edge_index, key, g)
+        if s is not None and pending[-1] is s:
+            _index_cache.put(batch, ("batch",), s)
+    return g, s

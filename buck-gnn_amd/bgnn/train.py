@@ -22,6 +22,8 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from .graph import prepare
+
 
 class RelativeErrorLoss(nn.Module):
     """mean(|pred - target| / (|target| + eps))  (Utils/Losses.py:755-761)."""
@@ -89,6 +91,8 @@ class GradAllReduce:
 
 def train_step(model, batch, optimizer, criterion, normalizer=None, allreduce: Optional[GradAllReduce] = None,
                sync_metrics: bool = False):
+    # graph + pooling structure for this batch, one host sync (cached per tensor)
+    prepare(batch.edge_index, batch.x.size(0), batch.batch, getattr(batch, "num_graphs", None) or None)
     pred, _ = model(batch.x, batch.edge_index, batch.edge_attr, batch.batch)
     if normalizer is not None:
         loss = criterion(normalizer.denormalize_eigenvalue(pred), normalizer.denormalize_eigenvalue(batch.y))

@@ -148,19 +148,16 @@ extern "C" size_t bgnn_graph_build_ws_bytes(int64_t E, int64_t N) {
 
 extern "C" int bgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int32_t* rowptr,
                                 int32_t* col, int32_t* rowptr_t, int32_t* col_t, int32_t* perm_t,
-                                void* ws, size_t ws_bytes, int32_t* host_status, void* stream) {
+                                void* ws, size_t ws_bytes, int32_t* dev_status, void* stream) {
     BGNN_REQUIRE(E >= 0 && N >= 0 && N < (int64_t(1) << 31) && E < (int64_t(1) << 31),
                  "graph_build: bad sizes E=%lld N=%lld", (long long)E, (long long)N);
     BGNN_REQUIRE(rowptr && rowptr_t, "graph_build: null rowptr");
     hipStream_t s = as_stream(stream);
-    if (N == 0) {
-        if (host_status) host_status[0] = 0;
-        return BGNN_OK;
-    }
+    if (dev_status) BGNN_HIP(hipMemsetAsync(dev_status, 0, sizeof(int32_t), s));
+    if (N == 0) return BGNN_OK;
     if (E == 0) {
         BGNN_HIP(hipMemsetAsync(rowptr, 0, (N + 1) * sizeof(int32_t), s));
         BGNN_HIP(hipMemsetAsync(rowptr_t, 0, (N + 1) * sizeof(int32_t), s));
-        if (host_status) host_status[0] = 0;
         return BGNN_OK;
     }
     BGNN_REQUIRE(edge_index && col && col_t && perm_t, "graph_build: null pointer");
@@ -173,14 +170,15 @@ extern "C" int bgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
     int32_t* iota = c.take<int32_t>(E);
     int32_t* src_sorted = c.take<int32_t>(E);
     int32_t* spare = c.take<int32_t>(E);
-    int32_t* bad = c.take<int32_t>(64);
+    int32_t* bad_ws = c.take<int32_t>(64);
     size_t tmp_bytes = radix_tmp_bytes(E);
     void* tmp = c.take<char>(tmp_bytes);
     BGNN_REQUIRE(c.ok, "graph_build: workspace carve failed");
     (void)spare;
+    int32_t* bad = dev_status ? dev_status : bad_ws;
 
     const int T = 256;
-    BGNN_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
+    if (!dev_status) BGNN_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
     k_split_coo<<<grid1d(E, T), T, 0, s>>>(edge_index, E, N, src, dst, bad);
     BGNN_CHECK_LAUNCH();
     const int nb = bits_for(N);
@@ -198,26 +196,19 @@ extern "C" int bgnn_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
     BGNN_CHECK_LAUNCH();
     k_gather_i32<<<grid1d(E, T), T, 0, s>>>(dst_sorted, perm_t, E, col_t);
     BGNN_CHECK_LAUNCH();
-    if (host_status) {
-        BGNN_HIP(hipMemcpyAsync(host_status, bad, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        BGNN_HIP(hipStreamSynchronize(s));
-    }
     return BGNN_OK;
 }
 
 extern "C" int bgnn_index_csr_build(const int64_t* index, int64_t n, int64_t R, int32_t* rowptr,
-                                    int32_t* col, void* ws, size_t ws_bytes, int32_t* host_status,
+                                    int32_t* col, void* ws, size_t ws_bytes, int32_t* dev_status,
                                     void* stream) {
     BGNN_REQUIRE(n >= 0 && R >= 0 && n < (int64_t(1) << 31) && R < (int64_t(1) << 31),
                  "index_csr_build: bad sizes");
     hipStream_t s = as_stream(stream);
-    if (R == 0) {
-        if (host_status) host_status[0] = 0;
-        return BGNN_OK;
-    }
+    if (dev_status) BGNN_HIP(hipMemsetAsync(dev_status, 0, sizeof(int32_t), s));
+    if (R == 0) return BGNN_OK;
     if (n == 0) {
         BGNN_HIP(hipMemsetAsync(rowptr, 0, (R + 1) * sizeof(int32_t), s));
-        if (host_status) host_status[0] = 0;
         return BGNN_OK;
     }
     BGNN_REQUIRE(ws_bytes >= bgnn_graph_build_ws_bytes(n, R), "index_csr_build: workspace too small");
@@ -228,22 +219,19 @@ extern "C" int bgnn_index_csr_build(const int64_t* index, int64_t n, int64_t R, 
     c.take<int32_t>(n);
     c.take<int32_t>(n);
     c.take<int32_t>(n);
-    int32_t* bad = c.take<int32_t>(64);
+    int32_t* bad_ws = c.take<int32_t>(64);
     size_t tmp_bytes = radix_tmp_bytes(n);
     void* tmp = c.take<char>(tmp_bytes);
     BGNN_REQUIRE(c.ok, "index_csr_build: workspace carve failed");
+    int32_t* bad = dev_status ? dev_status : bad_ws;
     const int T = 256;
-    BGNN_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
+    if (!dev_status) BGNN_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
     k_index_to_keys<<<grid1d(n, T), T, 0, s>>>(index, n, R, keys, vals, bad);
     BGNN_CHECK_LAUNCH();
     BGNN_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_sorted, vals, col, (int)n,
                                                 0, bits_for(R), s));
     k_rowptr_from_sorted<<<grid1d(n + 1, T), T, 0, s>>>(keys_sorted, n, R, rowptr);
     BGNN_CHECK_LAUNCH();
-    if (host_status) {
-        BGNN_HIP(hipMemcpyAsync(host_status, bad, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        BGNN_HIP(hipStreamSynchronize(s));
-    }
     return BGNN_OK;
 }
 
@@ -254,13 +242,13 @@ extern "C" size_t bgnn_heavy_plan_ws_bytes(int64_t R) {
 
 extern "C" int bgnn_heavy_plan(const int32_t* rowptr, int64_t R, int64_t nnz, int32_t chunk,
                                int32_t* heavy_row, int32_t* heavy_chunk0, int32_t* chunk_heavy,
-                               void* ws, size_t ws_bytes, int32_t* host_counts, void* stream) {
+                               int32_t* dev_counts, void* ws, size_t ws_bytes, void* stream) {
     BGNN_REQUIRE(chunk > 0, "heavy_plan: chunk must be > 0");
-    BGNN_REQUIRE(host_counts, "heavy_plan: host_counts is required");
+    BGNN_REQUIRE(dev_counts, "heavy_plan: dev_counts is required");
     hipStream_t s = as_stream(stream);
     const int64_t cap = 2 * (nnz / chunk) + 2;   // capacity of chunk_heavy (see bgnn.h)
     if (R == 0) {
-        host_counts[0] = host_counts[1] = 0;
+        BGNN_HIP(hipMemsetAsync(dev_counts, 0, 2 * sizeof(int32_t), s));
         return BGNN_OK;
     }
     BGNN_REQUIRE(ws_bytes >= bgnn_heavy_plan_ws_bytes(R), "heavy_plan: workspace too small");
@@ -269,7 +257,6 @@ extern "C" int bgnn_heavy_plan(const int32_t* rowptr, int64_t R, int64_t nnz, in
     int32_t* flag = c.take<int32_t>(R);
     int32_t* nch_off = c.take<int32_t>(R);
     int32_t* flag_off = c.take<int32_t>(R);
-    int32_t* counts = c.take<int32_t>(4);
     size_t tmp_bytes = scan_tmp_bytes(R);
     void* tmp = c.take<char>(tmp_bytes);
     BGNN_REQUIRE(c.ok, "heavy_plan: workspace carve failed");
@@ -279,9 +266,7 @@ extern "C" int bgnn_heavy_plan(const int32_t* rowptr, int64_t R, int64_t nnz, in
     BGNN_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, nch, nch_off, (int)R, s));
     BGNN_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, flag, flag_off, (int)R, s));
     k_heavy_fill<<<grid1d(R, T), T, 0, s>>>(rowptr, R, chunk, nch_off, flag_off, heavy_row,
-                                            heavy_chunk0, chunk_heavy, cap, counts);
+                                            heavy_chunk0, chunk_heavy, cap, dev_counts);
     BGNN_CHECK_LAUNCH();
-    BGNN_HIP(hipMemcpyAsync(host_counts, counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    BGNN_HIP(hipStreamSynchronize(s));
     return BGNN_OK;
 }

@@ -90,28 +90,29 @@ size_t bgnn_graph_build_ws_bytes(int64_t num_edges, int64_t num_nodes);
  *   transpose CSR (rows = sources): rowptr_t[N+1], col_t[E] = targets,
  *                                   perm_t[E] = forward-CSR position of the edge.
  * Both sorts are stable, so entries of a row keep edge_index order.
- * `host_status[0]` receives 0, or 1 if an index was outside [0, N); the call
- * synchronises the stream only when host_status != NULL. */
+ * `dev_status` (device int32, may be NULL) receives 0, or 1 if an index was outside
+ * [0, N). Fully asynchronous: no host synchronisation. */
 int bgnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
                      int32_t* rowptr, int32_t* col,
                      int32_t* rowptr_t, int32_t* col_t, int32_t* perm_t,
-                     void* ws, size_t ws_bytes, int32_t* host_status, void* stream);
+                     void* ws, size_t ws_bytes, int32_t* dev_status, void* stream);
 
 /* CSR over segments given a sorted-or-unsorted index vector (global_mean_pool's
  * `batch`, torch_scatter's `index`): row r lists the positions i with index[i]==r,
- * in increasing i. Same workspace rule as bgnn_graph_build with E = n. */
+ * in increasing i. Same workspace rule as bgnn_graph_build with E = n. Asynchronous. */
 int bgnn_index_csr_build(const int64_t* index, int64_t n, int64_t num_rows,
                          int32_t* rowptr, int32_t* col,
-                         void* ws, size_t ws_bytes, int32_t* host_status, void* stream);
+                         void* ws, size_t ws_bytes, int32_t* dev_status, void* stream);
 
 /* Heavy-row plan for a CSR (rows with deg > chunk). Outputs are device arrays
  * sized for the worst case: heavy_row[n_rows], heavy_chunk0[n_rows+1],
- * chunk_heavy[2 * (nnz / chunk) + 2]. host_counts[0] = n_heavy, [1] = n_chunks
- * (synchronises the stream). */
+ * chunk_heavy[2 * (nnz / chunk) + 2]. dev_counts[0] = n_heavy, [1] = n_chunks
+ * (device int32[2]); the caller copies them to the host (one sync for all plans of
+ * a batch) before filling bgnn_csr_t. Asynchronous. */
 size_t bgnn_heavy_plan_ws_bytes(int64_t n_rows);
 int bgnn_heavy_plan(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t chunk,
                     int32_t* heavy_row, int32_t* heavy_chunk0, int32_t* chunk_heavy,
-                    void* ws, size_t ws_bytes, int32_t* host_counts, void* stream);
+                    int32_t* dev_counts, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Generic segment reduce (SpMM with a 0/1 or 1/deg matrix):
