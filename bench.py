@@ -14,10 +14,15 @@ forward, RelativeErrorLoss on denormalised eigenvalues, backward, gradient all-r
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
-Rank 0 prints ONE JSON line. `roofline` is for the fused aggregation kernel
-(bgnn_sage_fwd: neighbour sum + lin_r term + bias + L2 normalize + BN statistics),
-HBM-bound; `roofline_mfma` for the forward GEMM. Both use HIP events recorded on the
-launching stream around each launch inside the timed region.
+Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel, the forward GEMM
+z = x [W_l;W_r]^T (18 GEMMs of this size make up ~60 % of the step), MFMA-bound: 84.6 GFLOP per
+launch; its peak is the ceiling of the algorithm that runs (bf16 dense MFMA 2.5 PF / 6 piece
+products = 416.7 TF f32-equivalent; the f32 MFMA peak 157.3 TF is reported beside it).
+`roofline_hbm` is the fused aggregation kernel (bgnn_sage_fwd: neighbour sum + lin_r term +
+bias + L2 normalize + BN statistics), 499.1 MB per launch against 8 TB/s. Both use HIP
+events recorded on the launching stream around each launch inside the timed region;
+`traffic` is the per-launch fabric traffic from rocprofv3 PMC passes
+(profiles/traffic_r01.json, tools/traffic.py).
 """
 from __future__ import annotations
 
@@ -32,6 +37,9 @@ sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md)
+X6_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6   # f32-equivalent ceiling of the 6-product bf16 split GEMM
+TRAFFIC_FILE = "traffic_r01.json"
 METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"
 
 
@@ -76,7 +84,7 @@ def main():
     import torch.distributed as dist
 
     import bgnn
-    from bgnn import fused, synthetic
+    from bgnn import _lib, fused, synthetic
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -138,15 +146,17 @@ def main():
     agg_ms = avg_ms("sage_fwd")
     agg_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
     agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_sage_fwd.json")
+    traffic = {}
+    tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     if os.path.exists(tpath):
         try:
-            traffic = json.load(open(tpath)).get("bytes_per_launch")
-        except (ValueError, OSError):
-            traffic = None
+            traffic = {k: v["bytes_per_launch"] for k, v in json.load(open(tpath))["kernels"].items()}
+        except (ValueError, OSError, KeyError):
+            traffic = {}
     gemm_ms = avg_ms("gemm_fwd")
     gemm_flop = 2.0 * N * (2 * H) * H
+    x6 = _lib.query("bgnn_get_tuning", 5) == 1
+    gemm_peak = X6_PEAK_TFS if (x6 and args.gemm == "hip") else FP32_MFMA_PEAK_TFS
     gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
     graphs = 16 * world * args.steps
     out = {
@@ -176,25 +186,33 @@ def main():
             "gemm": args.gemm,
         },
         "roofline": {
-            "kernel": "bgnn_sage_fwd (k_seg_light<4,2,64,SUM,SAGE> [+chunk/combine for super nodes])",
+            "kernel": (("bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<0,1,256,128,4,2> (f32-accurate bf16x6)"
+                        if x6 else "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_f32 (f32 MFMA)")
+                       if args.gemm == "hip" else "torch.mm"),
+            "bound": "mfma",
+            "achieved": round(gemm_tfs, 2),
+            "peak": gemm_peak,
+            "unit": "TFLOP/s",
+            "frac": round(gemm_tfs / gemm_peak, 4),
+            "traffic": traffic.get("gemm_fwd") if x6 and args.gemm == "hip" else None,
+            "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per f32 product" if gemm_peak == X6_PEAK_TFS
+                           else "f32 dense MFMA"),
+            "f32_mfma_peak": FP32_MFMA_PEAK_TFS,
+            "algorithmic_flop": gemm_flop,
+            "avg_launch_ms": round(gemm_ms, 5),
+            "launches": len(timers.get("gemm_fwd", [])),
+        },
+        "roofline_hbm": {
+            "kernel": "bgnn_sage_fwd (k_seg_sweep<2,0,1,8>, SAGE epilogue [+chunk/combine for super nodes])",
             "bound": "hbm",
             "achieved": round(agg_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(agg_gbs / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
+            "traffic": traffic.get("sage_fwd"),
             "algorithmic_bytes": agg_bytes,
             "avg_launch_ms": round(agg_ms, 5),
             "launches": len(timers.get("sage_fwd", [])),
-        },
-        "roofline_mfma": {
-            "kernel": "bgnn_gemm_f32 forward z = x [W_l;W_r]^T" if args.gemm == "hip" else "torch.mm",
-            "bound": "mfma",
-            "achieved": round(gemm_tfs, 2),
-            "peak": FP32_MFMA_PEAK_TFS,
-            "unit": "TFLOP/s",
-            "frac": round(gemm_tfs / FP32_MFMA_PEAK_TFS, 4),
-            "avg_launch_ms": round(gemm_ms, 5),
         },
         "spmm_bwd_avg_ms": round(avg_ms("spmm_bwd"), 5),
         "final_loss": loss_v,

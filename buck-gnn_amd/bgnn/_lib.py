@@ -47,6 +47,7 @@ class CsrStruct(ctypes.Structure):
 SIGNATURES = {
     "bgnn_abi_version": (c_i32, []),
     "bgnn_last_error_string": (ctypes.c_char_p, []),
+    "bgnn_get_tuning": (c_i32, [c_i32]),
     "bgnn_set_tuning": (c_i32, [c_i32, c_i32]),
     "bgnn_graph_build_ws_bytes": (c_sz, [c_i64, c_i64]),
     "bgnn_graph_build": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p]),
@@ -57,7 +58,8 @@ SIGNATURES = {
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
                               c_p, c_p]),
     "bgnn_sage_fwd_slots": (c_i32, [c_i64]),
-    "bgnn_sage_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "bgnn_sage_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p,
+                              c_p, c_p]),
     "bgnn_bn_finalize": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
                                  c_p]),
     "bgnn_bn_eval_coeffs": (c_i32, [c_i32, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p]),
@@ -69,6 +71,8 @@ SIGNATURES = {
                                    c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
     "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
+    "bgnn_gemm_f32_planes": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,
+                                     c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_sz, c_p]),
     "bgnn_gemm_f32_ex": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p,
                                  c_i64, c_p, c_i32, c_p, c_sz, c_p]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,

@@ -6,7 +6,8 @@ One autograd node per layer computes, for train or eval mode,
 
 with SAGEConv(aggr in {add, sum, mean}, normalize=True) evaluated transform-first:
 
-    z   = x_prev · [W_l ; W_r]^T                 one fp32 MFMA GEMM, [N, 2H]
+    z   = x_prev · [W_l ; W_r]^T                 one fp32 MFMA GEMM, stored as planes
+                                                  z_l [N, H] and z_r [N, H]
     h_i = AGG_{j->i} z_l[j] + z_r[i] + b_l        (= lin_l(AGG x) + lin_r(x): AGG is linear)
     o_i = h_i / max(||h_i||, 1e-12)               fused into the aggregation kernel,
                                                   which also emits BatchNorm partial sums
@@ -25,6 +26,16 @@ from .graph import Graph, _stream, require_cuda
 # "hip" = bgnn_gemm_f32 (hand-written f32 MFMA); "torch" = torch.mm (rocBLAS/hipBLASLt),
 # kept only for A/B measurement. Both run on the GPU.
 GEMM_BACKEND = "hip"
+
+# z = [z_l | z_r] and dz = [dz_l | dh] are stored either interleaved ([N, 2H], row i holds
+# both halves) or as two dense [N, H] planes (needs H % PLANE_TILE == 0, the GEMM tile width).
+# Measured on MI355X (cfg2, tools/tune_agg.py + tools/ab_step.py): the forward aggregation is
+# 5% faster on interleaved z (z_l[i], z_r[i] in one DRAM page), the transpose aggregation 4%
+# faster on dz planes, but the plane-operand GEMMs lose more than that: whole step 18.83 ms
+# interleaved vs 18.92 (dz planes) / 19.12 (z planes) / 19.23 (both).
+PLANE_TILE = 128
+Z_PLANES = False
+DZ_PLANES = False
 
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
@@ -51,9 +62,38 @@ class _timed:
         return False
 
 
-def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool, trans_b: bool, out: torch.Tensor = None,
-         beta: float = 0.0, alpha: float = 1.0, bias: torch.Tensor = None, relu: bool = False) -> torch.Tensor:
-    """C = act(alpha * op(a) @ op(b) + beta * C + bias) (fp32, row-major operands, unit column stride)."""
+class Planes:
+    """A row-major matrix [rows, P*blk] stored as P contiguous [rows, blk] planes (tensor t of
+    shape [P, rows, blk]). Used for z = [z_l | z_r] and dz = [dz_l | dh], whose halves the
+    aggregation kernels read as separate dense arrays."""
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        if t.dim() != 3 or not t.is_contiguous():
+            raise ValueError("Planes: need a contiguous [P, rows, blk] tensor")
+        self.t = t
+
+    def size(self, d):
+        return self.t.size(1) if d == 0 else self.t.size(0) * self.t.size(2)
+
+    def dense(self) -> torch.Tensor:
+        return self.t.permute(1, 0, 2).reshape(self.size(0), self.size(1))
+
+
+def _operand(x):
+    """(ptr, ld, blk, pstride) of a dense tensor or Planes operand."""
+    if isinstance(x, Planes):
+        P, R, blk = x.t.shape
+        return x.t.data_ptr(), blk, (blk if P > 1 else 0), R * blk
+    if x.stride(1) != 1:
+        raise ValueError("gemm: operands must have unit column stride")
+    return x.data_ptr(), x.stride(0), 0, 0
+
+
+def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float = 0.0, alpha: float = 1.0,
+         bias: torch.Tensor = None, relu: bool = False):
+    """C = act(alpha * op(a) @ op(b) + beta * C + bias) (fp32, row-major operands, unit column
+    stride). `a` and `out` may be Planes (bgnn_gemm_f32_planes)."""
     M = a.size(1) if trans_a else a.size(0)
     K = a.size(0) if trans_a else a.size(1)
     N = b.size(0) if trans_b else b.size(1)
@@ -61,31 +101,36 @@ def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool, trans_b: bool, out: to
     if K != Kb:
         raise ValueError(f"gemm: inner dims differ ({K} vs {Kb})")
     if out is None:
-        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+        out = torch.empty(M, N, dtype=torch.float32, device=b.device)
         beta = 0.0
+    if out.size(0) != M or out.size(1) != N:
+        raise ValueError(f"gemm: out is {out.size(0)}x{out.size(1)}, expected {M}x{N}")
     if GEMM_BACKEND == "torch":
-        ra = a.t() if trans_a else a
+        ad = a.dense() if isinstance(a, Planes) else a
+        od = out.dense() if isinstance(out, Planes) else out
+        ra = ad.t() if trans_a else ad
         rb = b.t() if trans_b else b
         if beta == 0.0:
-            torch.mm(ra, rb, out=out)
+            torch.mm(ra, rb, out=od)
             if alpha != 1.0:
-                out.mul_(alpha)
+                od.mul_(alpha)
         else:
-            out.mul_(beta).addmm_(ra, rb, alpha=alpha)
+            od.mul_(beta).addmm_(ra, rb, alpha=alpha)
         if bias is not None:
-            out.add_(bias)
+            od.add_(bias)
         if relu:
-            out.relu_()
+            od.relu_()
+        if isinstance(out, Planes):
+            out.t.copy_(od.view(M, out.t.size(0), out.t.size(2)).permute(1, 0, 2))
         return out
-    for t, nm in ((a, "A"), (b, "B"), (out, "C")):
-        if t.stride(1) != 1:
-            raise ValueError(f"gemm: {nm} must have unit column stride")
+    pa, lda, a_blk, a_ps = _operand(a)
+    pb, ldb, _, _ = _operand(b)
+    pc, ldc, c_blk, c_ps = _operand(out)
     ws_bytes = _lib.query("bgnn_gemm_ws_bytes", M, N, K, int(trans_a), int(trans_b))
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=a.device) if ws_bytes else None
-    _lib.call("bgnn_gemm_f32_ex", int(trans_a), int(trans_b), M, N, K, float(alpha), a.data_ptr(), a.stride(0),
-              b.data_ptr(), b.stride(0), float(beta), out.data_ptr(), out.stride(0),
-              None if bias is None else bias.data_ptr(), int(relu), None if ws is None else ws.data_ptr(),
-              ws_bytes, _stream())
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=b.device) if ws_bytes else None
+    _lib.call("bgnn_gemm_f32_planes", int(trans_a), int(trans_b), M, N, K, float(alpha), pa, lda, a_blk, a_ps,
+              pb, ldb, float(beta), pc, ldc, c_blk, c_ps, None if bias is None else bias.data_ptr(), int(relu),
+              None if ws is None else ws.data_ptr(), ws_bytes, _stream())
     return out
 
 
@@ -162,8 +207,15 @@ class SageLayerFn(torch.autograd.Function):
         dev = x_prev.device
         x_prev = x_prev.contiguous()
         wcat = torch.cat([w_l, w_r], 0).contiguous()             # [2H, H]
+        planes = Z_PLANES and H % PLANE_TILE == 0
         with _timed("gemm_fwd"):
-            z = gemm(x_prev, wcat, trans_a=False, trans_b=True)   # [N, 2H]
+            if planes:   # z = [z_l ; z_r] as two dense [N, H] planes
+                z = torch.empty(2, N, H, dtype=torch.float32, device=dev)
+                gemm(x_prev, wcat, trans_a=False, trans_b=True, out=Planes(z))
+                zl, zr, ldz = z[0], z[1], H
+            else:        # interleaved [N, 2H]
+                z = gemm(x_prev, wcat, trans_a=False, trans_b=True)
+                zl, zr, ldz = z, z[:, H:], 2 * H
         o = torch.empty(N, H, dtype=torch.float32, device=dev)
         nrm = torch.empty(N, dtype=torch.float32, device=dev)
         slots = _lib.query("bgnn_sage_fwd_slots", N) + graph.fwd.plan.n_heavy
@@ -172,9 +224,9 @@ class SageLayerFn(torch.autograd.Function):
                 if graph.fwd.plan.n_chunks else None)
         s = _stream()
         with _timed("sage_fwd"):
-            _lib.call("bgnn_sage_fwd", graph.fwd.ref(), z.data_ptr(), z.stride(0), b_l.data_ptr(), H, cfg.reduce,
-                      o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part), s)
-        del z
+            _lib.call("bgnn_sage_fwd", graph.fwd.ref(), zl.data_ptr(), ldz, zr.data_ptr(), ldz, b_l.data_ptr(), H,
+                      cfg.reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part), s)
+        del z, zl, zr
         scale = shift = mean = invstd = None
         if cfg.bn:
             scale = torch.empty(H, dtype=torch.float32, device=dev)
@@ -226,8 +278,13 @@ class SageLayerFn(torch.autograd.Function):
                 sum_g2, sum_g2xhat = sums[0], sums[1]
             else:
                 sum_g2 = sum_g2xhat = torch.zeros(H, dtype=torch.float32, device=dev)
-        dz = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)
-        dh = dz[:, H:]
+        planes = DZ_PLANES and H % PLANE_TILE == 0
+        if planes:   # dz = [dz_l ; dh] as two dense [N, H] planes
+            dzt = torch.empty(2, N, H, dtype=torch.float32, device=dev)
+            dz, dzl, dh, lddz = Planes(dzt), dzt[0], dzt[1], H
+        else:
+            dz = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)
+            dzl, dh, lddz = dz, dz[:, H:], 2 * H
         gskip = torch.empty(N, H, dtype=torch.float32, device=dev) if cfg.skip else None
         rs = _lib.query("bgnn_rows_slots", N)
         part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
@@ -235,7 +292,7 @@ class SageLayerFn(torch.autograd.Function):
                   _ptr(scale) if bn else None, _ptr(shift) if bn else None,
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
-                  float(cfg.p), cfg.seed, int(cfg.skip), N, H, dh.data_ptr(), dz.stride(0), _ptr(gskip),
+                  float(cfg.p), cfg.seed, int(cfg.skip), N, H, dh.data_ptr(), lddz, _ptr(gskip),
                   part_db.data_ptr(), s)
         db = torch.empty(H, dtype=torch.float32, device=dev)
         _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
@@ -244,7 +301,7 @@ class SageLayerFn(torch.autograd.Function):
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("spmm_bwd"):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
-                      dh.data_ptr(), dz.stride(0), H, cfg.reduce, None, dz.data_ptr(), dz.stride(0), _ptr(part), s)
+                      dh.data_ptr(), lddz, H, cfg.reduce, None, dzl.data_ptr(), lddz, _ptr(part), s)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         if gskip is not None:
             dx = gemm(dz, wcat, trans_a=False, trans_b=False, out=gskip, beta=1.0)

@@ -78,4 +78,8 @@ static inline uint32_t dropout_threshold(float p) {
     return (uint32_t)t;
 }
 
+// GEMM kernel family (gemm.hip): 0 = f32 MFMA, 1 = bf16x6 (f32-accurate split products)
+void set_gemm_mode(int mode);
+int gemm_mode();
+
 }  // namespace bgnn

@@ -15,23 +15,9 @@
 // pad of 2 floats makes those scalar stores conflict-free). Tile order is remapped
 // so each XCD owns a contiguous band of output rows (shared A panels stay in its L2).
 #include "common.h"
+#include "gemm_common.h"
 
 namespace bgnn {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-struct GemmArgs {
-    const float* A;
-    const float* B;
-    float* C;
-    float* ws;
-    int64_t M, N, K, lda, ldb, ldc;
-    float alpha, beta;
-    int64_t kchunk;   // K range per split-K slice (multiple of BK)
-    int split;
-    const float* bias;   // epilogue: + bias[col] (may be NULL)
-    int relu;            // epilogue: max(., 0)
-};
 
 // LDS row pad (floats): a K-contiguous operand is transposed by scalar ds_write_b32
 // into a [BK][R + PAD] image; PAD is chosen so one wave's 32-lane store groups hit 32
@@ -145,11 +131,13 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
     // interior tile with whole, aligned K slices: unguarded loads (uniform branch)
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % BK == 0);
     auto load_ab = [&](int64_t k0) {
+        // A planes are cut along K (TA = 0, per slice) or along M (TA = 1, per tile)
+        const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
         if (full) {
-            load_slice<AK, BM, BK, NT, true>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
+            load_slice<AK, BM, BK, NT, true>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra);
             load_slice<BKc, BN, BK, NT, true>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
         } else {
-            load_slice<AK, BM, BK, NT>(g.A, g.lda, g.M, m0, k0, ke, a_vec, ra);
+            load_slice<AK, BM, BK, NT>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra);
             load_slice<BKc, BN, BK, NT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb);
         }
     };
@@ -199,7 +187,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
     }
 
     // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-    float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)blockIdx.y * g.M * g.N : g.C;
+    float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)blockIdx.y * g.M * g.N
+                                          : const_cast<float*>(plane_base(g.C, n0, g.c_blk, g.c_pstride));
     const int64_t ldd = g.split > 1 ? g.N : g.ldc;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -227,7 +216,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
 
 __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ ws, int split, int64_t M,
                                                        int64_t N, float alpha, float beta, float* __restrict__ C,
-                                                       int64_t ldc, const float* __restrict__ bias, int relu) {
+                                                       int64_t ldc, const float* __restrict__ bias, int relu,
+                                                       int64_t c_blk, int64_t c_pstride) {
     const int64_t total = M * N;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -235,10 +225,11 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
         for (int k = 0; k < split; ++k) s += ws[(int64_t)k * total + i];
         const int64_t r = i / N, c = i % N;
         float v = alpha * s;
-        if (beta != 0.f) v += beta * C[r * ldc + c];
+        float* Cp = c_blk > 0 ? C + (c / c_blk) * (c_pstride - c_blk) : C;
+        if (beta != 0.f) v += beta * Cp[r * ldc + c];
         if (bias) v += bias[c];
         if (relu) v = fmaxf(v, 0.f);
-        C[r * ldc + c] = v;
+        Cp[r * ldc + c] = v;
     }
 }
 
@@ -260,13 +251,25 @@ constexpr GemmCfg kCfgs[] = {
 constexpr int kNumCfgs = 9;
 static int g_gemm_cfg = -1;   // -1 = automatic
 static int g_gemm_abl = 0;    // ablation (measurement only)
+static int g_gemm_mode = 1;   // 0 = f32 MFMA kernel, 1 = bf16x6 kernel (gemm_x6.hip, default:
+                              // 1.4x faster on the SAGE shapes at lower error, tools/tune_gemm.py)
+
+void set_gemm_mode(int mode) { g_gemm_mode = mode; }
+int gemm_mode() { return g_gemm_mode; }
+
+// bf16x6 tile choice (tools/tune_gemm.py)
+inline int pick_x6_cfg(int64_t M, int64_t N, int64_t K) {
+    if (M >= 4096 && N >= 128) return 1;              // tall (fwd / dgrad)
+    if (M >= 256 && N >= 128 && K >= 8192) return 1;  // short and deep (wgrad, split-K)
+    return 0;
+}
 
 // Measured on MI355X (tools/tune_gemm.py, SAGE layer shapes): 256x128 tiles of 8 waves for
 // the tall GEMMs (fwd 118 TF, dgrad 118 TF), 256x256 tiles of 8 waves + split-K for the
 // short-and-deep weight gradient (125 TF); small problems keep the 128x128 tile.
 inline int pick_cfg(int64_t M, int64_t N, int64_t K, int ta, int tb) {
     (void)ta; (void)tb;
-    if (g_gemm_cfg >= 0) return g_gemm_cfg;
+    if (g_gemm_cfg >= 0) return g_gemm_cfg % kNumCfgs;
     if (M >= 256 && N >= 256 && K >= 8192 && M * N <= (int64_t)4096 * 4096) return 1;
     if (M >= 4096 && N >= 128) return 3;
     return 0;
@@ -308,56 +311,105 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 using namespace bgnn;
 
 extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
-    BGNN_REQUIRE(cfg >= -1 && cfg < kNumCfgs + 300, "gemm: config %d out of range", cfg);
+    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 500,
+                 "gemm: config %d out of range", cfg);
     g_gemm_abl = cfg / 100;
     g_gemm_cfg = cfg % 100;
     return BGNN_OK;
 }
 
+// Launch plan of one GEMM call: kernel family, tile config and split-K factor.
+struct Plan {
+    int x6;            // 1 = bf16x6 kernel (gemm_x6.hip), 0 = f32 MFMA
+    int cfg;           // index into kX6Cfgs / kCfgs
+    int bm, bn, bk;    // tile
+    int split;
+};
+
+static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk) {
+    Plan p{};
+    auto planes_ok = [&](int bm, int bn, int bk) {
+        return (a_blk == 0 || a_blk % (ta ? bm : bk) == 0) && (c_blk == 0 || c_blk % bn == 0);
+    };
+    if (g_gemm_mode == 1) {
+        p.x6 = 1;
+        p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K);
+        if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
+        p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
+        p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves,
+                                                 kX6Cfgs[p.cfg].blocks_per_cu});
+    } else {
+        p.cfg = pick_cfg(M, N, K, ta, tb);
+        // plane blocks must be whole multiples of the tile along the split dimension; fall back
+        // to the smallest tile when the shape-picked one does not divide them
+        if (!planes_ok(kCfgs[p.cfg].bm, kCfgs[p.cfg].bn, kCfgs[p.cfg].bk)) p.cfg = 0;
+        const GemmCfg& c = kCfgs[p.cfg];
+        p.bm = c.bm; p.bn = c.bn; p.bk = c.bk;
+        p.split = choose_split(M, N, K, c);
+    }
+    return p;
+}
+
 extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb) {
-    const int s = choose_split(M, N, K, kCfgs[pick_cfg(M, N, K, ta, tb)]);
+    const int s = make_plan(M, N, K, ta, tb, 0, 0).split;
     return s > 1 ? (size_t)s * (size_t)M * (size_t)N * sizeof(float) : 0;
+}
+
+extern "C" int bgnn_gemm_f32_planes(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
+                                    const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
+                                    int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
+                                    int64_t c_pstride, const float* bias, int32_t relu, void* ws, size_t ws_bytes,
+                                    void* stream) {
+    BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
+    BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
+    const int64_t a_inner = a_blk > 0 ? a_blk : (ta ? M : K);
+    BGNN_REQUIRE((ta == 0 && lda >= a_inner) || (ta == 1 && lda >= a_inner) || M == 0 || K == 0, "gemm: bad lda");
+    BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm: bad ldb");
+    BGNN_REQUIRE(ldc >= (c_blk > 0 ? c_blk : N) || M == 0, "gemm: bad ldc");
+    BGNN_REQUIRE(a_blk >= 0 && c_blk >= 0, "gemm: negative plane block");
+    if (M == 0 || N == 0) return BGNN_OK;
+    const Plan pl = make_plan(M, N, K, ta, tb, a_blk, c_blk);
+    BGNN_REQUIRE((a_blk == 0 || a_blk % (ta ? pl.bm : pl.bk) == 0) && (c_blk == 0 || c_blk % pl.bn == 0),
+                 "gemm: plane blocks (a_blk %lld, c_blk %lld) must be multiples of the %dx%dx%d tile",
+                 (long long)a_blk, (long long)c_blk, pl.bm, pl.bn, pl.bk);
+    const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
+    BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
+    hipStream_t s = as_stream(stream);
+    int split = pl.split;
+    if (split > 1 && (ws == nullptr || ws_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
+    GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
+               a_blk, a_pstride, c_blk, c_pstride};
+    int64_t kc = (K + split - 1) / split;
+    kc = (kc + pl.bk - 1) / pl.bk * pl.bk;
+    g.kchunk = kc > 0 ? kc : pl.bk;
+    dim3 grid((unsigned)tiles, split);
+    if (pl.x6) launch_x6(ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
+    else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
+    else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
+    else if (ta == 1 && tb == 0) launch_cfg<1, 0>(pl.cfg, grid, s, g);
+    else launch_cfg<1, 1>(pl.cfg, grid, s, g);
+    BGNN_CHECK_LAUNCH();
+    if (split > 1) {
+        int64_t blocks = (M * N + 255) / 256;
+        if (blocks > 4096) blocks = 4096;
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, split, M, N,
+                           alpha, beta, C, ldc, bias, relu, c_blk, c_pstride);
+        BGNN_CHECK_LAUNCH();
+    }
+    return BGNN_OK;
 }
 
 extern "C" int bgnn_gemm_f32_ex(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
                                 const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                                 int64_t ldc, const float* bias, int32_t relu, void* ws, size_t ws_bytes,
                                 void* stream) {
-    BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
-    BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
-    BGNN_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M) || M == 0 || K == 0, "gemm: bad lda");
-    BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm: bad ldb");
-    BGNN_REQUIRE(ldc >= N || M == 0, "gemm: bad ldc");
-    if (M == 0 || N == 0) return BGNN_OK;
-    const int cfg = pick_cfg(M, N, K, ta, tb);
-    const GemmCfg& c = kCfgs[cfg];
-    const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
-    BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
-    hipStream_t s = as_stream(stream);
-    int split = choose_split(M, N, K, c);
-    if (split > 1 && (ws == nullptr || ws_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
-    GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu};
-    int64_t kc = (K + split - 1) / split;
-    kc = (kc + c.bk - 1) / c.bk * c.bk;
-    g.kchunk = kc > 0 ? kc : c.bk;
-    dim3 grid((unsigned)tiles, split);
-    if (ta == 0 && tb == 0) launch_cfg<0, 0>(cfg, grid, s, g);
-    else if (ta == 0 && tb == 1) launch_cfg<0, 1>(cfg, grid, s, g);
-    else if (ta == 1 && tb == 0) launch_cfg<1, 0>(cfg, grid, s, g);
-    else launch_cfg<1, 1>(cfg, grid, s, g);
-    BGNN_CHECK_LAUNCH();
-    if (split > 1) {
-        int64_t blocks = (M * N + 255) / 256;
-        if (blocks > 4096) blocks = 4096;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, split, M, N,
-                           alpha, beta, C, ldc, bias, relu);
-        BGNN_CHECK_LAUNCH();
-    }
-    return BGNN_OK;
+    return bgnn_gemm_f32_planes(ta, tb, M, N, K, alpha, A, lda, 0, 0, B, ldb, beta, C, ldc, 0, 0, bias, relu, ws,
+                                ws_bytes, stream);
 }
 
 extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                              int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc, void* ws,
                              size_t ws_bytes, void* stream) {
-    return bgnn_gemm_f32_ex(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr, 0, ws, ws_bytes, stream);
+    return bgnn_gemm_f32_planes(ta, tb, M, N, K, alpha, A, lda, 0, 0, B, ldb, beta, C, ldc, 0, 0, nullptr, 0, ws,
+                                ws_bytes, stream);
 }

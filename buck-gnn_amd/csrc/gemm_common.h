@@ -1,0 +1,43 @@
+// Shared GEMM argument block and plane-split addressing (gemm.hip, gemm_x6.hip).
+#pragma once
+#include "common.h"
+
+namespace bgnn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+    const float* A;
+    const float* B;
+    float* C;
+    float* ws;
+    int64_t M, N, K, lda, ldb, ldc;
+    float alpha, beta;
+    int64_t kchunk;   // K range per split-K slice (multiple of BK)
+    int split;
+    const float* bias;   // epilogue: + bias[col] (may be NULL)
+    int relu;            // epilogue: max(., 0)
+    // plane-split storage (0 = dense): A's contiguous dim (K if !TA, M if TA) and C's N dim
+    // are cut into blocks of a_blk / c_blk stored a_pstride / c_pstride elements apart
+    int64_t a_blk, a_pstride, c_blk, c_pstride;
+};
+
+// Base pointer that makes plane-split storage addressable with global coordinates:
+// element with split-dim index x lives at P + (x / blk) * pstride + (x % blk); for all x of
+// one plane that is Q + x with Q = P + plane * (pstride - blk).
+__device__ __forceinline__ const float* plane_base(const float* P, int64_t x0, int64_t blk, int64_t pstride) {
+    if (blk <= 0) return P;
+    const int64_t plane = x0 / blk;
+    return P + plane * (pstride - blk);
+}
+
+// f32-accurate GEMM on bf16 MFMAs (gemm_x6.hip): launches the main kernel of tile config
+// `cfg` (index into kX6Cfgs) on grid (tiles, split); abl != 0 selects a timing ablation.
+struct X6Cfg {
+    int bm, bn, waves, blocks_per_cu;
+};
+extern const X6Cfg kX6Cfgs[];
+extern const int kNumX6Cfgs;
+void launch_x6(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
+
+}  // namespace bgnn

@@ -51,7 +51,9 @@ struct SegArgs {
     float* nrm;
     float* bn_partial;  // [slots, 2, H]
     int32_t light_slots;
+    int32_t nt;         // stream-once data (z_r rows, output rows) with non-temporal hints
 };
+
 
 template <int VEC>
 struct Vec {
@@ -96,6 +98,20 @@ __device__ __forceinline__ void sti(int32_t* p, const int32_t (&o)[VEC]) {
     } else {
         *p = o[0];
     }
+}
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ Vec<4> ld_nt(const float* p) {
+    const f32x4_t q = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p));
+    Vec<4> v;
+    v.f[0] = q[0]; v.f[1] = q[1]; v.f[2] = q[2]; v.f[3] = q[3];
+    return v;
+}
+
+__device__ __forceinline__ void st_nt(float* p, const Vec<4>& v) {
+    f32x4_t q = {v.f[0], v.f[1], v.f[2], v.f[3]};
+    __builtin_nontemporal_store(q, reinterpret_cast<f32x4_t*>(p));
 }
 
 // Per-lane accumulator for NV vectors of VEC floats.
@@ -203,7 +219,12 @@ __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& 
             if constexpr (OP == OP_MAX) t = (deg > 0) ? t : 0.f;
             o.f[k] = t * sc;
         }
-        st<VEC>(A.out + r * A.ldo + cpos[v], o);
+        if constexpr (VEC == 4) {
+            if (A.nt) st_nt(A.out + r * A.ldo + cpos[v], o);
+            else st<VEC>(A.out + r * A.ldo + cpos[v], o);
+        } else {
+            st<VEC>(A.out + r * A.ldo + cpos[v], o);
+        }
         if constexpr (OP == OP_MAX) {
             if (A.arg) {
                 int32_t gi[VEC];
@@ -541,13 +562,14 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
             if (deg > chunk) continue;   // heavy row: k_seg_chunk + k_seg_combine
             Acc<4, NV, OP> acc;
             acc.init();
+            // issue the row's stream-once z_r load first, so it completes under the gathers
+            // (one memory round trip per light row)
             Vec<4> zr[NV];
-            if (deg > 0) sweep_gather<NV, OP, U>(A, acc, cur, beg, deg, 0, cpos, cok);
             if constexpr (EPI == EPI_SAGE) {
 #pragma unroll
-                for (int v = 0; v < NV; ++v) zr[v] = ld<4>(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
+                for (int v = 0; v < NV; ++v) zr[v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
             }
-            for (int e0 = U; e0 < deg; e0 += U) sweep_gather<NV, OP, U>(A, acc, cur, beg, deg, e0, cpos, cok);
+            for (int e0 = 0; e0 < deg; e0 += U) sweep_gather<NV, OP, U>(A, acc, cur, beg, deg, e0, cpos, cok);
             if constexpr (EPI == EPI_SAGE) {
                 const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
                 float h[NV][4];
@@ -572,7 +594,7 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
                         bs[v][q] += o.f[q];
                         bq[v][q] += o.f[q] * o.f[q];
                     }
-                    st<4>(A.out + r * A.ldo + cpos[v], o);
+                    st_nt(A.out + r * A.ldo + cpos[v], o);
                 }
                 if (lane == 0) A.nrm[r] = n;
             } else {
@@ -606,6 +628,7 @@ constexpr int kMaxLightBlocks = 1024;
 // Tuning knobs (process-wide; defaults are the production choice; see bgnn_set_tuning).
 static int g_seg_kernel = 0;     // 0 = sweep kernel where applicable, 1 = blocked kernel
 static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
+static int g_seg_nt = 1;         // non-temporal hints on stream-once data (default on: +8 % fwd)
 static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto:
                                  // 8 with the SAGE epilogue (register-bound), 12 otherwise)
 
@@ -667,6 +690,7 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
         blocks = light_grid(A.n_rows, kWave / LPR, max_blocks, &rpb);
     }
     A.rows_per_block = rpb;
+    A.nt = g_seg_nt;
     if (blocks_out) *blocks_out = blocks;
     A.light_slots = (int32_t)blocks;
     if (A.n_rows > 0) {
@@ -792,6 +816,17 @@ extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, con
 
 extern "C" int32_t bgnn_sage_fwd_slots(int64_t n_rows) { return (int32_t)sweep_grid(n_rows); }
 
+extern "C" int32_t bgnn_get_tuning(int32_t knob) {
+    switch (knob) {
+        case BGNN_TUNE_SEG_KERNEL: return g_seg_kernel;
+        case BGNN_TUNE_SEG_BLOCKS: return g_seg_blocks;
+        case BGNN_TUNE_SEG_U: return g_seg_u;
+        case BGNN_TUNE_SEG_NT: return g_seg_nt;
+        case BGNN_TUNE_GEMM_MODE: return gemm_mode();
+        default: return -1;
+    }
+}
+
 extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
     switch (knob) {
         case BGNN_TUNE_SEG_KERNEL: g_seg_kernel = value ? 1 : 0; return BGNN_OK;
@@ -803,26 +838,31 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             BGNN_REQUIRE(value == 0 || value == 8 || value == 12, "set_tuning: U must be 0 (auto), 8 or 12");
             g_seg_u = value;
             return BGNN_OK;
+        case BGNN_TUNE_SEG_NT: g_seg_nt = value ? 1 : 0; return BGNN_OK;
+        case BGNN_TUNE_GEMM_MODE:
+            BGNN_REQUIRE(value == 0 || value == 1, "set_tuning: gemm mode must be 0 (f32) or 1 (bf16x6)");
+            set_gemm_mode(value);
+            return BGNN_OK;
         default: return fail(BGNN_E_ARG, "set_tuning: unknown knob %d", knob);
     }
 }
 
-extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* z, int64_t ldz, const float* bias, int32_t H,
-                             int32_t reduce, float* o, float* nrm, float* bn_partial, float* partial,
-                             void* stream) {
+extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldzl, const float* zr, int64_t ldzr,
+                             const float* bias, int32_t H, int32_t reduce, float* o, float* nrm, float* bn_partial,
+                             float* partial, void* stream) {
     BGNN_REQUIRE(csr && csr->rowptr, "sage_fwd: null csr");
     BGNN_REQUIRE(H > 0 && H <= 512 && H % 4 == 0, "sage_fwd: H=%d unsupported (need H%%4==0, H<=512)", H);
-    BGNN_REQUIRE(ldz >= 2 * H && ldz % 4 == 0, "sage_fwd: ldz=%lld must be >= 2H and a multiple of 4",
-                 (long long)ldz);
+    BGNN_REQUIRE(ldzl >= H && ldzl % 4 == 0 && ldzr >= H && ldzr % 4 == 0,
+                 "sage_fwd: ldzl/ldzr must be >= H and multiples of 4");
     BGNN_REQUIRE(reduce == BGNN_REDUCE_SUM || reduce == BGNN_REDUCE_MEAN, "sage_fwd: reduce must be sum/mean");
-    BGNN_REQUIRE(aligned16(z) && aligned16(o) && aligned16(bias) && aligned16(bn_partial) &&
+    BGNN_REQUIRE(aligned16(zl) && aligned16(zr) && aligned16(o) && aligned16(bias) && aligned16(bn_partial) &&
                      (!partial || aligned16(partial)),
                  "sage_fwd: pointers must be 16-byte aligned");
     BGNN_REQUIRE(csr->n_chunks == 0 || partial, "sage_fwd: partial scratch required for heavy rows");
     SegArgs A = args_from_csr(csr);
     A.H = H;
-    A.x = z; A.ldx = ldz;
-    A.zr = z + H; A.ldzr = ldz;
+    A.x = zl; A.ldx = ldzl;
+    A.zr = zr; A.ldzr = ldzr;
     A.bias = bias;
     A.out = o; A.ldo = H;
     A.nrm = nrm;

@@ -60,6 +60,10 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_SEG_KERNEL 1   /* 0 = XCD-sweep light-row kernel (default), 1 = blocked */
 #define BGNN_TUNE_SEG_BLOCKS 2   /* sweep grid in blocks (default 1024)                   */
 #define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (default), 8, 12 */
+#define BGNN_TUNE_SEG_NT 4       /* non-temporal hints on stream-once rows (default 1)       */
+#define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6 f32-accurate (default) */
+/* Current value of a knob (-1 for an unknown knob). */
+int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);
 
 /* ------------------------------------------------------------------------
@@ -139,7 +143,7 @@ int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t*
 
 /* ------------------------------------------------------------------------
  * Fused SAGE layer (Models/BuckGNN.py:430-444, transform-first order):
- *   z = x · [W_l ; W_r]^T                   (bgnn_gemm_f32, [N, 2H], ld = ldz)
+ *   [z_l | z_r] = x · [W_l ; W_r]^T          (bgnn_gemm_f32_planes; two [N, H] planes)
  *   h_i = AGG_{j->i} z_l[j] + z_r[i] + b_l   (SUM or MEAN)
  *   o_i = h_i / max(||h_i||_2, 1e-12)        (SAGEConv normalize=True)
  *   BatchNorm statistics of o (train mode) as per-block partial sums.
@@ -147,8 +151,8 @@ int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t*
  *   n_slots = bgnn_sage_fwd_slots(N) + n_heavy.
  * ---------------------------------------------------------------------- */
 int32_t bgnn_sage_fwd_slots(int64_t n_rows);
-int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* z, int64_t ldz, const float* bias,
-                  int32_t H, int32_t reduce, float* o, float* nrm,
+int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldzl, const float* zr, int64_t ldzr,
+                  const float* bias, int32_t H, int32_t reduce, float* o, float* nrm,
                   float* bn_partial, float* partial, void* stream);
 
 /* BatchNorm1d finalize (train): sums the partials in fp64, writes
@@ -199,8 +203,12 @@ int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
                        float* gskip, float* partial_db, void* stream);
 
 /* ------------------------------------------------------------------------
- * fp32 GEMM on the gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain):
+ * fp32 GEMM (f32 operands, f32 result, f32 accumulation):
  *   C[M,N] = alpha * op(A)[M,K] · op(B)[K,N] + beta * C
+ * Two kernel families (BGNN_TUNE_GEMM_MODE): 1 (default) splits every operand exactly
+ * into three bf16 pieces and sums the six leading piece products on the bf16 MFMA
+ * (dropped terms <= 2^-23 |a||b| per product, measured error below the f32 MFMA's);
+ * 0 runs the f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain).
  * trans_a = 0: A is [M,K] row-major (lda >= K); 1: A is [K,M] row-major (lda >= M).
  * trans_b = 0: B is [K,N] row-major (ldb >= N);  1: B is [N,K] row-major (ldb >= K).
  * C is [M,N] row-major (ldc >= N). `ws` is scratch for split-K (may be NULL when
@@ -219,6 +227,16 @@ int bgnn_gemm_f32_ex(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int
                      float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
                      float beta, float* C, int64_t ldc, const float* bias, int32_t relu,
                      void* ws, size_t ws_bytes, void* stream);
+/* Plane-split operands (the SAGE layer's [z_l | z_r] and [dz_l | dh] kept as two
+ * contiguous [N, H] planes): A's contiguous dimension (K when trans_a = 0, M when
+ * trans_a = 1) is cut into blocks of a_blk elements stored a_pstride elements apart
+ * (element index x -> (x / a_blk) * a_pstride + x % a_blk); C's N dimension likewise with
+ * c_blk / c_pstride. 0 = dense. Blocks must be multiples of the kernel's tile. */
+int bgnn_gemm_f32_planes(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                         float alpha, const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride,
+                         const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                         int64_t c_blk, int64_t c_pstride, const float* bias, int32_t relu,
+                         void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

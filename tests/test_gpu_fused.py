@@ -70,6 +70,27 @@ def test_fused_layer_matches_oracle(dev, aggr, red, bn, training, skip, H):
         torch.testing.assert_close(rv.cpu(), t["rv"].detach().float(), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("z_planes,dz_planes", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("H", [128, 512])
+def test_fused_layer_layouts(dev, monkeypatch, z_planes, dz_planes, H):
+    """Every z / dz storage layout (interleaved [N, 2H] or two [N, H] planes) matches the oracle."""
+    monkeypatch.setattr(fused, "Z_PLANES", z_planes)
+    monkeypatch.setattr(fused, "DZ_PLANES", dz_planes)
+    test_fused_layer_matches_oracle(dev, "mean", 1, True, True, True, H)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("aggr,red", [("sum", 0), ("mean", 1)])
+def test_fused_layer_gemm_modes(dev, mode, aggr, red):
+    """The layer matches the oracle with either GEMM family (f32 MFMA / bf16x6)."""
+    from bgnn import _lib
+    _lib.call("bgnn_set_tuning", 5, mode)
+    try:
+        test_fused_layer_matches_oracle(dev, aggr, red, True, True, True, 512)
+    finally:
+        _lib.call("bgnn_set_tuning", 5, 1)
+
+
 def test_dropout_mask_fraction_and_backward_consistency(dev):
     H = 512
     b = S.make_batch(12, 2)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Same-process A/B of whole training steps (cfg2): alternates settings for R rounds of S
-steps and reports the median ms/step per setting. Settings are module attributes:
+steps and reports the median ms/step per setting. Settings are module attributes or C tuning knobs ("knob:5=1"):
     python tools/ab_step.py "bgnn.buckgnn.FUSED_ENCODER=True" "bgnn.buckgnn.FUSED_ENCODER=False"
 """
 import importlib
@@ -18,8 +18,12 @@ from bgnn import synthetic  # noqa: E402
 
 
 def apply(setting):
+    """'mod.attr=expr' sets a module attribute; 'knob:K=V' calls bgnn_set_tuning(K, V)."""
     for kv in setting.split(";"):
         k, v = kv.split("=")
+        if k.startswith("knob:"):
+            bgnn._lib.call("bgnn_set_tuning", int(k[5:]), int(v))
+            continue
         mod, attr = k.rsplit(".", 1)
         setattr(importlib.import_module(mod), attr, eval(v))
 

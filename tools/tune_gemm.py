@@ -1,6 +1,8 @@
 #!/usr/bin/env python
-"""A/B the f32 MFMA GEMM tile configurations (and torch.mm) on the SAGE layer shapes,
-interleaved in one process; median per-launch HIP-event time and TFLOP/s."""
+"""A/B the GEMM kernels and tile configurations (and torch.mm) on the SAGE layer shapes,
+interleaved in one process; median per-launch HIP-event time, TFLOP/s, and the error
+against an fp64 product as max_ij |c - c64|_ij / (|A| |B|)_ij.
+Variants: "3" = f32 MFMA config 3, "x1" = bf16x6 config 1, "torch" = torch.mm."""
 import argparse
 import os
 import statistics
@@ -21,7 +23,7 @@ SHAPES = {  # name: (M, N, K, trans_a, trans_b)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="0,1,2,3")
+    ap.add_argument("--cfgs", default="0,1,3,x0,x1,x2")
     ap.add_argument("--rounds", type=int, default=10)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -31,7 +33,13 @@ def main():
         a = torch.randn((K, M) if ta else (M, K), device=dev)
         b = torch.randn((N, K) if tb else (K, N), device=dev)
         ops[name] = (a, b, ta, tb, 2.0 * M * N * K)
-    variants = [int(c) for c in args.cfgs.split(",")] + ["torch"]
+    exact = {}
+    for name, (a, b, ta, tb, _) in ops.items():
+        A = a.double().t() if ta else a.double()
+        B = b.double().t() if tb else b.double()
+        exact[name] = (A @ B, A.abs() @ B.abs())
+    errs = {}
+    variants = args.cfgs.split(",") + ["torch"]
     times = {(v, n): [] for v in variants for n in SHAPES}
     ref = {}
     for rnd in range(args.rounds + 1):
@@ -41,7 +49,8 @@ def main():
                     fused.GEMM_BACKEND = "torch"
                 else:
                     fused.GEMM_BACKEND = "hip"
-                    _lib.call("bgnn_gemm_set_cfg", v)
+                    _lib.call("bgnn_set_tuning", 5, 1 if v.startswith("x") else 0)
+                    _lib.call("bgnn_gemm_set_cfg", int(v.lstrip("x")))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 c = fused.gemm(a, b, ta, tb)
@@ -50,18 +59,21 @@ def main():
                 if rnd:
                     times[(v, n)].append(e0.elapsed_time(e1))
                 else:
+                    c64, mag = exact[n]
+                    errs[(v, n)] = ((c.double() - c64).abs() / mag.clamp_min(1e-30)).max().item()
                     if n not in ref:
                         ref[n] = c
                     else:
                         err = (c - ref[n]).abs().max().item() / ref[n].abs().max().item()
-                        if err > 1e-5:
+                        if err > 1e-4:
                             print(f"MISMATCH cfg {v} {n}: rel {err:.2e}")
     _lib.call("bgnn_gemm_set_cfg", -1)
+    _lib.call("bgnn_set_tuning", 5, 0)
     for v in variants:
         line = f"cfg {str(v):6s}"
         for n, (a, b, ta, tb, fl) in ops.items():
             t = statistics.median(times[(v, n)])
-            line += f" | {n} {t*1e3:8.1f} us {fl/t/1e9:7.1f} TF"
+            line += f" | {n} {t*1e3:8.1f} us {fl/t/1e9:7.1f} TF err {errs[(v, n)]:.1e}"
         print(line)
 
 
