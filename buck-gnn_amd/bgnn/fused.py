@@ -36,6 +36,8 @@ GEMM_BACKEND = "hip"
 PLANE_TILE = 128
 Z_PLANES = False
 DZ_PLANES = False
+# dgrad B operand: transposed copy of [W_l;W_r] (K-contiguous loads) instead of strided reads
+DGRAD_WT = True
 
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
@@ -153,7 +155,10 @@ class LinearFn(torch.autograd.Function):
         g = g.contiguous()
         if ctx.relu:
             g = g * (y > 0)
-        dx = gemm(g, weight.contiguous(), trans_a=False, trans_b=False) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (gemm(g, weight.t().contiguous(), trans_a=False, trans_b=True) if DGRAD_WT
+                  else gemm(g, weight.contiguous(), trans_a=False, trans_b=False))
         dw = gemm(g, x, trans_a=True, trans_b=False)
         db = g.sum(0) if ctx.has_bias else None
         return dx, dw, db, None
@@ -303,10 +308,12 @@ class SageLayerFn(torch.autograd.Function):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
                       dh.data_ptr(), lddz, H, cfg.reduce, None, dzl.data_ptr(), lddz, _ptr(part), s)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
+        # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
+        wcat_t = wcat.t().contiguous() if DGRAD_WT else wcat
         if gskip is not None:
-            dx = gemm(dz, wcat, trans_a=False, trans_b=False, out=gskip, beta=1.0)
+            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, out=gskip, beta=1.0)
         else:
-            dx = gemm(dz, wcat, trans_a=False, trans_b=False)
+            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT)
         dw = gemm(dz, x_prev, trans_a=True, trans_b=False)      # [2H, H]
         dw_l, dw_r = dw[:H], dw[H:]
         has_affine = bn and gamma.numel() > 0

@@ -244,18 +244,17 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         }
         const uint4* as = As[cur];
         const uint4* bs = Bs[cur];
-#pragma unroll
-        for (int kk = 0; kk < X6_BK / 16; ++kk) {
+        bf16x8 a[X6_BK / 16][TM][3], b[X6_BK / 16][TN][3];
+        auto read_frags = [&](int kk) {
             const int c = 2 * kk + lh;
-            bf16x8 a[TM][3], b[TN][3];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int row = wm * (BM / WM) + i * 32 + li;
                 const int pos = x6_pos(row, c);
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    if constexpr (ABL == 4) a[i][p] = as_bf16x8(make_uint4(pos + p, kk, i, (int)kt));
-                    else a[i][p] = as_bf16x8(as[p * BM * 4 + pos]);
+                    if constexpr (ABL == 4) a[kk][i][p] = as_bf16x8(make_uint4(pos + p, kk, i, (int)kt));
+                    else a[kk][i][p] = as_bf16x8(as[p * BM * 4 + pos]);
                 }
             }
 #pragma unroll
@@ -264,11 +263,15 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
                 const int pos = x6_pos(row, c);
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    if constexpr (ABL == 4) b[j][p] = as_bf16x8(make_uint4(pos - p, kk, j, (int)kt));
-                    else b[j][p] = as_bf16x8(bs[p * BN * 4 + pos]);
+                    if constexpr (ABL == 4) b[kk][j][p] = as_bf16x8(make_uint4(pos - p, kk, j, (int)kt));
+                    else b[kk][j][p] = as_bf16x8(bs[p * BN * 4 + pos]);
                 }
             }
-            x6_mma<TM, TN>(acc, a, b);
+        };
+#pragma unroll
+        for (int kk = 0; kk < X6_BK / 16; ++kk) {
+            read_frags(kk);
+            x6_mma<TM, TN>(acc, a[kk], b[kk]);
         }
         __syncthreads();
     }
