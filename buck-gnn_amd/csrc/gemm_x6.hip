@@ -110,6 +110,8 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 q) { return __builtin_bit_cast(bf16x8, q); }
 
+
+
 // the six leading piece products of one 16-deep k-step, small terms first
 template <int TM, int TN>
 __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const bf16x8 (&a)[TM][3],
@@ -130,11 +132,11 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const bf16x8 (&a
 }
 
 // write one wave's TM x TN accumulator tiles (wave origin r0, c0; tile column origin n0 for
-// the plane base): C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+// the plane base; split-K slab ks): C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 template <int TM, int TN, int WTM, int WTN>
 __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
-                                            int64_t c0, int64_t n0, int lane) {
-    float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)blockIdx.y * g.M * g.N
+                                            int64_t c0, int64_t n0, int ks, int lane) {
+    float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)ks * g.M * g.N
                                           : const_cast<float*>(plane_base(g.C, n0, g.c_blk, g.c_pstride));
     const int64_t ldd = g.split > 1 ? g.N : g.ldc;
     const int li = lane & 31, lh = lane >> 5;
@@ -165,30 +167,32 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
 // ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored three
 // times), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA + barriers),
 // 4 = MFMA + barriers only.
-// NBUF = 2: double-buffered LDS, one barrier per slice (one workgroup per CU at these tile
-// sizes); NBUF = 1: single buffer, two barriers per slice, a third of the LDS, so several
-// independent workgroups share a CU and their staging and MFMA phases overlap.
-template <int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0, int NBUF = 2>
+template <int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-    constexpr int AK = (TA == 0) ? 1 : 0;
-    constexpr int BKc = (TB == 1) ? 1 : 0;
+    constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
+    constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
     static_assert(BM * 4 % NT == 0 && BN * 4 % NT == 0, "staging units must divide evenly");
     // [buffer][piece][row][4 chunks of 8 bf16]
-    __shared__ uint4 As[NBUF][3 * BM * 4];
-    __shared__ uint4 Bs[NBUF][3 * BN * 4];
+    __shared__ uint4 As[2][3 * BM * 4];
+    __shared__ uint4 Bs[2][3 * BN * 4];
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int wm = wave / WN, wn = wave % WN;
+    const int t = threadIdx.x;
     const int64_t ntn = (g.N + BN - 1) / BN;
     const int64_t ntm = (g.M + BM - 1) / BM;
     const int tiles = (int)(ntm * ntn);
-    const int lt = xcd_remap(blockIdx.x, tiles);
+    // XCD-aware order over the whole (tile, split) grid: the workgroups one XCD runs take
+    // consecutive tiles of the same K slice, so that slice's operand rows are fetched into
+    // that XCD's L2 once and shared (split-K wgrad: 16 tiles x 16 slices)
+    const int lt_all = xcd_remap(blockIdx.x + tiles * blockIdx.y, tiles * (int)gridDim.y);
+    const int lt = lt_all % tiles, ks = lt_all / tiles;
     const int64_t tm = lt / ntn, tn = lt % ntn;
     const int64_t m0 = tm * BM, n0 = tn * BN;
-    const int64_t kb = (int64_t)blockIdx.y * g.kchunk;
+    const int64_t kb = (int64_t)ks * g.kchunk;
     const int64_t ke = min(g.K, kb + g.kchunk);
 
     const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % 4 == 0);
@@ -208,92 +212,78 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     auto load_ab = [&](int64_t k0) {
         const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
         if (full) {
-            x6_load<AK, BM, NT, true>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra, (int)threadIdx.x);
-            x6_load<BKc, BN, NT, true>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb, (int)threadIdx.x);
+            x6_load<AK, BM, NT, true>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra, t);
+            x6_load<BKc, BN, NT, true>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb, t);
         } else {
-            x6_load<AK, BM, NT, false>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra, (int)threadIdx.x);
-            x6_load<BKc, BN, NT, false>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb, (int)threadIdx.x);
+            x6_load<AK, BM, NT, false>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra, t);
+            x6_load<BKc, BN, NT, false>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb, t);
         }
     };
-    if constexpr (NBUF == 2) {
-        if (nk > 0) {
-            load_ab(kb);
-            x6_store<AK, BM, NT, ABL>(As[0], ra, (int)threadIdx.x);
-            x6_store<BKc, BN, NT, ABL>(Bs[0], rb, (int)threadIdx.x);
-            if (nk > 1 && ABL != 2) load_ab(kb + X6_BK);
-        }
-        __syncthreads();
-    } else {
-        if (nk > 0) load_ab(kb);
+    auto store_ab = [&](int buf) {
+        x6_store<AK, BM, NT, ABL>(As[buf], ra, t);
+        x6_store<BKc, BN, NT, ABL>(Bs[buf], rb, t);
+    };
+    // Pipeline: slice t+1 is split and written to the free LDS buffer, slice t+2 is loaded
+    // into registers, then slice t is multiplied; one barrier per slice.
+    if (nk > 0) {
+        load_ab(kb);
+        store_ab(0);
+        if (nk > 1 && ABL != 2) load_ab(kb + X6_BK);
     }
+    __syncthreads();
 
     const int li = lane & 31, lh = lane >> 5;
     for (int64_t kt = 0; kt < nk; ++kt) {
-        const int cur = NBUF == 2 ? (kt & 1) : 0;
-        if constexpr (NBUF == 2) {
-            if (kt + 1 < nk && ABL < 3) {
-                x6_store<AK, BM, NT, ABL>(As[cur ^ 1], ra, (int)threadIdx.x);
-                x6_store<BKc, BN, NT, ABL>(Bs[cur ^ 1], rb, (int)threadIdx.x);
-            }
-            if (kt + 2 < nk && ABL != 2 && ABL < 3) load_ab(kb + (kt + 2) * X6_BK);
-        } else {
-            x6_store<AK, BM, NT, ABL>(As[0], ra, (int)threadIdx.x);
-            x6_store<BKc, BN, NT, ABL>(Bs[0], rb, (int)threadIdx.x);
-            if (kt + 1 < nk && ABL != 2) load_ab(kb + (kt + 1) * X6_BK);
-            __syncthreads();
-        }
-        const uint4* as = As[cur];
-        const uint4* bs = Bs[cur];
-        bf16x8 a[X6_BK / 16][TM][3], b[X6_BK / 16][TN][3];
-        auto read_frags = [&](int kk) {
-            const int c = 2 * kk + lh;
+        const int cur = kt & 1;
+        if (kt + 1 < nk && ABL < 3) store_ab(cur ^ 1);
+        if (kt + 2 < nk && ABL != 2 && ABL < 3) load_ab(kb + (kt + 2) * X6_BK);
+#pragma unroll
+        for (int kk = 0; kk < X6_BK / 16; ++kk) {
+            bf16x8 a[TM][3], b[TN][3];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const int row = wm * (BM / WM) + i * 32 + li;
-                const int pos = x6_pos(row, c);
+                const int row = wm * (BM / WM) + i * 32;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    if constexpr (ABL == 4) a[kk][i][p] = as_bf16x8(make_uint4(pos + p, kk, i, (int)kt));
-                    else a[kk][i][p] = as_bf16x8(as[p * BM * 4 + pos]);
+                    if constexpr (ABL == 4) {
+                        a[i][p] = as_bf16x8(make_uint4(row + p, kk, i, (int)kt));
+                    } else {
+                        a[i][p] = as_bf16x8(As[cur][p * BM * 4 + x6_pos(row + li, 2 * kk + lh)]);
+                    }
                 }
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int row = wn * (BN / WN) + j * 32 + li;
-                const int pos = x6_pos(row, c);
+                const int row = wn * (BN / WN) + j * 32;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    if constexpr (ABL == 4) b[kk][j][p] = as_bf16x8(make_uint4(pos - p, kk, j, (int)kt));
-                    else b[kk][j][p] = as_bf16x8(bs[p * BN * 4 + pos]);
+                    if constexpr (ABL == 4) {
+                        b[j][p] = as_bf16x8(make_uint4(row - p, kk, j, (int)kt));
+                    } else {
+                        b[j][p] = as_bf16x8(Bs[cur][p * BN * 4 + x6_pos(row + li, 2 * kk + lh)]);
+                    }
                 }
             }
-        };
-#pragma unroll
-        for (int kk = 0; kk < X6_BK / 16; ++kk) {
-            read_frags(kk);
-            x6_mma<TM, TN>(acc, a[kk], b[kk]);
+            x6_mma<TM, TN>(acc, a, b);
         }
         __syncthreads();
     }
-
-    x6_epilogue<TM, TN, BM / WM, BN / WN>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, lane);
+    x6_epilogue<TM, TN, BM / WM, BN / WN>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane);
 }
 
 const X6Cfg kX6Cfgs[] = {
     {128, 128, 4, 1},   // 0: 2x2 waves of 64x64 (1 wave / SIMD)
     {256, 128, 8, 1},   // 1: 4x2 waves of 64x64 (2 waves / SIMD)
     {128, 256, 8, 1},   // 2: 2x4 waves of 64x64
-    {128, 128, 4, 2},   // 3: as 0, single LDS buffer (48 KB: two workgroups per CU)
 };
-const int kNumX6Cfgs = 4;
+const int kNumX6Cfgs = 3;
 
 template <int TA, int TB, int ABL>
 static void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     switch (cfg) {
         case 0: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 128, 128, 2, 2, ABL>), grid, dim3(256), 0, s, g); break;
         case 1: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 256, 128, 4, 2, ABL>), grid, dim3(512), 0, s, g); break;
-        case 2: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 128, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); break;
-        default: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 128, 128, 2, 2, ABL, 1>), grid, dim3(256), 0, s, g); break;
+        default: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 128, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); break;
     }
 }
 
