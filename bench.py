@@ -27,6 +27,7 @@ events recorded on the launching stream around each launch inside the timed regi
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -54,6 +55,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
+    ap.add_argument("--data", default="static", choices=["static", "store", "host"],
+                    help="static: one resident 16-graph batch, graph structure rebuilt every step (default); "
+                         "store: a new shuffled 16-graph batch every step, gathered on the GPU from a resident "
+                         "GraphStore of --store-graphs meshes; host: the same batches collated on the host "
+                         "(PyG DataLoader path of the reference) and copied to the GPU inside the step")
+    ap.add_argument("--store-graphs", type=int, default=256)
     return ap.parse_args()
 
 
@@ -80,6 +87,7 @@ def cpu_baseline(batch, model_state, model_name, steps):
 
 def main():
     args = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -112,10 +120,35 @@ def main():
     norm = bgnn.EigenvalueScaler(center=1.0, scale=0.5)
     ar = bgnn.GradAllReduce(model) if world > 1 else None
 
-    def step():
-        if not args.cache_graph:
-            bgnn.clear_caches()
-        return bgnn.train_step(model, batch, opt, crit, norm, allreduce=ar)
+    if args.data == "static":
+        def step():
+            if not args.cache_graph:
+                bgnn.clear_caches()
+            return bgnn.train_step(model, batch, opt, crit, norm, allreduce=ar)
+    else:
+        # a pool of meshes per rank, a different shuffled 16-graph batch every step
+        c = synthetic.CONFIGS[args.config]
+        pool = [synthetic.make_mesh_graph(c["n"], 1000 * rank + g, super_node=c["super_node"])
+                for g in range(args.store_graphs)]
+        store = bgnn.GraphStore(pool, dev) if args.data == "store" else None
+        rng = np.random.default_rng(rank)
+        order = iter(())
+
+        def next_ids():
+            nonlocal order
+            ids = list(itertools.islice(order, 16))
+            if len(ids) < 16:
+                order = iter(rng.permutation(args.store_graphs))
+                ids = list(itertools.islice(order, 16))
+            return ids
+
+        def step():
+            ids = next_ids()
+            if store is not None:
+                b = store.batch(ids)
+            else:
+                b = bgnn.Batch.from_data_list([pool[i] for i in ids]).to(dev, non_blocking=True)
+            return bgnn.train_step(model, b, opt, crit, norm, allreduce=ar)
 
     for _ in range(args.warmup):
         step()
@@ -175,8 +208,13 @@ def main():
         "config": {
             "workload": f"{args.config}: 16 synthetic 71x71 quad+diagonal FE meshes per GPU"
                         + (" + super node" if args.config == "cfg3" else " + 13.33% random virtual edges")
-                        + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam; CSR rebuilt every step"
-                        if not args.cache_graph else f"{args.config} (CSR cached across steps)",
+                        + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam; "
+                        + {"static": "CSR rebuilt every step" if not args.cache_graph else "CSR cached across steps",
+                           "store": f"new shuffled batch every step gathered on the GPU from a resident "
+                                    f"GraphStore of {args.store_graphs} meshes",
+                           "host": f"new shuffled batch every step collated on the host from {args.store_graphs} "
+                                   f"meshes and copied to the GPU (reference DataLoader path)"}[args.data],
+            "data_path": args.data,
             "global_batch": 16 * world,
             "nodes_per_gpu": N,
             "edges_per_gpu": E,

@@ -12,6 +12,7 @@ from .nn import (SAGEConv, global_add_pool, global_max_pool, global_mean_pool, s
                  scatter_sum)
 from .ops import aggregate, segment_reduce
 from .pyg_shim import install_pyg_shim, uninstall_pyg_shim
+from .store import GraphStore
 from .train import EigenvalueScaler, GradAllReduce, RelativeErrorLoss, mape_error, train_step
 
 __all__ = [
@@ -19,7 +20,7 @@ __all__ = [
     "clear_caches", "graph_for", "prepare", "segments_for", "SAGEConv", "global_add_pool", "global_max_pool",
     "global_mean_pool", "scatter_add", "scatter_mean", "scatter_sum", "aggregate", "segment_reduce",
     "install_pyg_shim", "uninstall_pyg_shim", "EigenvalueScaler", "GradAllReduce", "RelativeErrorLoss",
-    "mape_error", "train_step", "load_library",
+    "mape_error", "train_step", "load_library", "GraphStore",
 ]
 
 

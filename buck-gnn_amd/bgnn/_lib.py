@@ -47,6 +47,9 @@ class CsrStruct(ctypes.Structure):
 SIGNATURES = {
     "bgnn_abi_version": (c_i32, []),
     "bgnn_last_error_string": (ctypes.c_char_p, []),
+    "bgnn_store_gather_graph": (c_i32, [c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p,
+                                        c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "bgnn_store_gather_rows": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_i64, c_p, c_p]),
     "bgnn_get_tuning": (c_i32, [c_i32]),
     "bgnn_set_tuning": (c_i32, [c_i32, c_i32]),
     "bgnn_graph_build_ws_bytes": (c_sz, [c_i64, c_i64]),

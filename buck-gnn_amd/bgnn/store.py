@@ -1,0 +1,257 @@
+"""Device-resident graph store and on-device mini-batching.
+
+The reference keeps its dataset as a host list of PyG `Data` (a pickled
+`dataset_cache_*.pkl`, GraphCreate.py:562-568) and collates every mini-batch on the host
+(`DataLoader`, TRAIN_FINAL.py:1298-1302); the GPU then sees a new `edge_index` each step.
+On MI355X the whole dataset fits in HBM (80,000 cfg4 meshes ~ 150 GB of 288 GB), so
+`GraphStore` uploads it once, builds every graph's CSR / transpose CSR once (one stable
+`bgnn_graph_build` per group of graphs) and keeps them graph-local. A mini-batch is then
+assembled on the device by two C-ABI calls (`bgnn_store_gather_graph`,
+`bgnn_store_gather_rows`) from a 16-row offset table: no host collation, no per-step
+sort and no host synchronisation. The batch's graph structure and pooling segments are
+registered in the caches `bgnn.prepare` / SAGEConv / BuckGNN consult, and they are
+identical to what `Graph.build` would produce from the collated `edge_index`.
+
+Collation follows PyG (and bgnn.data.Batch): per-node tensors (first dim = num_nodes)
+and per-edge tensors (first dim = num_edges) are concatenated, `edge_index` is offset by
+the running node count, per-graph tensors are concatenated along dim 0, `batch` and `ptr`
+are added.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterator, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .data import Batch, Data
+from .graph import (DEFAULT_CHUNK, Csr, Graph, Plan, SegmentIndex, _graph_cache, _index_cache, _stream,
+                    enqueue_plan)
+
+_GROUP_EDGES = 1 << 30   # graphs are CSR-built in groups of < 2^30 edges (int32 positions)
+
+
+def _heavy_counts(rowptr: torch.Tensor, gid: torch.Tensor, G: int, chunk: int):
+    """Per-graph (rows with degree > chunk, sum of their ceil(deg / chunk))."""
+    deg = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
+    heavy = deg > chunk
+    chunks = torch.where(heavy, (deg + chunk - 1) // chunk, torch.zeros_like(deg))
+    h = torch.zeros(G, dtype=torch.int64, device=rowptr.device).index_add_(0, gid, heavy.to(torch.int64))
+    c = torch.zeros(G, dtype=torch.int64, device=rowptr.device).index_add_(0, gid, chunks)
+    return h, c
+
+
+class GraphStore:
+    """All graphs of a dataset resident on one GPU, with graph-local CSR structures."""
+
+    def __init__(self, graphs: Sequence[Data], device=None, chunk: int = DEFAULT_CHUNK):
+        if len(graphs) == 0:
+            raise ValueError("GraphStore: empty dataset")
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if dev.type != "cuda":
+            raise RuntimeError("GraphStore: the store lives in GPU memory (bgnn has no CPU fallback)")
+        self.device = dev
+        self.chunk = chunk
+        G = len(graphs)
+        self.num_graphs = G
+        n = np.array([d.num_nodes for d in graphs], dtype=np.int64)
+        e = np.array([d.num_edges for d in graphs], dtype=np.int64)
+        if (e >= (1 << 31)).any() or (n >= (1 << 31)).any():
+            raise ValueError("GraphStore: a single graph must have < 2^31 nodes and edges")
+        self.n_nodes, self.n_edges = n, e
+        self.node_off = np.concatenate([[0], np.cumsum(n)])
+        self.edge_off = np.concatenate([[0], np.cumsum(e)])
+
+        # classify attributes like PyG collation
+        keys: List[str] = []
+        for d in graphs:
+            for k in d.keys():
+                if k not in keys and k not in ("num_nodes", "batch", "ptr"):
+                    keys.append(k)
+        self.node_keys, self.edge_keys, self.graph_keys, self.other_keys = [], [], [], []
+        for k in keys:
+            vals = [d._store.get(k) for d in graphs]
+            if k == "edge_index":
+                continue
+            if not all(isinstance(v, torch.Tensor) for v in vals):
+                self.other_keys.append(k)
+            # (PyG concatenates every tensor along dim 0; the class only picks the gather path)
+            elif all(v.dim() > 0 and v.size(0) == d.num_nodes for v, d in zip(vals, graphs)):
+                self.node_keys.append(k)
+            elif all(v.dim() > 0 and v.size(0) == d.num_edges for v, d in zip(vals, graphs)):
+                self.edge_keys.append(k)
+            else:
+                self.graph_keys.append(k)
+
+        self.node_data: Dict[str, torch.Tensor] = {
+            k: torch.cat([d._store[k] for d in graphs], 0).to(dev).contiguous() for k in self.node_keys}
+        self.edge_data: Dict[str, torch.Tensor] = {
+            k: torch.cat([d._store[k] for d in graphs], 0).to(dev).contiguous() for k in self.edge_keys}
+        self.graph_data: Dict[str, List[torch.Tensor]] = {}
+        self.graph_stacked: Dict[str, torch.Tensor] = {}
+        for k in self.graph_keys:
+            vals = [d._store[k] for d in graphs]
+            if all(v.dim() == 0 for v in vals):
+                self.graph_stacked[k] = torch.stack(vals).to(dev)
+            elif all(v.shape == vals[0].shape for v in vals):
+                self.graph_stacked[k] = torch.stack(vals).to(dev)     # [G, *shape]: gather + flatten dim 0
+            else:
+                self.graph_data[k] = [v.to(dev) for v in vals]
+        self.other = {k: [d._store.get(k) for d in graphs] for k in self.other_keys}
+
+        # graph-local edge_index (int32) and CSRs, built once per group of graphs
+        sumN, sumE = int(self.node_off[-1]), int(self.edge_off[-1])
+        ei_l = torch.empty(2, max(sumE, 1), dtype=torch.int32, device=dev)
+        self.rowptr = torch.empty(max(sumN, 1), dtype=torch.int32, device=dev)
+        self.rowptr_t = torch.empty(max(sumN, 1), dtype=torch.int32, device=dev)
+        self.col = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
+        self.col_t = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
+        self.perm_t = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
+        heavy = torch.zeros(G, 4, dtype=torch.int64, device=dev)
+        g0 = 0
+        while g0 < G:
+            g1 = g0 + 1
+            while g1 < G and self.edge_off[g1 + 1] - self.edge_off[g0] < _GROUP_EDGES:
+                g1 += 1
+            self._build_group(graphs, g0, g1, ei_l, heavy)
+            g0 = g1
+        self.edge_index = ei_l
+        self.heavy = heavy.cpu().numpy()          # per graph: fwd heavy rows, fwd chunks, bwd rows, bwd chunks
+        self._ptr_cache: Dict[int, torch.Tensor] = {}
+
+    def _build_group(self, graphs, g0, g1, ei_l, heavy):
+        dev = self.device
+        n0, n1 = int(self.node_off[g0]), int(self.node_off[g1])
+        e0, e1 = int(self.edge_off[g0]), int(self.edge_off[g1])
+        Gg = g1 - g0
+        ei = torch.cat([graphs[g]._store["edge_index"].to(torch.int64) + int(self.node_off[g] - n0)
+                        for g in range(g0, g1)], 1).to(dev) if e1 > e0 else \
+            torch.zeros(2, 0, dtype=torch.int64, device=dev)
+        gr = Graph.build(ei, n1 - n0, self.chunk)
+        noff = torch.as_tensor(self.node_off[g0:g1] - n0, device=dev)
+        eoff = torch.as_tensor(self.edge_off[g0:g1] - e0, device=dev)
+        gid_n = torch.repeat_interleave(torch.arange(Gg, device=dev), torch.as_tensor(self.n_nodes[g0:g1], device=dev))
+        gid_e = torch.repeat_interleave(torch.arange(Gg, device=dev), torch.as_tensor(self.n_edges[g0:g1], device=dev))
+        if n1 > n0:
+            self.rowptr[n0:n1] = (gr.fwd.rowptr[:-1].to(torch.int64) - eoff[gid_n]).to(torch.int32)
+            self.rowptr_t[n0:n1] = (gr.bwd.rowptr[:-1].to(torch.int64) - eoff[gid_n]).to(torch.int32)
+        if e1 > e0:
+            # CSR entries of graph g occupy [edge_off[g], edge_off[g+1]) in both sorted orders
+            self.col[e0:e1] = (gr.fwd.col[:e1 - e0].to(torch.int64) - noff[gid_e]).to(torch.int32)
+            self.col_t[e0:e1] = (gr.bwd.col[:e1 - e0].to(torch.int64) - noff[gid_e]).to(torch.int32)
+            self.perm_t[e0:e1] = (gr.perm_t[:e1 - e0].to(torch.int64) - eoff[gid_e]).to(torch.int32)
+            ei_l[:, e0:e1] = (ei - noff[gid_e]).to(torch.int32)
+        hf, cf = _heavy_counts(gr.fwd.rowptr, gid_n, Gg, self.chunk)
+        hb, cb = _heavy_counts(gr.bwd.rowptr, gid_n, Gg, self.chunk)
+        heavy[g0:g1] = torch.stack([hf, cf, hb, cb], 1)
+
+    # ------------------------------------------------------------------------------------
+    def batch(self, graph_ids: Sequence[int]) -> Batch:
+        """Assemble the mini-batch of the given graphs on the device (PyG collation order)."""
+        ids = np.asarray(graph_ids, dtype=np.int64)
+        B = ids.size
+        if B == 0:
+            raise ValueError("GraphStore.batch: empty selection")
+        if ids.min() < 0 or ids.max() >= self.num_graphs:
+            raise IndexError("GraphStore.batch: graph id out of range")
+        dev = self.device
+        nn_, ne = self.n_nodes[ids], self.n_edges[ids]
+        dn = np.concatenate([[0], np.cumsum(nn_)])
+        de = np.concatenate([[0], np.cumsum(ne)])
+        Nb, Eb = int(dn[-1]), int(de[-1])
+        if Eb >= (1 << 31):
+            raise ValueError("GraphStore.batch: a batch must have < 2^31 edges")
+        table = np.stack([self.node_off[ids], dn[:-1], nn_, self.edge_off[ids], de[:-1], ne], 1)
+        table_d = torch.from_numpy(np.ascontiguousarray(table)).pin_memory().to(dev, non_blocking=True)
+        s = _stream()
+        ei_b = torch.empty(2, Eb, dtype=torch.int64, device=dev)
+        rowptr = torch.empty(Nb + 1, dtype=torch.int32, device=dev)
+        rowptr_t = torch.empty(Nb + 1, dtype=torch.int32, device=dev)
+        col = torch.empty(max(Eb, 1), dtype=torch.int32, device=dev)
+        col_t = torch.empty(max(Eb, 1), dtype=torch.int32, device=dev)
+        perm_t = torch.empty(max(Eb, 1), dtype=torch.int32, device=dev)
+        batch = torch.empty(Nb, dtype=torch.int64, device=dev)
+        _lib.call("bgnn_store_gather_graph", table_d.data_ptr(), B, Nb, Eb, int(nn_.max()), int(ne.max()),
+                  self.edge_index.data_ptr(), self.edge_index.stride(0), self.rowptr.data_ptr(), self.col.data_ptr(),
+                  self.rowptr_t.data_ptr(), self.col_t.data_ptr(), self.perm_t.data_ptr(), ei_b.data_ptr(),
+                  rowptr.data_ptr(), col.data_ptr(), rowptr_t.data_ptr(), col_t.data_ptr(), perm_t.data_ptr(),
+                  batch.data_ptr(), s)
+        out = Batch()
+        st = out._store
+        for k, src in self.node_data.items():
+            st[k] = self._gather_rows(table_d, B, 0, int(nn_.max()), src, Nb)
+        st["edge_index"] = ei_b
+        for k, src in self.edge_data.items():
+            st[k] = self._gather_rows(table_d, B, 1, int(ne.max()), src, Eb)
+        sel = None
+        for k, t in self.graph_stacked.items():
+            if sel is None:
+                sel = torch.from_numpy(ids).pin_memory().to(dev, non_blocking=True)
+            v = t.index_select(0, sel)
+            st[k] = v if v.dim() == 1 else v.reshape(-1, *v.shape[2:])
+        for k, lst in self.graph_data.items():
+            st[k] = torch.cat([lst[i] for i in ids], 0)
+        for k, lst in self.other.items():
+            st[k] = [lst[i] for i in ids]
+        st["batch"] = batch
+        ptr = torch.from_numpy(dn).pin_memory().to(dev, non_blocking=True)
+        st["ptr"] = ptr
+        st["num_graphs"] = B
+        st["num_nodes"] = Nb
+
+        # graph structure of the batch, registered for prepare()/SAGEConv/BuckGNN
+        hv = self.heavy[ids].sum(0)
+        fwd = Csr(rowptr, col, Nb, Eb, self._plan(rowptr, Nb, Eb, int(hv[0]), int(hv[1])))
+        bwd = Csr(rowptr_t, col_t, Nb, Eb, self._plan(rowptr_t, Nb, Eb, int(hv[2]), int(hv[3])))
+        graph = Graph(Nb, Eb, fwd, bwd, perm_t, ei_b, None)
+        _graph_cache.put(ei_b, (Nb, self.chunk), graph)
+        # pooling segments: graph b owns positions [ptr[b], ptr[b+1])
+        heavy_g = nn_ > self.chunk
+        ptr32 = ptr.to(torch.int32)
+        seg_plan = self._plan(ptr32, B, Nb, int(heavy_g.sum()),
+                              int(((nn_ + self.chunk - 1) // self.chunk)[heavy_g].sum()))
+        seg_f = Csr(ptr32, self._arange(Nb), B, Nb, seg_plan)
+        empty = Plan(torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
+                     torch.zeros(1, dtype=torch.int32, device=dev), 0, 0, self.chunk)
+        seg_b = Csr(self._arange(Nb + 1), batch.to(torch.int32), Nb, Nb, empty)
+        _index_cache.put(batch, ("batch",), SegmentIndex(Nb, B, seg_f, seg_b, batch, None))
+        return out
+
+    def _gather_rows(self, table_d, B, per_edge, max_rows, src, n_out):
+        out = torch.empty((n_out,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        row_bytes = src[0].numel() * src.element_size() if src.size(0) else 0
+        if n_out == 0 or row_bytes == 0:
+            return out
+        if row_bytes % 4:
+            raise ValueError("GraphStore: per-row attribute size must be a multiple of 4 bytes")
+        _lib.call("bgnn_store_gather_rows", table_d.data_ptr(), B, per_edge, max_rows, src.data_ptr(), row_bytes,
+                  out.data_ptr(), _stream())
+        return out
+
+    def _plan(self, rowptr, n_rows, nnz, n_heavy, n_chunks) -> Plan:
+        counts = torch.empty(2, dtype=torch.int32, device=self.device)   # device copy unused: counts known
+        p = enqueue_plan(rowptr, n_rows, nnz, counts, self.chunk)
+        p.n_heavy, p.n_chunks = n_heavy, n_chunks
+        return p
+
+    def _arange(self, n: int) -> torch.Tensor:
+        t = self._ptr_cache.get(n)
+        if t is None:
+            t = torch.arange(max(n, 1), dtype=torch.int32, device=self.device)
+            self._ptr_cache[n] = t
+        return t
+
+    def loader(self, batch_size: int, shuffle: bool = False, seed: int = 0, drop_last: bool = False,
+               epoch: int = 0, rank: int = 0, world_size: int = 1) -> Iterator[Batch]:
+        """Iterate mini-batches of one epoch (DataLoader semantics; with world_size > 1 each rank
+        takes a disjoint DistributedSampler-style shard of the shuffled order)."""
+        order = np.arange(self.num_graphs)
+        if shuffle:
+            order = np.random.default_rng(seed + epoch).permutation(self.num_graphs)
+        order = order[rank::world_size]
+        for i in range(0, len(order), batch_size):
+            ids = order[i:i + batch_size]
+            if drop_last and len(ids) < batch_size:
+                break
+            yield self.batch(ids)

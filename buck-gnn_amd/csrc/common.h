@@ -34,6 +34,7 @@ int fail(int code, const char* fmt, ...);
     } while (0)
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 

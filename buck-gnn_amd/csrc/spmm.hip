@@ -741,7 +741,6 @@ int dispatch_plain(SegArgs A, const Geometry& g, hipStream_t s) {
     return fail(BGNN_E_UNSUPPORTED, "spmm: no kernel for vec=%d nv=%d lpr=%d", g.vec, g.nv, g.lpr);
 }
 
-inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 inline SegArgs args_from_csr(const bgnn_csr_t* c) {
     SegArgs A{};

@@ -238,6 +238,33 @@ int bgnn_gemm_f32_planes(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
                          int64_t c_blk, int64_t c_pstride, const float* bias, int32_t relu,
                          void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Device-resident graph store (replaces the host-side PyG
+ * DataLoader/Batch collation of TRAIN_FINAL.py:1298-1302 and the per-step graph
+ * structure build). Stored arrays are graph-local int32: edge_index [2][ld_ei] (node ids
+ * relative to the graph's first node), rowptr / rowptr_t [sum N] (edge offsets relative to
+ * the graph's first edge; the row end of a graph's last node is its edge count), col /
+ * col_t [sum E] (local node ids), perm_t [sum E] (local forward positions).
+ * table: device int64 [B][6] = {src_node, dst_node, n_nodes, src_edge, dst_edge, n_edges}
+ * per batch graph (dst offsets = running sums). max_nodes / max_edges bound the per-graph
+ * sizes (launch geometry only). Outputs are the batch's int64 edge_index [2][Eb], its
+ * forward / transpose CSR (rowptr [Nb+1], col [Eb], rowptr_t [Nb+1], col_t [Eb],
+ * perm_t [Eb]) and the int64 `batch` vector [Nb] -- identical to bgnn_graph_build on the
+ * collated edge_index.
+ * ---------------------------------------------------------------------- */
+int bgnn_store_gather_graph(const int64_t* table, int32_t B, int64_t Nb, int64_t Eb,
+                            int64_t max_nodes, int64_t max_edges,
+                            const int32_t* edge_index, int64_t ld_ei,
+                            const int32_t* rowptr, const int32_t* col,
+                            const int32_t* rowptr_t, const int32_t* col_t, const int32_t* perm_t,
+                            int64_t* edge_index_out, int32_t* rowptr_out, int32_t* col_out,
+                            int32_t* rowptr_t_out, int32_t* col_t_out, int32_t* perm_t_out,
+                            int64_t* batch_out, void* stream);
+/* Copy each batch graph's node rows (per_edge = 0) or edge rows (per_edge = 1) of a
+ * row-major store array (row_bytes per row, a multiple of 4) into the batch array. */
+int bgnn_store_gather_rows(const int64_t* table, int32_t B, int32_t per_edge, int64_t max_rows,
+                           const void* src, int64_t row_bytes, void* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -117,3 +117,11 @@ def test_super_node_index_vectorised():
     b = torch.tensor([0, 0, 0, 1, 1, 2, 2, 2, 2])
     assert super_node_index(b, 9, "cpu").tolist() == super_index(b, 9).tolist() == [2, 4, 8]
     assert super_node_index(None, 5, "cpu").tolist() == [4]
+
+
+def test_graph_store_requires_gpu():
+    """GraphStore lives in HBM: a CPU device is rejected (no CPU fallback)."""
+    import bgnn
+    from bgnn import synthetic as S
+    with pytest.raises(RuntimeError):
+        bgnn.GraphStore([S.make_mesh_graph(5, seed=0)], device="cpu")
