@@ -13,6 +13,8 @@ from .nn import (SAGEConv, global_add_pool, global_max_pool, global_mean_pool, s
 from .ops import aggregate, segment_reduce
 from .pyg_shim import install_pyg_shim, uninstall_pyg_shim
 from .store import GraphStore
+from .checkpoint import load_checkpoint, load_reference_checkpoint, save_checkpoint
+from .inference import evaluate
 from .train import EigenvalueScaler, GradAllReduce, RelativeErrorLoss, mape_error, train_step
 
 __all__ = [
@@ -20,7 +22,8 @@ __all__ = [
     "clear_caches", "graph_for", "prepare", "segments_for", "SAGEConv", "global_add_pool", "global_max_pool",
     "global_mean_pool", "scatter_add", "scatter_mean", "scatter_sum", "aggregate", "segment_reduce",
     "install_pyg_shim", "uninstall_pyg_shim", "EigenvalueScaler", "GradAllReduce", "RelativeErrorLoss",
-    "mape_error", "train_step", "load_library", "GraphStore",
+    "mape_error", "train_step", "load_library", "GraphStore", "load_checkpoint", "load_reference_checkpoint",
+    "save_checkpoint", "evaluate",
 ]
 
 
