@@ -134,6 +134,7 @@ size_t scan_tmp_bytes(int64_t n) {
     return tmp;
 }
 
+
 }  // namespace
 
 }  // namespace bgnn
@@ -270,3 +271,4 @@ extern "C" int bgnn_heavy_plan(const int32_t* rowptr, int64_t R, int64_t nnz, in
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
+

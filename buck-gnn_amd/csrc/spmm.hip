@@ -55,6 +55,9 @@ struct SegArgs {
 };
 
 
+// 1 / max(deg, 1), correctly rounded, identical in every kernel (MEAN backward weights)
+__device__ __forceinline__ float inv_deg(int32_t d) { return __frcp_rn((float)(d > 0 ? d : 1)); }
+
 template <int VEC>
 struct Vec {
     float f[VEC];
@@ -147,7 +150,7 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
         w[u] = 1.f;
         if constexpr (OP == OP_MEANT) {
             const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
-            w[u] = 1.f / (float)(d > 0 ? d : 1);
+            w[u] = inv_deg(d);
         }
     }
     Vec<VEC> val[U][NV];
@@ -186,7 +189,7 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
                 }
             } else {
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) acc.a[v][k] += ok ? val[u][v].f[k] * w[u] : 0.f;
+                for (int k = 0; k < VEC; ++k) acc.a[v][k] += ok ? __fmul_rn(val[u][v].f[k], w[u]) : 0.f;
             }
         }
     }
@@ -208,7 +211,7 @@ template <int VEC, int NV, int OP>
 __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& acc, int64_t r,
                                             int32_t deg, const int (&cpos)[NV],
                                             const bool (&cok)[NV]) {
-    const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
+    const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         if (!cok[v]) continue;
@@ -238,11 +241,18 @@ __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& 
 
 // Fused SAGE epilogue for one row held by a full wave (LPR == 64, VEC == 4):
 // h = acc*scale + z_r[r] + b; o = h / max(||h||, 1e-12); BN partial sums.
+// Canonical SAGE row arithmetic, written with explicit roundings so that every kernel
+// (light, sweep, combine) produces bit-identical o / nrm regardless of how the
+// compiler would contract it: h = (a * sc + zr) + b, ss = fma(h, h, ss).
+__device__ __forceinline__ float sage_h(float a, float sc, float zr, float b) {
+    return __fadd_rn(__fadd_rn(__fmul_rn(a, sc), zr), b);
+}
+
 template <int NV, int OP>
 __device__ __forceinline__ void store_sage(const SegArgs& A, Acc<4, NV, OP>& acc, int64_t r,
                                            int32_t deg, const int (&cpos)[NV], const bool (&cok)[NV],
                                            float (&bs)[NV][4], float (&bq)[NV][4]) {
-    const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
+    const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
     float h[NV][4];
     float ss = 0.f;
 #pragma unroll
@@ -252,8 +262,8 @@ __device__ __forceinline__ void store_sage(const SegArgs& A, Acc<4, NV, OP>& acc
             const Vec<4> b = ld<4>(A.bias + cpos[v]);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                h[v][k] = acc.a[v][k] * sc + zr.f[k] + b.f[k];
-                ss += h[v][k] * h[v][k];
+                h[v][k] = sage_h(acc.a[v][k], sc, zr.f[k], b.f[k]);
+                ss = fmaf(h[v][k], h[v][k], ss);
             }
         } else {
 #pragma unroll
@@ -485,7 +495,7 @@ __device__ __forceinline__ void sweep_gather(const SegArgs& A, Acc<4, NV, OP>& a
         w[u] = 1.f;
         if constexpr (OP == OP_MEANT) {
             const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
-            w[u] = 1.f / (float)(d > 0 ? d : 1);
+            w[u] = inv_deg(d);
         }
     }
     Vec<4> val[U][NV];
@@ -513,7 +523,7 @@ __device__ __forceinline__ void sweep_gather(const SegArgs& A, Acc<4, NV, OP>& a
                 }
             } else {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) acc.a[v][k] += ok ? val[u][v].f[k] * w[u] : 0.f;
+                for (int k = 0; k < 4; ++k) acc.a[v][k] += ok ? __fmul_rn(val[u][v].f[k], w[u]) : 0.f;
             }
         }
     }
@@ -528,15 +538,20 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
     int cpos[NV];
     bool cok[NV];
     lane_cols<4, NV, 64>(cb, lane, A.H, cpos, cok);
-    float bs[NV][4], bq[NV][4];
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) bs[v][k] = bq[v][k] = 0.f;
-    Vec<4> bias[NV];
+    // SAGE epilogue state lives in LDS, not VGPRs (it would cost 24 registers per lane and
+    // the occupancy that a 12-neighbour gather batch needs): per-wave BatchNorm partial sums
+    // red[wave][0/1][col] (each lane owns its columns: no barriers) and the bias row.
+    __shared__ __attribute__((aligned(16))) float red[(EPI == EPI_SAGE) ? 4 : 1][2][(EPI == EPI_SAGE) ? 512 : 4];
+    __shared__ __attribute__((aligned(16))) float sbias[(EPI == EPI_SAGE) ? 512 : 4];
     if constexpr (EPI == EPI_SAGE) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) bias[v] = ld<4>(A.bias + (cok[v] ? cpos[v] : 0));
+        for (int v = 0; v < NV; ++v)
+            if (cok[v]) {
+                *reinterpret_cast<float4*>(&red[wave][0][cpos[v]]) = make_float4(0.f, 0.f, 0.f, 0.f);
+                *reinterpret_cast<float4*>(&red[wave][1][cpos[v]]) = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        for (int c = threadIdx.x; c < A.H; c += 256) sbias[c] = A.bias[c];
+        __syncthreads();
     }
     const int32_t chunk = A.chunk;
 
@@ -571,16 +586,20 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
             }
             for (int e0 = 0; e0 < deg; e0 += U) sweep_gather<NV, OP, U>(A, acc, cur, beg, deg, e0, cpos, cok);
             if constexpr (EPI == EPI_SAGE) {
-                const float sc = (OP == OP_MEAN) ? 1.f / (float)(deg > 0 ? deg : 1) : 1.f;
+                const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
                 float h[NV][4];
                 float ss = 0.f;
 #pragma unroll
-                for (int v = 0; v < NV; ++v)
+                for (int v = 0; v < NV; ++v) {
+                    const float4 bv = cok[v] ? *reinterpret_cast<const float4*>(&sbias[cpos[v]])
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        h[v][q] = cok[v] ? acc.a[v][q] * sc + zr[v].f[q] + bias[v].f[q] : 0.f;
-                        ss += h[v][q] * h[v][q];
+                        h[v][q] = cok[v] ? sage_h(acc.a[v][q], sc, zr[v].f[q], bb[q]) : 0.f;
+                        ss = fmaf(h[v][q], h[v][q], ss);
                     }
+                }
                 ss = group_sum(ss, kWave);
                 const float n = sqrtf(ss);
                 const float d = fmaxf(n, 1e-12f);
@@ -589,12 +608,15 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
                     if (!cok[v]) continue;
                     Vec<4> o;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        o.f[q] = h[v][q] / d;
-                        bs[v][q] += o.f[q];
-                        bq[v][q] += o.f[q] * o.f[q];
-                    }
+                    for (int q = 0; q < 4; ++q) o.f[q] = h[v][q] / d;
                     st_nt(A.out + r * A.ldo + cpos[v], o);
+                    float4* ps = reinterpret_cast<float4*>(&red[wave][0][cpos[v]]);
+                    float4* pq = reinterpret_cast<float4*>(&red[wave][1][cpos[v]]);
+                    float4 a = *ps, b = *pq;
+                    a.x += o.f[0]; a.y += o.f[1]; a.z += o.f[2]; a.w += o.f[3];
+                    b.x += o.f[0] * o.f[0]; b.y += o.f[1] * o.f[1]; b.z += o.f[2] * o.f[2]; b.w += o.f[3] * o.f[3];
+                    *ps = a;
+                    *pq = b;
                 }
                 if (lane == 0) A.nrm[r] = n;
             } else {
@@ -604,15 +626,6 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
     }
 
     if constexpr (EPI == EPI_SAGE) {
-        __shared__ __attribute__((aligned(16))) float red[4][2][512];
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-            if (cok[v])
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    red[wave][0][cpos[v] + k] = bs[v][k];
-                    red[wave][1][cpos[v] + k] = bq[v][k];
-                }
         __syncthreads();
         float* dst = A.bn_partial + (int64_t)blockIdx.x * 2 * A.H;
         for (int c = threadIdx.x; c < A.H; c += 256) {
@@ -629,8 +642,8 @@ constexpr int kMaxLightBlocks = 1024;
 static int g_seg_kernel = 0;     // 0 = sweep kernel where applicable, 1 = blocked kernel
 static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
 static int g_seg_nt = 1;         // non-temporal hints on stream-once data (default on: +8 % fwd)
-static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto:
-                                 // 8 with the SAGE epilogue (register-bound), 12 otherwise)
+static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto = 12:
+                                 // mesh rows have 8 neighbours + ~1 virtual edge, one batch)
 
 struct Geometry {
     int vec, nv, lpr, ctiles;
@@ -696,9 +709,12 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     if (A.n_rows > 0) {
         if constexpr (VEC == 4 && LPR == 64) {
             if (sweep) {
-                const int u = g_seg_u ? g_seg_u : (EPI == EPI_SAGE ? 8 : 12);
+                const int u = g_seg_u ? g_seg_u : 12;
                 if (u == 8)
                     hipLaunchKernelGGL((k_seg_sweep<NV, OP, EPI, 8>), dim3((unsigned)blocks, ctiles), dim3(256), 0,
+                                       s, A);
+                else if (u == 16)
+                    hipLaunchKernelGGL((k_seg_sweep<NV, OP, EPI, 16>), dim3((unsigned)blocks, ctiles), dim3(256), 0,
                                        s, A);
                 else
                     hipLaunchKernelGGL((k_seg_sweep<NV, OP, EPI, 12>), dim3((unsigned)blocks, ctiles), dim3(256), 0,
@@ -828,13 +844,17 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
 
 extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
     switch (knob) {
-        case BGNN_TUNE_SEG_KERNEL: g_seg_kernel = value ? 1 : 0; return BGNN_OK;
+        case BGNN_TUNE_SEG_KERNEL:
+            BGNN_REQUIRE(value == 0 || value == 1, "set_tuning: kernel must be 0 (sweep) or 1 (blocked)");
+            g_seg_kernel = value;
+            return BGNN_OK;
         case BGNN_TUNE_SEG_BLOCKS:
             BGNN_REQUIRE(value >= 8 && value <= 65536, "set_tuning: blocks out of range");
             g_seg_blocks = value;
             return BGNN_OK;
         case BGNN_TUNE_SEG_U:
-            BGNN_REQUIRE(value == 0 || value == 8 || value == 12, "set_tuning: U must be 0 (auto), 8 or 12");
+            BGNN_REQUIRE(value == 0 || value == 8 || value == 12 || value == 16,
+                         "set_tuning: U must be 0 (auto), 8, 12 or 16");
             g_seg_u = value;
             return BGNN_OK;
         case BGNN_TUNE_SEG_NT: g_seg_nt = value ? 1 : 0; return BGNN_OK;

@@ -59,7 +59,7 @@ const char* bgnn_last_error_string(void);
  * changes. Not thread-safe against concurrent launches. */
 #define BGNN_TUNE_SEG_KERNEL 1   /* 0 = XCD-sweep light-row kernel (default), 1 = blocked */
 #define BGNN_TUNE_SEG_BLOCKS 2   /* sweep grid in blocks (default 1024)                   */
-#define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (default), 8, 12 */
+#define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (12), 8, 12, 16  */
 #define BGNN_TUNE_SEG_NT 4       /* non-temporal hints on stream-once rows (default 1)       */
 #define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6 f32-accurate (default) */
 /* Current value of a knob (-1 for an unknown knob). */

@@ -125,20 +125,46 @@ def test_full_size_cfg3_properties(dev):
         torch.testing.assert_close(ax[r].double(), ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("knobs", [(1, 0), (0, 8), (0, 12)], ids=["blocked", "sweep8", "sweep12"])
-def test_kernel_variants_bit_identical(dev, knobs):
-    """Every light-row kernel variant (tuning knobs) gives bit-identical aggregation results."""
+@pytest.mark.parametrize("knobs", [(1, 0), (0, 8), (0, 12), (0, 16)],
+                         ids=["blocked", "sweep8", "sweep12", "sweep16"])
+@pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
+def test_kernel_variants_bit_identical(dev, knobs, graph):
+    """Every light-row kernel variant (tuning knobs) gives bit-identical aggregation results,
+    forward and transpose (backward), on meshes with super nodes and on a dense random graph."""
     from bgnn import _lib
-    b = S.make_batch(25, 3, super_node=True)
-    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    if graph == "mesh_super":
+        b = S.make_batch(25, 3, super_node=True)
+        ei, n = b.edge_index.to(dev), b.num_nodes
+    else:
+        n = 3000
+        gen = torch.Generator().manual_seed(11)
+        ei = torch.randint(0, n, (2, 24 * n), generator=gen).to(dev)
+    g = Graph.build(ei, n)
     torch.manual_seed(3)
-    x = torch.randn(b.num_nodes, 512, device=dev)
-    ref = {r: bgnn.aggregate(x, g, r) for r in ("sum", "mean", "max")}
+    x = torch.randn(n, 512, device=dev)
+    gy = torch.randn(n, 512, device=dev)
+
+    def run():
+        out = {}
+        for r in ("sum", "mean", "max"):
+            xx = x.clone().requires_grad_(True)
+            y = bgnn.aggregate(xx, g, r)
+            y.backward(gy)
+            out[r] = (y.detach(), xx.grad)
+        return out
+
+    old = (_lib.query("bgnn_get_tuning", 1), _lib.query("bgnn_get_tuning", 3))
+    ref = None
     try:
+        _lib.call("bgnn_set_tuning", 1, 0)
+        _lib.call("bgnn_set_tuning", 3, 8)
+        ref = run()
         _lib.call("bgnn_set_tuning", 1, knobs[0])
         _lib.call("bgnn_set_tuning", 3, knobs[1])
+        got = run()
         for r in ("sum", "mean", "max"):
-            assert torch.equal(bgnn.aggregate(x, g, r), ref[r]), r
+            assert torch.equal(got[r][0], ref[r][0]), (r, "fwd")
+            assert torch.equal(got[r][1], ref[r][1]), (r, "bwd")
     finally:
-        _lib.call("bgnn_set_tuning", 1, 0)
-        _lib.call("bgnn_set_tuning", 3, 0)
+        _lib.call("bgnn_set_tuning", 1, old[0])
+        _lib.call("bgnn_set_tuning", 3, old[1])

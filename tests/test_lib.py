@@ -42,10 +42,26 @@ def test_library_is_built_for_gfx950():
     assert b"gfx950" in blob or "gfx950" in out.stdout
 
 
-def test_csr_struct_layout_matches_header():
+def test_csr_struct_layout_matches_header(tmp_path):
+    """The ctypes mirror of bgnn_csr_t has the C compiler's size and field offsets."""
+    import shutil
+    import subprocess
+
     from bgnn import _lib
 
-    assert ctypes.sizeof(_lib.CsrStruct) == 5 * 8 + 2 * 8 + 4 * 4
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    names = [f[0] for f in _lib.CsrStruct._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"bgnn.h\"\nint main(void){\n"
+                   + 'printf("%zu\\n", sizeof(bgnn_csr_t));\n'
+                   + "".join(f'printf("%zu\\n", offsetof(bgnn_csr_t, {n}));\n' for n in names) + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(_lib.CsrStruct)
+    for n, off in zip(names, vals[1:]):
+        assert getattr(_lib.CsrStruct, n).offset == off, n
 
 
 def test_size_queries_need_no_gpu():

@@ -24,9 +24,13 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--variants", default="blocked,sweep8,sweep12,sweep12_b2048,sweep8_b2048,sweep12_b512")
+    ap.add_argument("--no-virtual", action="store_true", help="cfg2 meshes without the random virtual edges")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    b = synthetic.make_config_batch(args.config)
+    if args.no_virtual:
+        b = synthetic.Batch.from_data_list([synthetic.make_mesh_graph(71, g, virtual_edges=False) for g in range(16)])
+    else:
+        b = synthetic.make_config_batch(args.config)
     g = Graph.build(b.edge_index.to(dev), b.num_nodes)
     N, E, H = b.num_nodes, b.num_edges, 512
     torch.manual_seed(0)
@@ -38,7 +42,8 @@ def main():
     layout = {"il": False}
 
     def set_variant(v):
-        # "blocked" | "sweep[U][_b<blocks>][_nt][_il]"  (U = 0 auto, 8, 12; il = interleaved [N, 2H] z)
+        # "blocked" | "sweep[U][_b<blocks>][_nt][_il]"  (U = 0 auto, 8, 12, 16;
+        # il = interleaved [N, 2H] z)
         kern, u, blocks, nt = 0, 0, 1024, 0
         layout["il"] = v.endswith("_il")
         if v == "blocked":
