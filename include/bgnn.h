@@ -18,7 +18,10 @@
  *   bgnn_sage_fwd_*, bgnn_bn_*, bgnn_sage_bwd_*  ← the fused layer of
  *       Models/BuckGNN.py:430-444: SAGEConv(normalize=True) → BatchNorm1d → ReLU →
  *       skip (0<i<L-1) → Dropout, and its autograd backward.
- *   bgnn_gemm_f32  ← lin_l / lin_r of SAGEConv (dense fp32 linear, MFMA).
+ *   bgnn_gemm_f32*  ← lin_l / lin_r of SAGEConv (dense fp32 linear, MFMA) and the
+ *       node encoder's Linear+ReLU (Models/BuckGNN.py:67-74).
+ *   bgnn_store_gather_*  ← the PyG DataLoader collation of TRAIN_FINAL.py:1298-1302
+ *       plus the per-step edge_index preprocessing, for a device-resident dataset.
  *
  * Conventions (all functions):
  *   - every pointer is a DEVICE pointer unless named host_*;
