@@ -15,9 +15,10 @@ forward, RelativeErrorLoss on denormalised eigenvalues, backward, gradient all-r
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
 Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel, the forward GEMM
-z = x [W_l;W_r]^T (18 GEMMs of this size make up ~60 % of the step), MFMA-bound: 84.6 GFLOP per
-launch; its peak is the ceiling of the algorithm that runs (bf16 dense MFMA 2.5 PF / 6 piece
-products = 416.7 TF f32-equivalent; the f32 MFMA peak 157.3 TF is reported beside it).
+z = x [W_l;W_r]^T (18 GEMMs of this size make up about half of the step), MFMA-bound: 84.6 GFLOP
+per launch; its peak is the ceiling of the algorithm that runs (default f16x3: f16 dense MFMA
+2.5 PF / 3 piece products = 833.3 TF f32-equivalent; bf16x6: 2.5 PF / 6 = 416.7 TF; the f32
+MFMA peak 157.3 TF is reported beside it).
 `roofline_hbm` is the fused aggregation kernel (bgnn_sage_fwd: neighbour sum + lin_r term +
 bias + L2 normalize + BN statistics), 499.1 MB per launch against 8 TB/s. Both use HIP
 events recorded on the launching stream around each launch inside the timed region;
@@ -40,6 +41,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md)
 X6_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6   # f32-equivalent ceiling of the 6-product bf16 split GEMM
+H3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 3   # f32-equivalent ceiling of the 3-product f16 split GEMM (f16 = bf16 rate)
 TRAFFIC_FILE = "traffic_r01.json"
 METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"
 
@@ -188,8 +190,13 @@ def main():
             traffic = {}
     gemm_ms = avg_ms("gemm_fwd")
     gemm_flop = 2.0 * N * (2 * H) * H
-    x6 = _lib.query("bgnn_get_tuning", 5) == 1
-    gemm_peak = X6_PEAK_TFS if (x6 and args.gemm == "hip") else FP32_MFMA_PEAK_TFS
+    gmode = _lib.query("bgnn_get_tuning", 5) if args.gemm == "hip" else -1
+    gemm_peak = {1: X6_PEAK_TFS, 2: H3_PEAK_TFS}.get(gmode, FP32_MFMA_PEAK_TFS)
+    gemm_kernel = {2: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<1,0,1,256,128,4,2> (f32-accurate f16x3)",
+                   1: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<0,0,1,256,128,4,2> (f32-accurate bf16x6)",
+                   0: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_f32 (f32 MFMA)"}.get(gmode, "torch.mm")
+    gemm_basis = {2: "f16 dense MFMA 2500 TF / 3 f16 products per f32 product",
+                  1: "bf16 dense MFMA 2500 TF / 6 bf16 products per f32 product"}.get(gmode, "f32 dense MFMA")
     gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
     graphs = 16 * world * args.steps
     out = {
@@ -224,17 +231,14 @@ def main():
             "gemm": args.gemm,
         },
         "roofline": {
-            "kernel": (("bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<0,1,256,128,4,2> (f32-accurate bf16x6)"
-                        if x6 else "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_f32 (f32 MFMA)")
-                       if args.gemm == "hip" else "torch.mm"),
+            "kernel": gemm_kernel,
             "bound": "mfma",
             "achieved": round(gemm_tfs, 2),
             "peak": gemm_peak,
             "unit": "TFLOP/s",
             "frac": round(gemm_tfs / gemm_peak, 4),
-            "traffic": traffic.get("gemm_fwd") if x6 and args.gemm == "hip" else None,
-            "peak_basis": ("bf16 dense MFMA 2500 TF / 6 bf16 products per f32 product" if gemm_peak == X6_PEAK_TFS
-                           else "f32 dense MFMA"),
+            "traffic": traffic.get({2: "gemm_fwd_h3", 1: "gemm_fwd"}.get(gmode, ""), None),
+            "peak_basis": gemm_basis,
             "f32_mfma_peak": FP32_MFMA_PEAK_TFS,
             "algorithmic_flop": gemm_flop,
             "avg_launch_ms": round(gemm_ms, 5),

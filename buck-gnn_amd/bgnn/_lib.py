@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lock = threading.Lock()
 _lib = None
@@ -59,23 +59,26 @@ SIGNATURES = {
     "bgnn_heavy_plan": (c_i32, [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
-                              c_p, c_p]),
+                              c_p, c_p, c_p]),
     "bgnn_sage_fwd_slots": (c_i32, [c_i64]),
     "bgnn_sage_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p,
                               c_p, c_p]),
     "bgnn_bn_finalize": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
                                  c_p]),
     "bgnn_bn_eval_coeffs": (c_i32, [c_i32, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p]),
-    "bgnn_sage_apply": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_f32, c_u64, c_i64, c_i32, c_p, c_p]),
+    "bgnn_sage_apply": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_f32, c_u64, c_i64, c_i32, c_p, c_p, c_p]),
     "bgnn_rows_slots": (c_i32, [c_i64]),
     "bgnn_sage_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i64, c_i32, c_p, c_p]),
     "bgnn_reduce_partials": (c_i32, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p]),
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
-                                   c_i32, c_p, c_i64, c_p, c_p, c_p]),
+                                   c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
     "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
     "bgnn_gemm_f32_planes": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,
                                      c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_sz, c_p]),
+    "bgnn_gemm_f32_scaled": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,
+                                     c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "bgnn_absmax_f32": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p]),
     "bgnn_gemm_f32_ex": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p,
                                  c_i64, c_p, c_i32, c_p, c_sz, c_p]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,

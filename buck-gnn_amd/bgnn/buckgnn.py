@@ -204,12 +204,13 @@ class BuckGNN(nn.Module):
         if self._fused_ok(x) and aggr in ("add", "sum", "mean"):
             graph = graph_for(edge_index, x.size(0))
             red = 1 if aggr == "mean" else 0
+            amax = None   # max|x| of the running features: each layer's apply kernel folds it in
             for i in range(L):
                 conv = convs[i] if convs is not None else self.shared_graphsage_block
                 bn = bns[i] if bns is not None else None
                 skip = 0 < i < L - 1
-                x = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
-                               skip, p, self.training, self._seed())
+                x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
+                                     skip, p, self.training, self._seed(), x_amax=amax, return_amax=True)
             return x
         for i in range(L):
             x_prev = x

@@ -92,10 +92,25 @@ def _operand(x):
     return x.data_ptr(), x.stride(0), 0, 0
 
 
+def absmax(x: torch.Tensor, out: torch.Tensor = None, accumulate: bool = False) -> torch.Tensor:
+    """max |x| of a row-major fp32 matrix (unit column stride) into a 1-element device tensor
+    (bgnn_absmax_f32; accumulate folds into out's current value)."""
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=x.device)
+        accumulate = False
+    x2 = x.reshape(x.size(0), -1) if x.dim() != 2 else x
+    _lib.call("bgnn_absmax_f32", x2.data_ptr(), x2.size(0), x2.size(1), x2.stride(0), out.data_ptr(),
+              int(accumulate), _stream())
+    return out
+
+
 def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float = 0.0, alpha: float = 1.0,
-         bias: torch.Tensor = None, relu: bool = False):
+         bias: torch.Tensor = None, relu: bool = False, a_amax: torch.Tensor = None,
+         b_amax: torch.Tensor = None, c_amax: torch.Tensor = None):
     """C = act(alpha * op(a) @ op(b) + beta * C + bias) (fp32, row-major operands, unit column
-    stride). `a` and `out` may be Planes (bgnn_gemm_f32_planes)."""
+    stride). `a` and `out` may be Planes. a_amax / b_amax: optional device scalars holding
+    max|a| / max|b| (the f16x3 operand scales; computed inside when absent); c_amax: optional
+    device scalar that max |C| is folded into (bgnn_gemm_f32_scaled)."""
     M = a.size(1) if trans_a else a.size(0)
     K = a.size(0) if trans_a else a.size(1)
     N = b.size(0) if trans_b else b.size(1)
@@ -130,9 +145,9 @@ def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float
     pc, ldc, c_blk, c_ps = _operand(out)
     ws_bytes = _lib.query("bgnn_gemm_ws_bytes", M, N, K, int(trans_a), int(trans_b))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=b.device) if ws_bytes else None
-    _lib.call("bgnn_gemm_f32_planes", int(trans_a), int(trans_b), M, N, K, float(alpha), pa, lda, a_blk, a_ps,
+    _lib.call("bgnn_gemm_f32_scaled", int(trans_a), int(trans_b), M, N, K, float(alpha), pa, lda, a_blk, a_ps,
               pb, ldb, float(beta), pc, ldc, c_blk, c_ps, None if bias is None else bias.data_ptr(), int(relu),
-              None if ws is None else ws.data_ptr(), ws_bytes, _stream())
+              _ptr(a_amax), _ptr(b_amax), _ptr(c_amax), None if ws is None else ws.data_ptr(), ws_bytes, _stream())
     return out
 
 
@@ -205,21 +220,30 @@ class LayerConfig:
 
 
 class SageLayerFn(torch.autograd.Function):
+    """Outputs (x_next, max|x_next|): the second output (non-differentiable) is the f16x3 GEMM
+    operand scale of the next layer, folded in by bgnn_sage_apply at no extra pass."""
+
     @staticmethod
-    def forward(ctx, x_prev, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
+    def forward(ctx, x_prev, x_amax, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
                 cfg: LayerConfig):
         N, H = x_prev.shape
         dev = x_prev.device
         x_prev = x_prev.contiguous()
         wcat = torch.cat([w_l, w_r], 0).contiguous()             # [2H, H]
+        # operand maxima: [0] = max|W|, [1] = max|x_next| (this layer's output), [2] = max|dz|
+        amax = torch.zeros(3, dtype=torch.float32, device=dev)
+        w_amax, next_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
+        absmax(wcat, w_amax, accumulate=True)
+        if x_amax is None:
+            x_amax = absmax(x_prev)
         planes = Z_PLANES and H % PLANE_TILE == 0
         with _timed("gemm_fwd"):
             if planes:   # z = [z_l ; z_r] as two dense [N, H] planes
                 z = torch.empty(2, N, H, dtype=torch.float32, device=dev)
-                gemm(x_prev, wcat, trans_a=False, trans_b=True, out=Planes(z))
+                gemm(x_prev, wcat, trans_a=False, trans_b=True, out=Planes(z), a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z[0], z[1], H
             else:        # interleaved [N, 2H]
-                z = gemm(x_prev, wcat, trans_a=False, trans_b=True)
+                z = gemm(x_prev, wcat, trans_a=False, trans_b=True, a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z, z[:, H:], 2 * H
         o = torch.empty(N, H, dtype=torch.float32, device=dev)
         nrm = torch.empty(N, dtype=torch.float32, device=dev)
@@ -249,19 +273,21 @@ class SageLayerFn(torch.autograd.Function):
                 invstd.copy_(torch.rsqrt(running_var + cfg.eps))
         x_next = torch.empty(N, H, dtype=torch.float32, device=dev)
         _lib.call("bgnn_sage_apply", o.data_ptr(), _ptr(scale), _ptr(shift), x_prev.data_ptr(), int(cfg.skip),
-                  float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), s)
+                  float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), s)
         ctx.graph = graph
         ctx.cfg = cfg
         ctx.save_for_backward(x_prev, o, nrm, wcat, gamma if gamma is not None else torch.empty(0, device=dev),
                               scale if scale is not None else torch.empty(0, device=dev),
                               shift if shift is not None else torch.empty(0, device=dev),
                               mean if mean is not None else torch.empty(0, device=dev),
-                              invstd if invstd is not None else torch.empty(0, device=dev))
-        return x_next
+                              invstd if invstd is not None else torch.empty(0, device=dev),
+                              x_amax, w_amax, dz_amax)
+        ctx.mark_non_differentiable(next_amax)
+        return x_next, next_amax
 
     @staticmethod
-    def backward(ctx, g):
-        x_prev, o, nrm, wcat, gamma, scale, shift, mean, invstd = ctx.saved_tensors
+    def backward(ctx, g, _g_amax):
+        x_prev, o, nrm, wcat, gamma, scale, shift, mean, invstd, x_amax, w_amax, dz_amax = ctx.saved_tensors
         cfg: LayerConfig = ctx.cfg
         graph: Graph = ctx.graph
         g = g.contiguous()
@@ -298,7 +324,7 @@ class SageLayerFn(torch.autograd.Function):
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
                   float(cfg.p), cfg.seed, int(cfg.skip), N, H, dh.data_ptr(), lddz, _ptr(gskip),
-                  part_db.data_ptr(), s)
+                  part_db.data_ptr(), dz_amax.data_ptr(), s)
         db = torch.empty(H, dtype=torch.float32, device=dev)
         _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
         # dz_l = A^T dh (transpose CSR; MEAN scales by the target's in-degree)
@@ -306,25 +332,29 @@ class SageLayerFn(torch.autograd.Function):
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("spmm_bwd"):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
-                      dh.data_ptr(), lddz, H, cfg.reduce, None, dzl.data_ptr(), lddz, _ptr(part), s)
+                      dh.data_ptr(), lddz, H, cfg.reduce, None, dzl.data_ptr(), lddz, _ptr(part),
+                      dz_amax.data_ptr(), s)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
         wcat_t = wcat.t().contiguous() if DGRAD_WT else wcat
         if gskip is not None:
-            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, out=gskip, beta=1.0)
+            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, out=gskip, beta=1.0, a_amax=dz_amax,
+                      b_amax=w_amax)
         else:
-            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT)
-        dw = gemm(dz, x_prev, trans_a=True, trans_b=False)      # [2H, H]
+            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
+        dw = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)      # [2H, H]
         dw_l, dw_r = dw[:H], dw[H:]
         has_affine = bn and gamma.numel() > 0
-        return (dx, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
+        return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
                 None, None, None, None)
 
 
 def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
-               seed: int) -> torch.Tensor:
-    """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN)."""
+               seed: int, x_amax: torch.Tensor = None, return_amax: bool = False):
+    """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
+    x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
+    spares the GEMM a pass over x_prev; return_amax: also return max|x_next|."""
     require_cuda(x_prev, w_l, b_l, w_r, what="sage_layer")
     H = x_prev.size(1)
     if H % 4 or H > 512:
@@ -341,7 +371,9 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
         cfg = LayerConfig(reduce, True, use_batch_stats, float(momentum or 0.0) if bn_module.track_running_stats
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
-        return SageLayerFn.apply(x_prev, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
-                                 bn_module.running_mean, bn_module.running_var, graph, cfg)
-    cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
-    return SageLayerFn.apply(x_prev, w_l, b_l, w_r, None, None, None, None, graph, cfg)
+        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
+                                bn_module.running_mean, bn_module.running_var, graph, cfg)
+    else:
+        cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
+        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg)
+    return out if return_amax else out[0]

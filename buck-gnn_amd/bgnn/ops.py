@@ -46,7 +46,7 @@ def spmm_fwd(csr, x: torch.Tensor, reduce: int, out_rows: int, want_arg: bool = 
     return out, arg
 
 
-def spmm_bwd(csr_t, perm_t, fwd_rowptr, g: torch.Tensor, reduce: int, arg, out_rows: int):
+def spmm_bwd(csr_t, perm_t, fwd_rowptr, g: torch.Tensor, reduce: int, arg, out_rows: int, amax=None):
     g = g.contiguous()
     H = g.size(1)
     gx = torch.empty(out_rows, H, dtype=torch.float32, device=g.device)
@@ -55,7 +55,7 @@ def spmm_bwd(csr_t, perm_t, fwd_rowptr, g: torch.Tensor, reduce: int, arg, out_r
         _lib.call("bgnn_spmm_bwd", csr_t.ref(), None if perm_t is None else perm_t.data_ptr(),
                   None if fwd_rowptr is None else fwd_rowptr.data_ptr(), g.data_ptr(), g.stride(0), H, reduce,
                   None if arg is None else arg.data_ptr(), gx.data_ptr(), gx.stride(0),
-                  None if part is None else part.data_ptr(), _stream())
+                  None if part is None else part.data_ptr(), None if amax is None else amax.data_ptr(), _stream())
     return gx
 
 

@@ -251,14 +251,15 @@ constexpr GemmCfg kCfgs[] = {
 constexpr int kNumCfgs = 9;
 static int g_gemm_cfg = -1;   // -1 = automatic
 static int g_gemm_abl = 0;    // ablation (measurement only)
-static int g_gemm_mode = 1;   // 0 = f32 MFMA kernel, 1 = bf16x6 kernel (gemm_x6.hip, default:
-                              // 1.4x faster on the SAGE shapes at lower error, tools/tune_gemm.py)
+static int g_gemm_mode = 2;   // 0 = f32 MFMA kernel, 1 = bf16x6, 2 = f16x3 (gemm_x6.hip, default:
+                              // half the MFMAs of bf16x6, error below the f32 MFMA's; tools/tune_gemm.py)
 
 void set_gemm_mode(int mode) { g_gemm_mode = mode; }
 int gemm_mode() { return g_gemm_mode; }
 
-// bf16x6 tile choice (tools/tune_gemm.py)
-inline int pick_x6_cfg(int64_t M, int64_t N, int64_t K) {
+// bf16x6 / f16x3 tile choice (tools/tune_gemm.py)
+inline int pick_x6_cfg(int64_t M, int64_t N, int64_t K, int prec) {
+    (void)prec;
     if (M >= 4096 && N >= 128) return 1;              // tall (fwd / dgrad)
     if (M >= 256 && N >= 128 && K >= 8192) return 1;  // short and deep (wgrad, split-K)
     return 0;
@@ -311,7 +312,7 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 using namespace bgnn;
 
 extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
-    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 500,
+    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 600,
                  "gemm: config %d out of range", cfg);
     g_gemm_abl = cfg / 100;
     g_gemm_cfg = cfg % 100;
@@ -320,7 +321,8 @@ extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
 
 // Launch plan of one GEMM call: kernel family, tile config and split-K factor.
 struct Plan {
-    int x6;            // 1 = bf16x6 kernel (gemm_x6.hip), 0 = f32 MFMA
+    int x6;            // 1 = split-precision kernel (gemm_x6.hip), 0 = f32 MFMA
+    int prec;          // split kernel: 0 = bf16x6, 1 = f16x3
     int cfg;           // index into kX6Cfgs / kCfgs
     int bm, bn, bk;    // tile
     int split;
@@ -331,9 +333,11 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
     auto planes_ok = [&](int bm, int bn, int bk) {
         return (a_blk == 0 || a_blk % (ta ? bm : bk) == 0) && (c_blk == 0 || c_blk % bn == 0);
     };
-    if (g_gemm_mode == 1) {
+    if (g_gemm_mode >= 1) {
         p.x6 = 1;
-        p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K);
+        p.prec = g_gemm_mode == 2 ? 1 : 0;
+        p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
+        if (p.prec == 0 && p.cfg > 2) p.cfg = 1;   // 256x256 tiles exceed the LDS with three pieces
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves,
@@ -350,15 +354,36 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
     return p;
 }
 
-extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb) {
-    const int s = make_plan(M, N, K, ta, tb, 0, 0).split;
-    return s > 1 ? (size_t)s * (size_t)M * (size_t)N * sizeof(float) : 0;
+// workspace: [256 B operand-max head (f16x3)] [split-K slabs]
+constexpr size_t kAmaxHead = 256;
+
+static size_t ws_need(const Plan& p, int64_t M, int64_t N) {
+    const size_t head = (p.x6 && p.prec == 1) ? kAmaxHead : 0;
+    return head + (p.split > 1 ? (size_t)p.split * (size_t)M * (size_t)N * sizeof(float) : 0);
 }
 
-extern "C" int bgnn_gemm_f32_planes(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
+extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb) {
+    return ws_need(make_plan(M, N, K, ta, tb, 0, 0), M, N);
+}
+
+extern "C" int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out,
+                               int32_t accumulate, void* stream) {
+    BGNN_REQUIRE(rows >= 0 && cols >= 0 && (ld >= cols || rows <= 1), "absmax: bad shape");
+    BGNN_REQUIRE(out != nullptr, "absmax: null output");
+    hipStream_t s = as_stream(stream);
+    if (!accumulate) BGNN_HIP(hipMemsetAsync(out, 0, sizeof(float), s));
+    if (rows > 0 && cols > 0) {
+        launch_absmax(x, rows, cols, ld, 0, 0, out, s);
+        BGNN_CHECK_LAUNCH();
+    }
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
                                     const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
                                     int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
-                                    int64_t c_pstride, const float* bias, int32_t relu, void* ws, size_t ws_bytes,
+                                    int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
+                                    const float* b_amax, float* c_amax, void* ws, size_t ws_bytes,
                                     void* stream) {
     BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
     BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
@@ -375,15 +400,38 @@ extern "C" int bgnn_gemm_f32_planes(int32_t ta, int32_t tb, int64_t M, int64_t N
     const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
     BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm: too many tiles");
     hipStream_t s = as_stream(stream);
+    const bool h3 = pl.x6 && pl.prec == 1;
+    const size_t head = h3 ? kAmaxHead : 0;
+    if (h3) {
+        BGNN_REQUIRE(ws != nullptr && ws_bytes >= head, "gemm: f16x3 needs the workspace of bgnn_gemm_ws_bytes()");
+        // operand maxima not supplied by the caller: one pass over each operand
+        float* head_amax = static_cast<float*>(ws);
+        if (a_amax == nullptr || b_amax == nullptr) BGNN_HIP(hipMemsetAsync(ws, 0, 2 * sizeof(float), s));
+        if (a_amax == nullptr) {
+            launch_absmax(A, ta ? K : M, ta ? M : K, lda, a_blk, a_pstride, head_amax, s);
+            BGNN_CHECK_LAUNCH();
+            a_amax = head_amax;
+        }
+        if (b_amax == nullptr) {
+            launch_absmax(B, tb ? N : K, tb ? K : N, ldb, 0, 0, head_amax + 1, s);
+            BGNN_CHECK_LAUNCH();
+            b_amax = head_amax + 1;
+        }
+    }
+    float* slabs = ws ? reinterpret_cast<float*>(static_cast<char*>(ws) + head) : nullptr;
+    const size_t slab_bytes = ws_bytes > head ? ws_bytes - head : 0;
     int split = pl.split;
-    if (split > 1 && (ws == nullptr || ws_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
-    GemmArgs g{A, B, C, (float*)ws, M, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
-               a_blk, a_pstride, c_blk, c_pstride};
+    if (split > 1 && (slabs == nullptr || slab_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
+    GemmArgs g{A, B, C, slabs, M, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
+               a_blk, a_pstride, c_blk, c_pstride, a_amax, b_amax, nullptr};
+    // max |C| for the next GEMM's operand scale: in the split kernels' epilogue, else one pass
+    const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1;
+    if (c_amax_fused) g.c_amax = c_amax;
     int64_t kc = (K + split - 1) / split;
     kc = (kc + pl.bk - 1) / pl.bk * pl.bk;
     g.kchunk = kc > 0 ? kc : pl.bk;
     dim3 grid((unsigned)tiles, split);
-    if (pl.x6) launch_x6(ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
+    if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
     else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
     else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
     else if (ta == 1 && tb == 0) launch_cfg<1, 0>(pl.cfg, grid, s, g);
@@ -392,11 +440,24 @@ extern "C" int bgnn_gemm_f32_planes(int32_t ta, int32_t tb, int64_t M, int64_t N
     if (split > 1) {
         int64_t blocks = (M * N + 255) / 256;
         if (blocks > 4096) blocks = 4096;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)ws, split, M, N,
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)slabs, split, M, N,
                            alpha, beta, C, ldc, bias, relu, c_blk, c_pstride);
         BGNN_CHECK_LAUNCH();
     }
+    if (c_amax != nullptr && !c_amax_fused) {
+        launch_absmax(C, M, N, ldc, c_blk, c_pstride, c_amax, s);
+        BGNN_CHECK_LAUNCH();
+    }
     return BGNN_OK;
+}
+
+extern "C" int bgnn_gemm_f32_planes(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
+                                    const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
+                                    int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
+                                    int64_t c_pstride, const float* bias, int32_t relu, void* ws, size_t ws_bytes,
+                                    void* stream) {
+    return bgnn_gemm_f32_scaled(ta, tb, M, N, K, alpha, A, lda, a_blk, a_pstride, B, ldb, beta, C, ldc, c_blk,
+                                c_pstride, bias, relu, nullptr, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 extern "C" int bgnn_gemm_f32_ex(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,

@@ -20,6 +20,9 @@ struct GemmArgs {
     // plane-split storage (0 = dense): A's contiguous dim (K if !TA, M if TA) and C's N dim
     // are cut into blocks of a_blk / c_blk stored a_pstride / c_pstride elements apart
     int64_t a_blk, a_pstride, c_blk, c_pstride;
+    const float* a_amax;   // f16x3 (PREC 1): device max|A| and max|B|, which set the power-of-two
+    const float* b_amax;   // operand scales
+    float* c_amax;         // split kernels, no split-K: max |C| folded in here (NULL = off)
 };
 
 // Base pointer that makes plane-split storage addressable with global coordinates:
@@ -31,13 +34,18 @@ __device__ __forceinline__ const float* plane_base(const float* P, int64_t x0, i
     return P + plane * (pstride - blk);
 }
 
-// f32-accurate GEMM on bf16 MFMAs (gemm_x6.hip): launches the main kernel of tile config
-// `cfg` (index into kX6Cfgs) on grid (tiles, split); abl != 0 selects a timing ablation.
+// f32-accurate GEMMs on 16-bit MFMAs (gemm_x6.hip): prec 0 = bf16x6, 1 = f16x3; launches the
+// main kernel of tile config `cfg` (index into kX6Cfgs) on grid (tiles, split); abl != 0
+// selects a timing ablation.
 struct X6Cfg {
     int bm, bn, waves, blocks_per_cu;
 };
 extern const X6Cfg kX6Cfgs[];
 extern const int kNumX6Cfgs;
-void launch_x6(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
+void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
+// folds max |P| over the rows x cols matrix (ld; plane-split by blk / pstride when blk > 0)
+// into *out (f32 bits, unsigned atomic max; *out must hold a non-negative value)
+void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64_t blk, int64_t pstride,
+                   float* out, hipStream_t s);
 
 }  // namespace bgnn

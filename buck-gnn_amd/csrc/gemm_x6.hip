@@ -1,5 +1,18 @@
-// f32-accurate GEMM on the gfx950 bf16 MFMA (v_mfma_f32_32x32x16_bf16), for the same
-// SAGEConv linears as gemm.hip (Models/BuckGNN.py:135-149; fwd, dgrad, wgrad shapes).
+// f32-accurate GEMMs on the gfx950 16-bit MFMAs, for the same SAGEConv linears as gemm.hip
+// (Models/BuckGNN.py:135-149; fwd, dgrad, wgrad shapes). Two split precisions (PREC):
+//
+// PREC 1 = f16x3 (default). Each operand is scaled by a power of two s = 2^k chosen from its
+// max |value| (max |a| * s in [2^14, 2^15), so nothing overflows the f16 range) and split
+// into two round-to-nearest f16 pieces, a*s = a0 + a1 + e with |a1| <= 2^-11 |a*s| and
+// |e| <= 2^-22 |a*s|. The product is a.b = (a0.b0 + a0.b1 + a1.b0) / (s_a s_b) + O(2^-21 |a||b|)
+// (a1.b1 <= 2^-22, e terms <= 2^-22 each): three f16 MFMAs per f32 product, every
+// f16 x f16 product (11 x 11 bits) exact in the f32 accumulator, and the unscale an exact
+// power-of-two multiply. The representation error stays an order of magnitude below the
+// f32 accumulation error of a K = 512 sum (measured against fp64 in tests/test_gpu_gemm.py).
+// Elements below 2^-39 max|A| (f16 subnormal range after scaling) lose relative precision;
+// their absolute error stays below 2^-39 max|A| |b|.
+//
+// PREC 0 = bf16x6:
 //
 // Every f32 operand element is split exactly into three bf16 pieces by round-to-nearest:
 //   a0 = bf16(a), a1 = bf16(a - a0), a2 = bf16(a - a0 - a1),  a = a0 + a1 + a2
@@ -24,6 +37,8 @@
 namespace bgnn {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -44,6 +59,34 @@ __device__ __forceinline__ void split2(float x, float y, uint32_t& p0, uint32_t&
     x -= __uint_as_float(p1 << 16);
     y -= __uint_as_float(p1 & 0xffff0000u);
     p2 = pack_bf16(x, y);
+}
+
+// two f32 -> packed f16x2 (round to nearest even; v_cvt_pk_f16_f32)
+__device__ __forceinline__ uint32_t pack_f16(float x, float y) {
+    const f32x2 v = {x, y};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+}
+
+// two-way f16 split of the (already scaled) pair (x, y); scalar residuals (no packed f32 VALU)
+__device__ __forceinline__ void split2h(float x, float y, uint32_t& p0, uint32_t& p1) {
+    p0 = pack_f16(x, y);
+    const f16x2 h = __builtin_bit_cast(f16x2, p0);
+    x -= (float)h[0];
+    y -= (float)h[1];
+    p1 = pack_f16(x, y);
+}
+
+// power-of-two operand scale for PREC 1: s = 2^k with max|a| * s in [2^14, 2^15), k clamped to
+// [-126, 126] (zero, Inf or NaN max -> s = 1); inv = 1 / s
+__device__ __forceinline__ void h3_scale(float amax, float& s, float& inv) {
+    const uint32_t b = __float_as_uint(amax) & 0x7fffffffu;
+    int k = 0;
+    if (b != 0 && b < 0x7f800000u) {
+        k = 14 - ((int)(b >> 23) - 127);
+        k = k < -126 ? -126 : (k > 126 ? 126 : k);
+    }
+    s = __uint_as_float((uint32_t)(127 + k) << 23);
+    inv = __uint_as_float((uint32_t)(127 - k) << 23);
 }
 
 // 16-B chunk index of (row, chunk) in a [R][32]-bf16 image
@@ -81,15 +124,33 @@ __device__ __forceinline__ void x6_load(const float* __restrict__ P, int64_t ld,
     }
 }
 
-// split the staged units and write the three piece images (S = piece 0; piece p at S + p*R*4)
-template <int KCONTIG, int R, int NT, int ABL = 0>
-__device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)[R * 4 / NT][8], int t) {
+// split the staged units and write the piece images (S = piece 0; piece p at S + p*R*4);
+// PREC 1 scales by sc first (exact: a power of two)
+template <int KCONTIG, int R, int NT, int PREC, int ABL = 0>
+__device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)[R * 4 / NT][8], int t, float sc) {
     constexpr int NU = R * 4 / NT;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int idx = t + NT * u;
         const int r = KCONTIG ? (idx >> 2) : (idx % R);
         const int c = KCONTIG ? (idx & 3) : (idx / R);
+        const int pos = x6_pos(r, c);
+        if constexpr (PREC == 1) {
+            uint4 q0, q1;
+            if constexpr (ABL == 1) {
+                q0.x = pack_f16(v[u][0], v[u][1]); q0.y = pack_f16(v[u][2], v[u][3]);
+                q0.z = pack_f16(v[u][4], v[u][5]); q0.w = pack_f16(v[u][6], v[u][7]);
+                q1 = q0;
+            } else {
+                split2h(v[u][0] * sc, v[u][1] * sc, q0.x, q1.x);
+                split2h(v[u][2] * sc, v[u][3] * sc, q0.y, q1.y);
+                split2h(v[u][4] * sc, v[u][5] * sc, q0.z, q1.z);
+                split2h(v[u][6] * sc, v[u][7] * sc, q0.w, q1.w);
+            }
+            S[pos] = q0;
+            S[R * 4 + pos] = q1;
+            continue;
+        }
         uint4 q0, q1, q2;
         if constexpr (ABL == 1) {
             q0.x = pack_bf16(v[u][0], v[u][1]); q0.y = pack_bf16(v[u][2], v[u][3]);
@@ -101,7 +162,6 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
             split2(v[u][4], v[u][5], q0.z, q1.z, q2.z);
             split2(v[u][6], v[u][7], q0.w, q1.w, q2.w);
         }
-        const int pos = x6_pos(r, c);
         S[pos] = q0;
         S[R * 4 + pos] = q1;
         S[2 * R * 4 + pos] = q2;
@@ -109,74 +169,172 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
 }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 q) { return __builtin_bit_cast(bf16x8, q); }
+__device__ __forceinline__ f16x8 as_f16x8(uint4 q) { return __builtin_bit_cast(f16x8, q); }
 
 
 
 // the six leading piece products of one 16-deep k-step, small terms first
-template <int TM, int TN>
-__device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const bf16x8 (&a)[TM][3],
-                                       const bf16x8 (&b)[TN][3]) {
+template <int TM, int TN, int PREC, int NP>
+__device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa)[TM][NP],
+                                       const uint4 (&fb)[TN][NP]) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             floatx16 t = acc[i][j];
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], t, 0, 0, 0);
+            if constexpr (PREC == 1) {   // f16x3: the two cross terms, then the leading product
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+                acc[i][j] = t;
+                continue;
+            }
+            bf16x8 a[3], b[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) { a[p] = as_bf16x8(fa[i][p < NP ? p : 0]); b[p] = as_bf16x8(fb[j][p < NP ? p : 0]); }
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], t, 0, 0, 0);
             acc[i][j] = t;
         }
 }
 
-// write one wave's TM x TN accumulator tiles (wave origin r0, c0; tile column origin n0 for
-// the plane base; split-K slab ks): C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-template <int TM, int TN, int WTM, int WTN>
+// Epilogue: each wave writes its TM x TN accumulator tiles one 32-column block at a time
+// into a wave-private LDS stage [TM*32][32] f32 (C/D map of the 32x32 MFMA: col = lane & 31,
+// row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5); one ds_write_b32 group per row, conflict-free)
+// and reads it back as float4 rows (8 lanes per 128-B row segment, conflict-free
+// ds_read_b128), so C leaves as 16-B stores, 1 KiB per wave instruction. Unscale (f16x3),
+// alpha, beta, bias, ReLU and the max |C| (c_amax) are applied per float4.
+template <int TM, int TN, int ABL = 0>
 __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
-                                            int64_t c0, int64_t n0, int ks, int lane) {
-    float* __restrict__ dst = g.split > 1 ? g.ws + (int64_t)ks * g.M * g.N
-                                          : const_cast<float*>(plane_base(g.C, n0, g.c_blk, g.c_pstride));
-    const int64_t ldd = g.split > 1 ? g.N : g.ldc;
+                                            int64_t c0, int64_t n0, int ks, int lane, float ia, float ib,
+                                            float* __restrict__ stage) {
+    const bool split = g.split > 1;
+    float* __restrict__ dst = split ? g.ws + (int64_t)ks * g.M * g.N
+                                    : const_cast<float*>(plane_base(g.C, n0, g.c_blk, g.c_pstride));
+    const int64_t ldd = split ? g.N : g.ldc;
+    const bool vec = (((uintptr_t)dst & 15) == 0) && (ldd % 4 == 0);
+    const bool bias_vec = g.bias && (((uintptr_t)g.bias & 15) == 0);
     const int li = lane & 31, lh = lane >> 5;
+    const int rq = lane >> 3, c4 = (lane & 7) * 4;
+    uint32_t cmax = 0;
+    // interior tile, no split-K, no beta, aligned: per-column-block bias and pointer, per-row
+    // pointer increments only (the general path below recomputes everything per float4)
+    const bool fast = !split && vec && g.beta == 0.f && (!g.bias || bias_vec) && r0 + TM * 32 <= g.M &&
+                      c0 + TN * 32 <= g.N;
+    const float iab = ia * ib;   // exact unless the two scales over/underflow together
+    const bool one_mul = iab != 0.f && iab < 3.0e38f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int64_t col = c0 + j * 32 + li;
-            if (col >= g.N) continue;
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t row = r0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (row >= g.M) continue;
-                float v = acc[i][j][r];
-                if (g.split > 1) {
-                    dst[row * ldd + col] = v;
-                } else {
-                    v *= g.alpha;
-                    if (g.beta != 0.f) v += g.beta * dst[row * ldd + col];
-                    if (g.bias) v += g.bias[col];
+            for (int r = 0; r < 16; ++r) stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (fast) {
+            const int64_t col = c0 + j * 32 + c4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (g.bias) bv = *reinterpret_cast<const float4*>(g.bias + col);
+            float* p = dst + (r0 + rq) * ldd + col;
+            const int64_t step = 8 * ldd;
+#pragma unroll
+            for (int q = 0; q < TM * 4; ++q, p += step) {
+                const float4 sv = *reinterpret_cast<const float4*>(stage + (q * 8 + rq) * 32 + c4);
+                float e[4] = {sv.x, sv.y, sv.z, sv.w};
+                const float b4[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float v = one_mul ? e[k] * iab : (e[k] * ia) * ib;
+                    if (g.alpha != 1.f) v *= g.alpha;
+                    if (g.bias) v += b4[k];
                     if (g.relu) v = fmaxf(v, 0.f);
-                    dst[row * ldd + col] = v;
+                    e[k] = v;
+                    cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
+                }
+                if (ABL == 5 && e[0] != 1234.5f) continue;   // ablation: no C stores
+                *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            continue;
+        }
+        const int64_t col = c0 + j * 32 + c4;
+#pragma unroll
+        for (int q = 0; q < TM * 4; ++q) {
+            const int rr = q * 8 + rq;
+            const float4 sv = *reinterpret_cast<const float4*>(stage + rr * 32 + c4);
+            const int64_t row = r0 + rr;
+            float e[4] = {(sv.x * ia) * ib, (sv.y * ia) * ib, (sv.z * ia) * ib, (sv.w * ia) * ib};
+            if (ABL == 5 && e[0] != 1234.5f) continue;   // ablation: no C stores
+            if (row >= g.M || col >= g.N) continue;
+            float* p = dst + row * ldd + col;
+            const bool full = vec && col + 3 < g.N;
+            if (!split) {
+                float prev[4] = {0.f, 0.f, 0.f, 0.f}, bv[4] = {0.f, 0.f, 0.f, 0.f};
+                if (g.beta != 0.f) {
+                    if (full) {
+                        const float4 t = *reinterpret_cast<const float4*>(p);
+                        prev[0] = t.x; prev[1] = t.y; prev[2] = t.z; prev[3] = t.w;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) prev[k] = col + k < g.N ? p[k] : 0.f;
+                    }
+                }
+                if (g.bias) {
+                    if (bias_vec && col + 3 < g.N) {
+                        const float4 t = *reinterpret_cast<const float4*>(g.bias + col);
+                        bv[0] = t.x; bv[1] = t.y; bv[2] = t.z; bv[3] = t.w;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) bv[k] = col + k < g.N ? g.bias[col + k] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float v = e[k] * g.alpha;
+                    if (g.beta != 0.f) v += g.beta * prev[k];
+                    if (g.bias) v += bv[k];
+                    if (g.relu) v = fmaxf(v, 0.f);
+                    e[k] = v;
+                    if (col + k < g.N) cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
                 }
             }
+            if (full) {
+                *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (col + k < g.N) p[k] = e[k];
+            }
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (g.c_amax && !split) {
+        for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, o, kWave));
+        if (lane == 0 && cmax) atomicMax(reinterpret_cast<uint32_t*>(g.c_amax), cmax);
+    }
 }
 
-// ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored three
-// times), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA + barriers),
-// 4 = MFMA + barriers only.
-template <int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
+// ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored in
+// every piece slot), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA +
+// barriers), 4 = MFMA + barriers only, 5 = everything but the C stores.
+template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int NT = 64 * WM * WN;
+    constexpr int NP = PREC == 1 ? 2 : 3;   // pieces per operand
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
     static_assert(BM * 4 % NT == 0 && BN * 4 % NT == 0, "staging units must divide evenly");
-    // [buffer][piece][row][4 chunks of 8 bf16]
-    __shared__ uint4 As[2][3 * BM * 4];
-    __shared__ uint4 Bs[2][3 * BN * 4];
+    // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
+    // epilogue as one [TM*32][32] f32 stage per wave
+    constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
+    static_assert((2 * (A_U4 + B_U4)) * 16 >= WM * WN * TM * 32 * 32 * 4, "epilogue stage exceeds the LDS tiles");
+    __shared__ uint4 smem[2 * (A_U4 + B_U4)];
+    uint4 (*As)[A_U4] = reinterpret_cast<uint4 (*)[A_U4]>(smem);
+    uint4 (*Bs)[B_U4] = reinterpret_cast<uint4 (*)[B_U4]>(smem + 2 * A_U4);
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -197,6 +355,12 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
 
     const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % 4 == 0);
     const bool b_vec = (((uintptr_t)g.B & 15) == 0) && (g.ldb % 4 == 0);
+
+    float sa = 1.f, sb = 1.f, ia = 1.f, ib = 1.f;
+    if constexpr (PREC == 1) {
+        h3_scale(*g.a_amax, sa, ia);
+        h3_scale(*g.b_amax, sb, ib);
+    }
 
     floatx16 acc[TM][TN];
 #pragma unroll
@@ -220,8 +384,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         }
     };
     auto store_ab = [&](int buf) {
-        x6_store<AK, BM, NT, ABL>(As[buf], ra, t);
-        x6_store<BKc, BN, NT, ABL>(Bs[buf], rb, t);
+        x6_store<AK, BM, NT, PREC, ABL>(As[buf], ra, t, sa);
+        x6_store<BKc, BN, NT, PREC, ABL>(Bs[buf], rb, t, sb);
     };
     // Pipeline: slice t+1 is split and written to the free LDS buffer, slice t+2 is loaded
     // into registers, then slice t is multiplied; one barrier per slice.
@@ -239,75 +403,138 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         if (kt + 2 < nk && ABL != 2 && ABL < 3) load_ab(kb + (kt + 2) * X6_BK);
 #pragma unroll
         for (int kk = 0; kk < X6_BK / 16; ++kk) {
-            bf16x8 a[TM][3], b[TN][3];
+            uint4 a[TM][NP], b[TN][NP];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int row = wm * (BM / WM) + i * 32;
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    if constexpr (ABL == 4) {
-                        a[i][p] = as_bf16x8(make_uint4(row + p, kk, i, (int)kt));
-                    } else {
-                        a[i][p] = as_bf16x8(As[cur][p * BM * 4 + x6_pos(row + li, 2 * kk + lh)]);
-                    }
+                for (int p = 0; p < NP; ++p) {
+                    if constexpr (ABL == 4) a[i][p] = make_uint4(row + p, kk, i, (int)kt);
+                    else a[i][p] = As[cur][p * BM * 4 + x6_pos(row + li, 2 * kk + lh)];
                 }
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int row = wn * (BN / WN) + j * 32;
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    if constexpr (ABL == 4) {
-                        b[j][p] = as_bf16x8(make_uint4(row - p, kk, j, (int)kt));
-                    } else {
-                        b[j][p] = as_bf16x8(Bs[cur][p * BN * 4 + x6_pos(row + li, 2 * kk + lh)]);
-                    }
+                for (int p = 0; p < NP; ++p) {
+                    if constexpr (ABL == 4) b[j][p] = make_uint4(row - p, kk, j, (int)kt);
+                    else b[j][p] = Bs[cur][p * BN * 4 + x6_pos(row + li, 2 * kk + lh)];
                 }
             }
-            x6_mma<TM, TN>(acc, a, b);
+            x6_mma<TM, TN, PREC, NP>(acc, a, b);
         }
         __syncthreads();
     }
-    x6_epilogue<TM, TN, BM / WM, BN / WN>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane);
+    // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
+    float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
+    x6_epilogue<TM, TN, ABL>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
 }
 
+// bm, bn, waves, workgroups per CU; configs 3 and 4 (128 KB of LDS) are built for f16x3 only
 const X6Cfg kX6Cfgs[] = {
     {128, 128, 4, 1},   // 0: 2x2 waves of 64x64 (1 wave / SIMD)
     {256, 128, 8, 1},   // 1: 4x2 waves of 64x64 (2 waves / SIMD)
     {128, 256, 8, 1},   // 2: 2x4 waves of 64x64
+    {256, 256, 8, 1},   // 3: 2x4 waves of 128x64
+    {256, 256, 8, 1},   // 4: 4x2 waves of 64x128
 };
-const int kNumX6Cfgs = 3;
+const int kNumX6Cfgs = 5;
 
-template <int TA, int TB, int ABL>
+template <int PREC, int TA, int TB, int ABL>
 static void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if constexpr (PREC == 1) {
+        if (cfg == 3) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); return; }
+        if (cfg == 4) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL>), grid, dim3(512), 0, s, g); return; }
+    }
     switch (cfg) {
-        case 0: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 128, 128, 2, 2, ABL>), grid, dim3(256), 0, s, g); break;
-        case 1: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 256, 128, 4, 2, ABL>), grid, dim3(512), 0, s, g); break;
-        default: hipLaunchKernelGGL((k_gemm_x6<TA, TB, 128, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); break;
+        case 0: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 128, 2, 2, ABL>), grid, dim3(256), 0, s, g); break;
+        case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); break;
+        default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL>), grid, dim3(512), 0, s, g); break;
     }
 }
 
-template <int TA, int TB>
+template <int PREC, int TA, int TB>
 static void launch_x6_t(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    if (abl == 0) { launch_x6_a<TA, TB, 0>(cfg, grid, s, g); return; }
+    if (abl == 0) { launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g); return; }
     // ablations are built for the forward shape only (TA = 0, TB = 1)
     if constexpr (TA == 0 && TB == 1) {
         switch (abl) {
-            case 1: launch_x6_a<TA, TB, 1>(cfg, grid, s, g); break;
-            case 2: launch_x6_a<TA, TB, 2>(cfg, grid, s, g); break;
-            case 3: launch_x6_a<TA, TB, 3>(cfg, grid, s, g); break;
-            default: launch_x6_a<TA, TB, 4>(cfg, grid, s, g); break;
+            case 1: launch_x6_a<PREC, TA, TB, 1>(cfg, grid, s, g); break;
+            case 2: launch_x6_a<PREC, TA, TB, 2>(cfg, grid, s, g); break;
+            case 3: launch_x6_a<PREC, TA, TB, 3>(cfg, grid, s, g); break;
+            case 4: launch_x6_a<PREC, TA, TB, 4>(cfg, grid, s, g); break;
+            default: launch_x6_a<PREC, TA, TB, 5>(cfg, grid, s, g); break;
         }
     } else {
-        launch_x6_a<TA, TB, 0>(cfg, grid, s, g);
+        launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);
     }
 }
 
-void launch_x6(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    if (ta == 0 && tb == 0) launch_x6_t<0, 0>(cfg, abl, grid, s, g);
-    else if (ta == 0 && tb == 1) launch_x6_t<0, 1>(cfg, abl, grid, s, g);
-    else if (ta == 1 && tb == 0) launch_x6_t<1, 0>(cfg, abl, grid, s, g);
-    else launch_x6_t<1, 1>(cfg, abl, grid, s, g);
+template <int PREC>
+static void launch_prec(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if (ta == 0 && tb == 0) launch_x6_t<PREC, 0, 0>(cfg, abl, grid, s, g);
+    else if (ta == 0 && tb == 1) launch_x6_t<PREC, 0, 1>(cfg, abl, grid, s, g);
+    else if (ta == 1 && tb == 0) launch_x6_t<PREC, 1, 0>(cfg, abl, grid, s, g);
+    else launch_x6_t<PREC, 1, 1>(cfg, abl, grid, s, g);
+}
+
+void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if (prec == 1) launch_prec<1>(ta, tb, cfg, abl, grid, s, g);
+    else launch_prec<0>(ta, tb, cfg > 2 ? 1 : cfg, abl, grid, s, g);
+}
+
+// max |x| over a strided (optionally plane-split) matrix, folded into *out by an unsigned
+// atomic max on the f32 bits (monotone for non-negative floats; NaN compares above Inf).
+// tpr threads per row (a power of two dividing 256) sweep a row's float4 (or float) columns;
+// 256 / tpr rows per block step; no integer division inside the loops.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ P, int64_t rows, int64_t cols, int64_t ld,
+                                                int64_t blk, int64_t pstride, int tpr, uint32_t* __restrict__ out) {
+    const int rpi = 256 / tpr;
+    const int tc = threadIdx.x % tpr;
+    uint32_t m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * rpi + threadIdx.x / tpr; r < rows; r += (int64_t)gridDim.x * rpi) {
+        if constexpr (VEC) {
+            const float4* row = reinterpret_cast<const float4*>(P + r * ld);
+            for (int64_t c = tc; c < cols / 4; c += tpr) {
+                const float4 v = row[c];
+                m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                               max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+            }
+        } else {
+            int64_t cb = 0;   // plane of column c (blk > 0): element at P + plane * pstride + r * ld + c - plane * blk
+            int64_t c = tc;
+            for (; c < cols; c += tpr) {
+                if (blk > 0) cb = c / blk;
+                const float* base = P + cb * (pstride - blk);
+                m = max(m, __float_as_uint(base[r * ld + c]) & 0x7fffffffu);
+            }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    __shared__ uint32_t red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (m) atomicMax(out, m);
+    }
+}
+
+void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64_t blk, int64_t pstride,
+                   float* out, hipStream_t s) {
+    const bool vec = blk == 0 && cols % 4 == 0 && ld % 4 == 0 && (((uintptr_t)P & 15) == 0);
+    const int64_t units = vec ? cols / 4 : cols;
+    int tpr = 1;
+    while (tpr < 256 && tpr < units) tpr <<= 1;
+    const int64_t rpi = 256 / tpr;
+    int64_t blocks = (rows + rpi - 1) / rpi;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    uint32_t* o = reinterpret_cast<uint32_t*>(out);
+    if (vec) hipLaunchKernelGGL(k_absmax<true>, dim3((unsigned)blocks), dim3(256), 0, s, P, rows, cols, ld, blk, pstride, tpr, o);
+    else hipLaunchKernelGGL(k_absmax<false>, dim3((unsigned)blocks), dim3(256), 0, s, P, rows, cols, ld, blk, pstride, tpr, o);
 }
 
 }  // namespace bgnn

@@ -132,12 +132,26 @@ __global__ void k_bn_eval(int H, const float* __restrict__ gamma, const float* _
 }
 
 // ---------------------------------------------------------------------------
+// Fold a thread's running max |value| (f32 bits) into *amax: block max over 256 threads,
+// then one atomic per block. Must be reached by every thread of the block.
+__device__ __forceinline__ void block_amax(uint32_t* amax, uint32_t m) {
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    __shared__ uint32_t red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (m) atomicMax(amax, m);
+    }
+}
+
 // x_next = drop(relu(o*scale+shift) + skip*x_prev). Grid-stride over float4s.
 __global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o, const float* __restrict__ scale,
                                                     const float* __restrict__ shift,
                                                     const float4* __restrict__ xprev, int skip, uint32_t thr,
                                                     float inv_keep, uint64_t seed, int64_t n4, int H4,
-                                                    float4* __restrict__ xn) {
+                                                    float4* __restrict__ xn, uint32_t* __restrict__ amax) {
+    uint32_t m = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)(i % H4) * 4;
         float4 v = o[i];
@@ -155,12 +169,15 @@ __global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o
             y[0] += p.x; y[1] += p.y; y[2] += p.z; y[3] += p.w;
         }
         if (thr) {
-            const uint32_t m = keep_bits4(seed, (uint64_t)i, thr);
+            const uint32_t keep = keep_bits4(seed, (uint64_t)i, thr);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) y[k] = ((m >> k) & 1u) ? y[k] * inv_keep : 0.f;
+            for (int k = 0; k < 4; ++k) y[k] = ((keep >> k) & 1u) ? y[k] * inv_keep : 0.f;
         }
         xn[i] = make_float4(y[0], y[1], y[2], y[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m = max(m, __float_as_uint(y[k]) & 0x7fffffffu);
     }
+    if (amax) block_amax(amax, m);
 }
 
 // Backward pass 1: partial sums over rows of g2 and g2*xhat per channel.
@@ -235,8 +252,9 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sum_g2,
     const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
     int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
-    float* __restrict__ gskip, float* __restrict__ part) {
+    float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax) {
     const int lane = threadIdx.x & 63;
+    uint32_t tmax = 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lb = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t r0 = (int64_t)lb * rows_per_block;
@@ -321,6 +339,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
             for (int k = 0; k < 4; ++k) {
                 out[k] = through ? (dov[v][k] - ov[v][k] * dot) * rn : dov[v][k] * rn;
                 db[v][k] += out[k];
+                tmax = max(tmax, __float_as_uint(out[k]) & 0x7fffffffu);
             }
             *reinterpret_cast<float4*>(dh + r * lddh + cpos[v]) = make_float4(out[0], out[1], out[2], out[3]);
             if (skip)
@@ -328,6 +347,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
                     make_float4(g1v[v][0], g1v[v][1], g1v[v][2], g1v[v][3]);
         }
     }
+    if (amax) block_amax(amax, tmax);
     __shared__ __attribute__((aligned(16))) float red[4][512];
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -387,7 +407,7 @@ extern "C" int bgnn_bn_eval_coeffs(int32_t H, const float* gamma, const float* b
 
 extern "C" int bgnn_sage_apply(const float* o, const float* scale, const float* shift, const float* x_prev,
                                int32_t skip, float p, uint64_t seed, int64_t n_rows, int32_t H, float* x_next,
-                               void* stream) {
+                               float* amax, void* stream) {
     BGNN_REQUIRE(H > 0 && H % 4 == 0, "sage_apply: H must be a multiple of 4");
     BGNN_REQUIRE(p >= 0.f && p < 1.f, "sage_apply: dropout p must be in [0, 1)");
     BGNN_REQUIRE((scale == nullptr) == (shift == nullptr), "sage_apply: scale/shift must both be set or NULL");
@@ -402,7 +422,8 @@ extern "C" int bgnn_sage_apply(const float* o, const float* scale, const float* 
     const uint32_t thr = dropout_threshold(p);
     const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
     hipLaunchKernelGGL(k_sage_apply, dim3((unsigned)blocks), dim3(256), 0, s, (const float4*)o, scale, shift,
-                       (const float4*)x_prev, skip, thr, inv_keep, seed, n4, H / 4, (float4*)x_next);
+                       (const float4*)x_prev, skip, thr, inv_keep, seed, n4, H / 4, (float4*)x_next,
+                       reinterpret_cast<uint32_t*>(amax));
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
@@ -434,7 +455,7 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
                                   const float* shift, const float* gamma, const float* mean, const float* invstd,
                                   const float* sum_g2, const float* sum_g2xhat, float p, uint64_t seed,
                                   int32_t skip, int64_t n_rows, int32_t H, float* dh, int64_t lddh, float* gskip,
-                                  float* partial_db, void* stream) {
+                                  float* partial_db, float* amax, void* stream) {
     BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 512, "sage_bwd_rows: H=%d unsupported", H);
     BGNN_REQUIRE(lddh >= H && lddh % 4 == 0, "sage_bwd_rows: bad lddh");
     BGNN_REQUIRE(!skip || gskip, "sage_bwd_rows: skip requires gskip");
@@ -449,11 +470,11 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
     if (H > 256)
         hipLaunchKernelGGL(k_sage_bwd_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db);
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax));
     else
         hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db);
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax));
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

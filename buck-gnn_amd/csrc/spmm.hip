@@ -52,7 +52,15 @@ struct SegArgs {
     float* bn_partial;  // [slots, 2, H]
     int32_t light_slots;
     int32_t nt;         // stream-once data (z_r rows, output rows) with non-temporal hints
+    uint32_t* amax;     // plain epilogue: max |out| folded in (f32 bits, atomic max; NULL = off)
 };
+
+// fold a lane's running max |out| into *amax: wave max, then one atomic per wave
+__device__ __forceinline__ void amax_flush_wave(uint32_t* amax, uint32_t m) {
+    if (!amax) return;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(amax, m);
+}
 
 
 // 1 / max(deg, 1), correctly rounded, identical in every kernel (MEAN backward weights)
@@ -210,7 +218,7 @@ __device__ __forceinline__ void gather_range(const SegArgs& A, Acc<VEC, NV, OP>&
 template <int VEC, int NV, int OP>
 __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& acc, int64_t r,
                                             int32_t deg, const int (&cpos)[NV],
-                                            const bool (&cok)[NV]) {
+                                            const bool (&cok)[NV], uint32_t& tmax) {
     const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -221,6 +229,7 @@ __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& 
             float t = acc.a[v][k];
             if constexpr (OP == OP_MAX) t = (deg > 0) ? t : 0.f;
             o.f[k] = t * sc;
+            tmax = max(tmax, __float_as_uint(o.f[k]) & 0x7fffffffu);
         }
         if constexpr (VEC == 4) {
             if (A.nt) st_nt(A.out + r * A.ldo + cpos[v], o);
@@ -320,6 +329,7 @@ __global__ __launch_bounds__(256) void k_seg_light(SegArgs A) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) bs[v][k] = bq[v][k] = 0.f;
     }
+    uint32_t tmax = 0;
 
     for (int64_t rb = r_begin + (int64_t)wave * RPW; rb < r_end; rb += 4 * RPW) {
         const int64_t r = (RPW == 1) ? rb : rb + sub;
@@ -333,9 +343,10 @@ __global__ __launch_bounds__(256) void k_seg_light(SegArgs A) {
         if constexpr (EPI == EPI_SAGE) {
             store_sage<NV, OP>(A, *reinterpret_cast<Acc<4, NV, OP>*>(&acc), r, deg, cpos, cok, bs, bq);
         } else {
-            store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok);
+            store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok, tmax);
         }
     }
+    if constexpr (EPI == EPI_PLAIN) amax_flush_wave(A.amax, tmax);
 
     if constexpr (EPI == EPI_SAGE) {
         // block-reduce the BatchNorm partial sums over the 4 waves -> slot lb
@@ -445,7 +456,9 @@ __global__ __launch_bounds__(64) void k_seg_combine(SegArgs A) {
                 st<4>(dst + A.H + cpos[v], s2);
             }
     } else {
-        store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok);
+        uint32_t tmax = 0;
+        store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok, tmax);
+        if (A.amax && tmax) atomicMax(A.amax, tmax);   // one heavy row per wave: few atomics
     }
 }
 
@@ -554,6 +567,7 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
         __syncthreads();
     }
     const int32_t chunk = A.chunk;
+    uint32_t tmax = 0;
 
     for (int t0 = 0; t0 < sw.T; t0 += 64) {
         const int nrow = min(64, sw.T - t0);
@@ -620,10 +634,11 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
                 }
                 if (lane == 0) A.nrm[r] = n;
             } else {
-                store_plain<4, NV, OP>(A, acc, r, deg, cpos, cok);
+                store_plain<4, NV, OP>(A, acc, r, deg, cpos, cok, tmax);
             }
         }
     }
+    if constexpr (EPI == EPI_PLAIN) amax_flush_wave(A.amax, tmax);
 
     if constexpr (EPI == EPI_SAGE) {
         __syncthreads();
@@ -778,6 +793,7 @@ using namespace bgnn;
 
 extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H, int32_t reduce,
                              float* out, int64_t ldo, int32_t* arg, float* partial, void* stream) {
+    // (no max |out| here: nothing downstream scales by it)
     BGNN_REQUIRE(csr && csr->rowptr, "spmm_fwd: null csr");
     BGNN_REQUIRE(H > 0 && ldx >= H && ldo >= H, "spmm_fwd: bad H/ld");
     BGNN_REQUIRE(reduce >= 0 && reduce <= 2, "spmm_fwd: bad reduce %d", reduce);
@@ -802,7 +818,7 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
 
 extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                              const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
-                             float* gx, int64_t ldgx, float* partial, void* stream) {
+                             float* gx, int64_t ldgx, float* partial, float* amax, void* stream) {
     BGNN_REQUIRE(csr_t && csr_t->rowptr, "spmm_bwd: null csr");
     BGNN_REQUIRE(H > 0 && ldg >= H && ldgx >= H, "spmm_bwd: bad H/ld");
     BGNN_REQUIRE(csr_t->n_chunks == 0 || partial, "spmm_bwd: partial scratch required");
@@ -814,6 +830,7 @@ extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, con
     A.fwd_rowptr = fwd_rowptr;
     A.perm_t = perm_t;
     A.arg_in = arg;
+    A.amax = reinterpret_cast<uint32_t*>(amax);
     const bool al = aligned16(g) && aligned16(gx) && ldg % 4 == 0 && ldgx % 4 == 0 &&
                     (!partial || aligned16(partial)) && (!arg || aligned16(arg));
     const Geometry geo = pick_geometry(H, al);
@@ -859,7 +876,7 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             return BGNN_OK;
         case BGNN_TUNE_SEG_NT: g_seg_nt = value ? 1 : 0; return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
-            BGNN_REQUIRE(value == 0 || value == 1, "set_tuning: gemm mode must be 0 (f32) or 1 (bf16x6)");
+            BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: gemm mode must be 0 (f32), 1 (bf16x6) or 2 (f16x3)");
             set_gemm_mode(value);
             return BGNN_OK;
         default: return fail(BGNN_E_ARG, "set_tuning: unknown knob %d", knob);

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 1
+#define BGNN_ABI_VERSION 2
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -64,7 +64,7 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_SEG_BLOCKS 2   /* sweep grid in blocks (default 1024)                   */
 #define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (12), 8, 12, 16  */
 #define BGNN_TUNE_SEG_NT 4       /* non-temporal hints on stream-once rows (default 1)       */
-#define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6 f32-accurate (default) */
+#define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (default) */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);
@@ -139,10 +139,12 @@ int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H,
  *   MEAN: gx[j] = sum_{q in rowT j} g[col_t[q]] / max(deg_fwd(col_t[q]), 1)
  *   MAX : gx[j, c] = sum_{q in rowT j, arg[col_t[q], c] == perm_t[q]} g[col_t[q], c]
  * `fwd_rowptr` is the forward CSR's rowptr (for MEAN degrees); `perm_t` and `arg`
- * are needed for MAX only. Deterministic (gather form, no atomics). */
+ * are needed for MAX only. Deterministic (gather form, no atomics on gx).
+ * amax (optional): *amax = max(*amax, max |gx|), the operand scale of the f16x3 GEMMs
+ * that consume gx (bgnn_gemm_f32_scaled). */
 int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                   const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
-                  float* gx, int64_t ldgx, float* partial, void* stream);
+                  float* gx, int64_t ldgx, float* partial, float* amax, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused SAGE layer (Models/BuckGNN.py:430-444, transform-first order):
@@ -174,10 +176,11 @@ int bgnn_bn_eval_coeffs(int32_t H, const float* gamma, const float* beta, float 
 /* x_next = Dropout_p( ReLU(o*scale + shift) + (skip ? x_prev : 0) ).
  * scale/shift NULL => identity (no BatchNorm, the *_Shared variant).
  * The dropout mask is a counter-based hash of (seed, element index): keep with
- * probability 1-p, scaled by 1/(1-p); p == 0 disables dropout. */
+ * probability 1-p, scaled by 1/(1-p); p == 0 disables dropout.
+ * amax (optional): *amax = max(*amax, max |x_next|) (next layer's GEMM operand scale). */
 int bgnn_sage_apply(const float* o, const float* scale, const float* shift,
                     const float* x_prev, int32_t skip, float p, uint64_t seed,
-                    int64_t n_rows, int32_t H, float* x_next, void* stream);
+                    int64_t n_rows, int32_t H, float* x_next, float* amax, void* stream);
 
 /* Backward pass 1: BatchNorm statistics of the incoming gradient g (= dL/dx_next):
  *   g2 = relu'(o*scale+shift) * dropout'(g);  partial sums of g2 and g2*xhat. */
@@ -196,22 +199,27 @@ int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
  * backward, giving dh [N, H] (ld = lddh). If skip, writes dropout'(g) into
  * gskip [N, H] (the skip branch's gradient, the initial value of dL/dx_prev).
  * Partial sums of dh (for db_l) go to partial_db [slots, 2, H] (second half 0).
- * sum_g2 / sum_g2xhat are the reduced stats of pass 1 (NULL when BatchNorm is off). */
+ * sum_g2 / sum_g2xhat are the reduced stats of pass 1 (NULL when BatchNorm is off).
+ * amax (optional): *amax = max(*amax, max |dh|). */
 int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
                        const float* scale, const float* shift, const float* gamma,
                        const float* mean, const float* invstd,
                        const float* sum_g2, const float* sum_g2xhat,
                        float p, uint64_t seed, int32_t skip,
                        int64_t n_rows, int32_t H, float* dh, int64_t lddh,
-                       float* gskip, float* partial_db, void* stream);
+                       float* gskip, float* partial_db, float* amax, void* stream);
 
 /* ------------------------------------------------------------------------
  * fp32 GEMM (f32 operands, f32 result, f32 accumulation):
  *   C[M,N] = alpha * op(A)[M,K] · op(B)[K,N] + beta * C
- * Two kernel families (BGNN_TUNE_GEMM_MODE): 1 (default) splits every operand exactly
- * into three bf16 pieces and sums the six leading piece products on the bf16 MFMA
- * (dropped terms <= 2^-23 |a||b| per product, measured error below the f32 MFMA's);
- * 0 runs the f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain).
+ * Three kernel families (BGNN_TUNE_GEMM_MODE):
+ *   2 (default) f16x3: each operand is scaled by a power of two from its max |value| and
+ *     split into two f16 pieces; three f16 MFMAs per product (a0b0 + a0b1 + a1b0), f32
+ *     accumulation, exact unscale (dropped terms <= ~2^-21 |a||b|; measured error vs fp64 at
+ *     or below the f32 MFMA's). Needs the workspace of bgnn_gemm_ws_bytes() (the operand
+ *     maxima live there unless the caller passes them to bgnn_gemm_f32_scaled).
+ *   1 bf16x6: three exact bf16 pieces per operand, six products (dropped <= 2^-23 |a||b|).
+ *   0 the f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain).
  * trans_a = 0: A is [M,K] row-major (lda >= K); 1: A is [K,M] row-major (lda >= M).
  * trans_b = 0: B is [K,N] row-major (ldb >= N);  1: B is [N,K] row-major (ldb >= K).
  * C is [M,N] row-major (ldc >= N). `ws` is scratch for split-K (may be NULL when
@@ -235,6 +243,21 @@ int bgnn_gemm_f32_ex(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int
  * trans_a = 1) is cut into blocks of a_blk elements stored a_pstride elements apart
  * (element index x -> (x / a_blk) * a_pstride + x % a_blk); C's N dimension likewise with
  * c_blk / c_pstride. 0 = dense. Blocks must be multiples of the kernel's tile. */
+/* Plane-split GEMM with caller-supplied operand maxima for f16x3 (a_amax = max|A|,
+ * b_amax = max|B| as device floats, e.g. from bgnn_absmax_f32 or a producer kernel; the
+ * exact max gives full accuracy, a larger value loses precision gradually, a smaller one is
+ * undefined). NULL = computed here (one read pass). c_amax (optional, any mode): *c_amax =
+ * max(*c_amax, max |C|) over the result (fused into the epilogue when possible), so the
+ * result can feed the next GEMM without another pass. */
+int bgnn_gemm_f32_scaled(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                         float alpha, const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride,
+                         const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                         int64_t c_blk, int64_t c_pstride, const float* bias, int32_t relu,
+                         const float* a_amax, const float* b_amax, float* c_amax,
+                         void* ws, size_t ws_bytes, void* stream);
+/* *out = max(accumulate ? *out : 0, max |x|) over a row-major [rows, cols] matrix (ld). */
+int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out,
+                    int32_t accumulate, void* stream);
 int bgnn_gemm_f32_planes(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                          float alpha, const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride,
                          const float* B, int64_t ldb, float beta, float* C, int64_t ldc,

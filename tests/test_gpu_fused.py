@@ -55,8 +55,10 @@ def test_fused_layer_matches_oracle(dev, aggr, red, bn, training, skip, H):
     rm, rv = d["rm"].detach().clone(), d["rv"].detach().clone()
     xd = x.to(dev).requires_grad_(True)
     cfg = fused.LayerConfig(red, bn, training, 0.1, 1e-5, skip, 0.0, 123)
-    out = fused.SageLayerFn.apply(xd, d["w_l"], d["b_l"], d["w_r"], d["gamma"] if bn else None,
-                                  d["beta"] if bn else None, rm if bn else None, rv if bn else None, graph, cfg)
+    out, amax = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"] if bn else None,
+                                        d["beta"] if bn else None, rm if bn else None, rv if bn else None, graph,
+                                        cfg)
+    assert amax.item() == out.detach().abs().max().item()   # next layer's operand scale, exact
     up = torch.randn_like(out)
     out.backward(up)
     ro, xc, t = oracle_layer(x, b.edge_index, p, aggr, bn, training, skip)
@@ -79,16 +81,16 @@ def test_fused_layer_layouts(dev, monkeypatch, z_planes, dz_planes, H):
     test_fused_layer_matches_oracle(dev, "mean", 1, True, True, True, H)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("aggr,red", [("sum", 0), ("mean", 1)])
 def test_fused_layer_gemm_modes(dev, mode, aggr, red):
-    """The layer matches the oracle with either GEMM family (f32 MFMA / bf16x6)."""
+    """The layer matches the oracle with every GEMM family (f32 MFMA / bf16x6 / f16x3)."""
     from bgnn import _lib
     _lib.call("bgnn_set_tuning", 5, mode)
     try:
         test_fused_layer_matches_oracle(dev, aggr, red, True, True, True, 512)
     finally:
-        _lib.call("bgnn_set_tuning", 5, 1)
+        _lib.call("bgnn_set_tuning", 5, 2)
 
 
 def test_dropout_mask_fraction_and_backward_consistency(dev):
@@ -103,8 +105,8 @@ def test_dropout_mask_fraction_and_backward_consistency(dev):
     xd = x.to(dev).requires_grad_(True)
     drop = 0.25
     cfg = fused.LayerConfig(0, True, True, 0.1, 1e-5, True, drop, 987654321)
-    out = fused.SageLayerFn.apply(xd, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"], d["rm"].detach().clone(),
-                                  d["rv"].detach().clone(), graph, cfg)
+    out, _ = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"],
+                                     d["rm"].detach().clone(), d["rv"].detach().clone(), graph, cfg)
     y0, _, _ = oracle_layer(x, b.edge_index, p, "sum", True, True, True)
     keep = out.detach().cpu() != 0
     nz = y0.detach().abs() > 1e-6

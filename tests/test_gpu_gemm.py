@@ -1,5 +1,5 @@
-"""GPU: bgnn_gemm_f32 (f32 MFMA) against an fp64 torch reference, all transposes,
-ragged shapes, split-K and beta accumulation."""
+"""GPU: bgnn_gemm_f32 (f32 MFMA, bf16x6, f16x3 kernel families) against an fp64 torch
+reference, all transposes, ragged shapes, split-K, beta accumulation, operand scaling."""
 import pytest
 import torch
 
@@ -8,12 +8,19 @@ from bgnn import _lib, fused
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1], ids=["f32", "x6"])
+DEFAULT_MODE = 2
+
+
+@pytest.fixture(params=[0, 1, 2], ids=["f32", "x6", "h3"])
 def mode(request):
-    """GEMM kernel family: 0 = f32 MFMA, 1 = bf16x6 (BGNN_TUNE_GEMM_MODE)."""
+    """GEMM kernel family: 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (BGNN_TUNE_GEMM_MODE)."""
     _lib.call("bgnn_set_tuning", 5, request.param)
     yield request.param
-    _lib.call("bgnn_set_tuning", 5, 0)
+    _lib.call("bgnn_set_tuning", 5, DEFAULT_MODE)
+
+
+def test_default_mode_is_f16x3():
+    assert _lib.query("bgnn_get_tuning", 5) == DEFAULT_MODE
 
 
 def ref(a, b, ta, tb):
@@ -90,25 +97,103 @@ def test_gemm_planes_layouts(dev, mode, blk, N):
     assert (w1.double().cpu() - rw).abs().max().item() <= 2e-6 * 16 * N + 1e-5
 
 
-@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-def test_gemm_error_class_per_element(dev, ta, tb):
-    """Per-element error bound max |c - c64| / (|A||B|) of both kernel families on a SAGE-like
-    shape: the bf16x6 split is in the f32 MFMA's error class (f32 unit roundoff 6e-8 times a
-    small factor), far below the 1e-4 parity tolerance."""
-    torch.manual_seed(5)
-    M, N, K = 3000, 512, 1024
-    a = torch.randn((K, M) if ta else (M, K), device=dev)
-    b = torch.randn((N, K) if tb else (K, N), device=dev) * 0.03
+def _err_class(a, b, ta, tb, modes):
     A = a.double().t() if ta else a.double()
     B = b.double().t() if tb else b.double()
     c64, mag = A @ B, A.abs() @ B.abs()
     errs = []
-    for m in (0, 1):
+    for m in modes:
         _lib.call("bgnn_set_tuning", 5, m)
         try:
             c = fused.gemm(a, b, ta, tb)
         finally:
-            _lib.call("bgnn_set_tuning", 5, 0)
-        errs.append(((c.double() - c64).abs() / mag).max().item())
-    assert errs[0] < 1e-6 and errs[1] < 1e-6, errs
+            _lib.call("bgnn_set_tuning", 5, DEFAULT_MODE)
+        errs.append(((c.double() - c64).abs() / mag.clamp_min(1e-300)).max().item())
+    return errs
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+def test_gemm_error_class_per_element(dev, ta, tb):
+    """Per-element error bound max |c - c64| / (|A||B|) of the three kernel families on a
+    SAGE-like shape: the bf16x6 and f16x3 splits are in the f32 MFMA's error class (f32 unit
+    roundoff 6e-8 times a small factor: the f32 accumulation dominates), far below the 1e-4
+    parity tolerance."""
+    torch.manual_seed(5)
+    M, N, K = 3000, 512, 1024
+    a = torch.randn((K, M) if ta else (M, K), device=dev)
+    b = torch.randn((N, K) if tb else (K, N), device=dev) * 0.03
+    errs = _err_class(a, b, ta, tb, (0, 1, 2))
+    assert max(errs) < 1e-6, errs
     assert errs[1] < 4 * errs[0] + 1e-7, errs
+    assert errs[2] < 4 * errs[0] + 1e-7, errs
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (True, False)])
+def test_gemm_f16x3_row_magnitudes_spread(dev, ta, tb):
+    """f16x3 scales per tensor: rows spanning six decades (and relu zeros) keep f32-class
+    per-element error relative to |A||B|."""
+    torch.manual_seed(6)
+    M, N, K = 2000, 256, 512
+    a = torch.randn(M, K, device=dev) * torch.pow(10.0, -6 * torch.rand(M, 1, device=dev))
+    a = a.clamp_min(0) if ta else a
+    a = a.t().contiguous() if ta else a
+    b = torch.randn((N, K) if tb else (K, N), device=dev)
+    errs = _err_class(a, b, ta, tb, (0, 2))
+    assert errs[1] < 2e-6, errs
+
+
+@pytest.mark.parametrize("scale", [1e-30, 1e-12, 1.0, 1e12, 1e30])
+def test_gemm_f16x3_extreme_magnitudes(dev, scale):
+    """Operand scales are powers of two chosen from max|A|, max|B|: tensors far outside the
+    f16 range (both ways) multiply at f32-class accuracy; zero operands give exact zeros."""
+    torch.manual_seed(7)
+    a = torch.randn(300, 200, device=dev) * scale
+    b = torch.randn(100, 200, device=dev) / scale ** 0.5
+    errs = _err_class(a, b, False, True, (2,))
+    assert errs[0] < 2e-6, errs
+    z = fused.gemm(torch.zeros(64, 32, device=dev), b[:, :32].contiguous(), False, True)
+    assert bool((z == 0).all())
+
+
+def test_absmax_and_supplied_maxima(dev):
+    """bgnn_absmax_f32 matches torch; bgnn_gemm_f32_scaled with supplied maxima equals the
+    self-scaled call bit for bit (maxima computed inside from the same data)."""
+    torch.manual_seed(8)
+    x = torch.randn(1000, 96, device=dev)
+    x[123, 45] = -77.5
+    out = torch.full((1,), 3.0, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("bgnn_absmax_f32", x.data_ptr(), 1000, 96, 96, out.data_ptr(), 0, s)
+    assert out.item() == 77.5
+    _lib.call("bgnn_absmax_f32", x[:, :50].data_ptr(), 1000, 50, 96, out.data_ptr(), 1, s)
+    assert out.item() == 77.5
+    w = torch.randn(64, 96, device=dev)
+    amax = torch.stack([x.abs().max(), w.abs().max()]).contiguous()
+    c1 = fused.gemm(x, w, False, True)
+    c2 = torch.empty_like(c1)
+    ws_bytes = _lib.query("bgnn_gemm_ws_bytes", 1000, 64, 96, 0, 1)
+    ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
+    _lib.call("bgnn_gemm_f32_scaled", 0, 1, 1000, 64, 96, 1.0, x.data_ptr(), 96, 0, 0, w.data_ptr(), 96, 0.0,
+              c2.data_ptr(), 64, 0, 0, None, 0, amax[0:].data_ptr(), amax[1:].data_ptr(), None, ws.data_ptr(),
+              ws.numel(), s)
+    torch.testing.assert_close(c1, c2, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("shape", [(1000, 64, 96, 0, 1), (1000, 37, 96, 0, 1), (512, 256, 9000, 1, 0)])
+def test_gemm_c_amax(dev, mode, shape):
+    """c_amax = max |C| of the result, fused into the epilogue (split kernels, no split-K) or one
+    extra pass (f32 kernel, split-K); folds into the running value; bias/ReLU applied first."""
+    M, N, K, ta, tb = shape
+    torch.manual_seed(9)
+    a = torch.randn((K, M) if ta else (M, K), device=dev)
+    b = torch.randn((N, K) if tb else (K, N), device=dev)
+    bias = torch.randn(N, device=dev)
+    c = torch.empty(M, N, device=dev)
+    cm = torch.full((1,), 0.5, device=dev)
+    ws_bytes = _lib.query("bgnn_gemm_ws_bytes", M, N, K, ta, tb)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("bgnn_gemm_f32_scaled", ta, tb, M, N, K, 1.0, a.data_ptr(), a.stride(0), 0, 0, b.data_ptr(), b.stride(0),
+              0.0, c.data_ptr(), N, 0, 0, bias.data_ptr(), 1, None, None, cm.data_ptr(), ws.data_ptr(), ws_bytes, s)
+    assert cm.item() == c.abs().max().item()
+    assert bool((c >= 0).all())

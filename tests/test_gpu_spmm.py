@@ -168,3 +168,26 @@ def test_kernel_variants_bit_identical(dev, knobs, graph):
     finally:
         _lib.call("bgnn_set_tuning", 1, old[0])
         _lib.call("bgnn_set_tuning", 3, old[1])
+
+
+@pytest.mark.parametrize("kernel", [0, 1], ids=["sweep", "blocked"])
+@pytest.mark.parametrize("reduce", [0, 1])
+def test_spmm_bwd_folds_max_abs(dev, kernel, reduce):
+    """bgnn_spmm_bwd's optional amax output is max |gx| over light rows and the super-node
+    (chunked + combined) rows alike, folded into the running value."""
+    from bgnn import _lib, ops
+    b = S.make_batch(25, 3, super_node=True)
+    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    assert g.bwd.plan.n_heavy > 0
+    torch.manual_seed(4)
+    gy = torch.randn(b.num_nodes, 512, device=dev)
+    gy[b.ptr[1:] - 1] *= 50.0   # make a heavy row hold the maximum in one case
+    old = _lib.query("bgnn_get_tuning", 1)
+    try:
+        _lib.call("bgnn_set_tuning", 1, kernel)
+        for scale in (1.0, 1e-3):
+            amax = torch.full((1,), 1e-9, device=dev)
+            gx = ops.spmm_bwd(g.bwd, g.perm_t, g.fwd.rowptr, gy * scale, reduce, None, b.num_nodes, amax=amax)
+            assert amax.item() == gx.abs().max().item()
+    finally:
+        _lib.call("bgnn_set_tuning", 1, old)

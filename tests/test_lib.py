@@ -69,8 +69,14 @@ def test_size_queries_need_no_gpu():
 
     assert _lib.query("bgnn_graph_build_ws_bytes", 1000, 100) > 0
     assert _lib.query("bgnn_sage_fwd_slots", 80656) == 1024
-    assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 0      # forward: no split-K
-    assert _lib.query("bgnn_gemm_ws_bytes", 1024, 512, 80656, 1, 0) > 0       # wgrad: split-K
+    # f16x3 (default): a 256-B head for the operand maxima, plus split-K slabs where used
+    assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 256    # forward: no split-K
+    assert _lib.query("bgnn_gemm_ws_bytes", 1024, 512, 80656, 1, 0) > 256     # wgrad: split-K
+    _lib.call("bgnn_set_tuning", 5, 1)
+    try:
+        assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 0  # bf16x6: no head
+    finally:
+        _lib.call("bgnn_set_tuning", 5, 2)
 
 
 def test_error_string_and_argument_validation():

@@ -2,7 +2,8 @@
 """A/B the GEMM kernels and tile configurations (and torch.mm) on the SAGE layer shapes,
 interleaved in one process; median per-launch HIP-event time, TFLOP/s, and the error
 against an fp64 product as max_ij |c - c64|_ij / (|A| |B|)_ij.
-Variants: "3" = f32 MFMA config 3, "x1" = bf16x6 config 1, "torch" = torch.mm."""
+Variants: "3" = f32 MFMA config 3, "x1" = bf16x6 config 1, "h1" = f16x3 config 1,
+"torch" = torch.mm; add 100*k to a config for timing ablation k (wrong results)."""
 import argparse
 import os
 import statistics
@@ -23,7 +24,7 @@ SHAPES = {  # name: (M, N, K, trans_a, trans_b)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="0,1,3,x0,x1,x2")
+    ap.add_argument("--cfgs", default="3,x1,h0,h1,h2,h3,h4")
     ap.add_argument("--rounds", type=int, default=10)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -49,8 +50,8 @@ def main():
                     fused.GEMM_BACKEND = "torch"
                 else:
                     fused.GEMM_BACKEND = "hip"
-                    _lib.call("bgnn_set_tuning", 5, 1 if v.startswith("x") else 0)
-                    _lib.call("bgnn_gemm_set_cfg", int(v.lstrip("x")))
+                    _lib.call("bgnn_set_tuning", 5, {"x": 1, "h": 2}.get(v[0], 0))
+                    _lib.call("bgnn_gemm_set_cfg", int(v.lstrip("xh")))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 c = fused.gemm(a, b, ta, tb)
@@ -68,7 +69,7 @@ def main():
                         if err > 1e-4:
                             print(f"MISMATCH cfg {v} {n}: rel {err:.2e}")
     _lib.call("bgnn_gemm_set_cfg", -1)
-    _lib.call("bgnn_set_tuning", 5, 0)
+    _lib.call("bgnn_set_tuning", 5, 2)
     for v in variants:
         line = f"cfg {str(v):6s}"
         for n, (a, b, ta, tb, fl) in ops.items():
