@@ -192,7 +192,7 @@ def main():
     gemm_flop = 2.0 * N * (2 * H) * H
     gmode = _lib.query("bgnn_get_tuning", 5) if args.gemm == "hip" else -1
     gemm_peak = {1: X6_PEAK_TFS, 2: H3_PEAK_TFS}.get(gmode, FP32_MFMA_PEAK_TFS)
-    gemm_kernel = {2: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<1,0,1,256,128,4,2> (f32-accurate f16x3)",
+    gemm_kernel = {2: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<1,0,1,256,256,4,2> (f32-accurate f16x3)",
                    1: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<0,0,1,256,128,4,2> (f32-accurate bf16x6)",
                    0: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_f32 (f32 MFMA)"}.get(gmode, "torch.mm")
     gemm_basis = {2: "f16 dense MFMA 2500 TF / 3 f16 products per f32 product",

@@ -198,13 +198,14 @@ class BuckGNN(nn.Module):
     def _fused_ok(self, x: Tensor) -> bool:
         return self.use_fused and x.is_cuda and self.hidden_channels % 4 == 0 and self.hidden_channels <= 512
 
-    def _sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, aggr: str, skip_last_excluded: bool):
+    def _sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, aggr: str, skip_last_excluded: bool,
+                   x_amax: Optional[Tensor] = None):
         L = len(convs) if convs is not None else self.num_layers
         p = self.dropout.p
         if self._fused_ok(x) and aggr in ("add", "sum", "mean"):
             graph = graph_for(edge_index, x.size(0))
             red = 1 if aggr == "mean" else 0
-            amax = None   # max|x| of the running features: each layer's apply kernel folds it in
+            amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
             for i in range(L):
                 conv = convs[i] if convs is not None else self.shared_graphsage_block
                 bn = bns[i] if bns is not None else None
@@ -230,8 +231,9 @@ class BuckGNN(nn.Module):
             is_real_node = x[:, -1] == 0 if x.size(1) > 0 else torch.ones(x.size(0), dtype=torch.bool,
                                                                            device=x.device)
             real_node_batch = batch[is_real_node] if batch is not None else None
+        x_amax = None   # max|x| after the encoder (f16x3 operand scale of the first SAGE GEMM)
         if self._fused_ok(x) and x.size(0) >= 1024 and FUSED_ENCODER:
-            x = mlp(self.node_encoder, x)        # encoder GEMMs with fused bias+ReLU epilogues
+            x, x_amax = mlp(self.node_encoder, x, return_amax=True)   # GEMMs with fused bias+ReLU epilogues
         else:
             x = self.node_encoder(x)
         if name == "EA_GNN_Shared":
@@ -243,7 +245,7 @@ class BuckGNN(nn.Module):
                     x, e = x + x_prev, e + e_prev
                 x, e = self.dropout(x), self.dropout(e)
         if name == "GraphSage_addAggr_Shared":
-            x = self._sage_loop(x, edge_index, None, None, "add", True)
+            x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax)
         elif name == "EA_GNN":
             e = self.edge_encoder(edge_attr)
             L = len(self.gn_blocks)
@@ -255,7 +257,7 @@ class BuckGNN(nn.Module):
                 x, e = self.dropout(x), self.dropout(e)
         elif name in _SAGE_VARIANTS:
             attr, aggr, _ = _SAGE_VARIANTS[name]
-            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True)
+            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax)
         elif name in ("GraphSage_addAggr_woBatchNorm", "GraphSage_MLP"):
             getattr(self, "sage_blocks_add")  # AttributeError, as in the reference (:405,473)
         elif name == "GraphSage_sumAggr_woBatchNorm":

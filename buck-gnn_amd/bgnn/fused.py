@@ -152,52 +152,67 @@ def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float
 
 
 class LinearFn(torch.autograd.Function):
-    """y = act(x W^T + b) on bgnn_gemm_f32_ex (bias + ReLU fused in the GEMM epilogue);
-    backward: dgrad and wgrad GEMMs on the same kernel (Models/BuckGNN.py:67-74 encoder)."""
+    """(y, max|y|) with y = act(x W^T + b) on the bgnn GEMM (bias + ReLU fused in the epilogue,
+    max|y| folded in there too: the next Linear's operand scale); backward: dgrad and wgrad
+    GEMMs on the same kernel, sharing one max|g| pass (Models/BuckGNN.py:67-74 encoder)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool):
+    def forward(ctx, x, weight, bias, relu: bool, x_amax):
         x = x.contiguous()
-        y = gemm(x, weight.contiguous(), trans_a=False, trans_b=True, bias=bias, relu=relu)
+        amax = torch.zeros(2, dtype=torch.float32, device=x.device)   # [max|W|, max|y|]
+        w_amax, y_amax = amax[0:1], amax[1:2]
+        absmax(weight, w_amax, accumulate=True)
+        if x_amax is None:
+            x_amax = absmax(x)
+        y = gemm(x, weight.contiguous(), trans_a=False, trans_b=True, bias=bias, relu=relu, a_amax=x_amax,
+                 b_amax=w_amax, c_amax=y_amax)
         ctx.relu = relu
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device))
-        return y
+        ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device), x_amax, w_amax)
+        ctx.mark_non_differentiable(y_amax)
+        return y, y_amax
 
     @staticmethod
-    def backward(ctx, g):
-        x, weight, y = ctx.saved_tensors
+    def backward(ctx, g, _g_amax):
+        x, weight, y, x_amax, w_amax = ctx.saved_tensors
         g = g.contiguous()
         if ctx.relu:
             g = g * (y > 0)
+        g_amax = absmax(g)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (gemm(g, weight.t().contiguous(), trans_a=False, trans_b=True) if DGRAD_WT
-                  else gemm(g, weight.contiguous(), trans_a=False, trans_b=False))
-        dw = gemm(g, x, trans_a=True, trans_b=False)
+            dx = (gemm(g, weight.t().contiguous(), trans_a=False, trans_b=True, a_amax=g_amax, b_amax=w_amax)
+                  if DGRAD_WT else
+                  gemm(g, weight.contiguous(), trans_a=False, trans_b=False, a_amax=g_amax, b_amax=w_amax))
+        dw = gemm(g, x, trans_a=True, trans_b=False, a_amax=g_amax, b_amax=x_amax)
         db = g.sum(0) if ctx.has_bias else None
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, relu: bool = False) -> torch.Tensor:
-    return LinearFn.apply(x, weight, bias, relu)
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, relu: bool = False,
+           x_amax: torch.Tensor = None, return_amax: bool = False):
+    y, y_amax = LinearFn.apply(x, weight, bias, relu, x_amax)
+    return (y, y_amax) if return_amax else y
 
 
-def mlp(seq: torch.nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+def mlp(seq: torch.nn.Sequential, x: torch.Tensor, return_amax: bool = False):
     """Run an nn.Sequential of Linear/ReLU through bgnn GEMMs, fusing each ReLU into the
-    preceding Linear's epilogue (same parameters, same result as seq(x))."""
+    preceding Linear's epilogue (same parameters, same result as seq(x)). With return_amax,
+    also returns max|output| (device scalar) when the last module is a Linear, else None."""
     mods = list(seq)
     i = 0
+    amax = None
     while i < len(mods):
         m = mods[i]
         if isinstance(m, torch.nn.Linear):
             fuse = i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.ReLU)
-            x = linear(x, m.weight, m.bias, fuse)
+            x, amax = linear(x, m.weight, m.bias, fuse, x_amax=amax, return_amax=True)
             i += 2 if fuse else 1
         else:
             x = m(x)
+            amax = None
             i += 1
-    return x
+    return (x, amax) if return_amax else x
 
 
 def _ptr(t):

@@ -79,8 +79,19 @@ static inline uint32_t dropout_threshold(float p) {
     return (uint32_t)t;
 }
 
-// GEMM kernel family (gemm.hip): 0 = f32 MFMA, 1 = bf16x6 (f32-accurate split products)
+// GEMM kernel family (gemm.hip): 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (f32-accurate split products)
 void set_gemm_mode(int mode);
 int gemm_mode();
+// non-temporal output stores of the row-wise SAGE kernels (sage.hip)
+void set_rows_nt(int on);
+int rows_nt();
+
+// 16-byte store, non-temporal (streamed once: no write-allocate in L2 / Infinity Cache)
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d, bool nt) {
+    typedef float f32x4_t __attribute__((ext_vector_type(4)));
+    const f32x4_t t = {a, b, c, d};
+    if (nt) __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(p));
+    else *reinterpret_cast<f32x4_t*>(p) = t;
+}
 
 }  // namespace bgnn

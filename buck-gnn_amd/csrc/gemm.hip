@@ -258,8 +258,16 @@ void set_gemm_mode(int mode) { g_gemm_mode = mode; }
 int gemm_mode() { return g_gemm_mode; }
 
 // bf16x6 / f16x3 tile choice (tools/tune_gemm.py)
+// f16x3 (MI355X, tools/gemm_one.py under rocprofv3, cfg2 SAGE shapes): fwd 80656x1024x512
+// 256x256 tiles 293 us (256x128: 341); dgrad 80656x512x1024 128x256 311 us (256x128: 329,
+// 256x256: 323, under-filled last wave); wgrad 1024x512x80656 256x256 + split-K 302 us
+// (256x128: 604 -- half the operand re-reads).
 inline int pick_x6_cfg(int64_t M, int64_t N, int64_t K, int prec) {
-    (void)prec;
+    if (prec == 1) {
+        if (M >= 4096 && N >= 1024) return 4;
+        if (M >= 4096 && N >= 256) return 2;
+        if (M >= 256 && N >= 256 && K >= 8192) return 4;
+    }
     if (M >= 4096 && N >= 128) return 1;              // tall (fwd / dgrad)
     if (M >= 256 && N >= 128 && K >= 8192) return 1;  // short and deep (wgrad, split-K)
     return 0;
@@ -312,7 +320,7 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 using namespace bgnn;
 
 extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
-    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 600,
+    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 800,
                  "gemm: config %d out of range", cfg);
     g_gemm_abl = cfg / 100;
     g_gemm_cfg = cfg % 100;

@@ -31,6 +31,8 @@
 // registers and stored as three bf16 row images [R][32] per operand (K contiguous, 64-B
 // rows, 16-B chunks XOR-swizzled by (row >> 2) & 3 so a 16-lane ds_read_b128 group hits 16
 // distinct bank quads). Each MFMA operand is one ds_read_b128 per piece per lane.
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_common.h"
 
@@ -168,6 +170,45 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
     }
 }
 
+// k-major quad staging (f16x3, both operands k-major: the weight gradient dW = dZ^T X, whose
+// K is the node dimension). A quad is 4 consecutive rows r x 8 consecutive k of one operand:
+// eight coalesced float4 loads along r (one per k), transposed in registers into four
+// 8-k units, written as the same [row][32 k] swizzled images as the K-contiguous path (so
+// the MFMA reads are unchanged). Quads of A go to threads [0, BM), of B to [BM, BM + BN).
+// Measured (wgrad 1024x512x80656, 256x256 tiles): 804 -> 300 us against per-lane dword loads.
+template <int R, bool FULL>
+__device__ __forceinline__ void kq_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
+                                        int64_t kend, bool vec_ok, float (&v)[4][8], int q) {
+    const int r4 = q % (R / 4), c = q / (R / 4);
+    const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
+            const float4 f = *reinterpret_cast<const float4*>(P + (gk + k) * ld + gr);
+            v[0][k] = f.x; v[1][k] = f.y; v[2][k] = f.z; v[3][k] = f.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i][k] = (gr + i < Rlim && gk + k < kend) ? P[(gk + k) * ld + gr + i] : 0.f;
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void kq_store(uint4* __restrict__ S, const float (&v)[4][8], int q, float sc) {
+    const int r4 = q % (R / 4), c = q / (R / 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint4 q0, q1;
+        split2h(v[i][0] * sc, v[i][1] * sc, q0.x, q1.x);
+        split2h(v[i][2] * sc, v[i][3] * sc, q0.y, q1.y);
+        split2h(v[i][4] * sc, v[i][5] * sc, q0.z, q1.z);
+        split2h(v[i][6] * sc, v[i][7] * sc, q0.w, q1.w);
+        const int pos = x6_pos(4 * r4 + i, c);
+        S[pos] = q0;
+        S[R * 4 + pos] = q1;
+    }
+}
+
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 q) { return __builtin_bit_cast(bf16x8, q); }
 __device__ __forceinline__ f16x8 as_f16x8(uint4 q) { return __builtin_bit_cast(f16x8, q); }
 
@@ -200,6 +241,14 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
             t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], t, 0, 0, 0);
             acc[i][j] = t;
         }
+}
+
+// C leaves with non-temporal stores: it is streamed once, and write-allocating it in L2 / the
+// Infinity Cache costs ~40 % of the kernel (fwd 360 -> 220 us, measured on MI355X).
+__device__ __forceinline__ void st_nt4(float* p, const float (&e)[4]) {
+    typedef float f32x4_t __attribute__((ext_vector_type(4)));
+    const f32x4_t t = {e[0], e[1], e[2], e[3]};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(p));
 }
 
 // Epilogue: each wave writes its TM x TN accumulator tiles one 32-column block at a time
@@ -255,7 +304,11 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                     cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
                 }
                 if (ABL == 5 && e[0] != 1234.5f) continue;   // ablation: no C stores
-                *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
+                if constexpr (ABL == 6) {   // ablation: cached (write-allocate) C stores
+                    *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
+                } else {
+                    st_nt4(p, e);
+                }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             continue;
@@ -302,7 +355,7 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                 }
             }
             if (full) {
-                *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
+                st_nt4(p, e);
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -319,7 +372,8 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
 
 // ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored in
 // every piece slot), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA +
-// barriers), 4 = MFMA + barriers only, 5 = everything but the C stores.
+// barriers), 4 = MFMA + barriers only, 5 = everything but the C stores, 6 = cached C stores,
+// 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands.
 template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int NT = 64 * WM * WN;
@@ -370,62 +424,101 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float ra[BM * 4 / NT][8], rb[BN * 4 / NT][8];
+    constexpr bool KQ = !AK && !BKc && PREC == 1 && ABL != 7 && BM + BN <= NT && BM % 64 == 0 && BN % 64 == 0 &&
+                        BM * BN >= 256 * 128;   // (128x128: measured slower than the dword path)
+    // two register sets for the staged slices: slice kt+1 is split into LDS while slices kt+2
+    // and kt+3 are in flight (prefetch distance 2; ABL 7 = distance 1 for measurement). The
+    // second set fits the VGPR budget only for K-contiguous operands and tiles up to 256x128
+    // (measured: fwd 363 -> 334 us, dgrad 384 -> 322 us at 256x128).
+    constexpr int PF = (ABL == 7 || BM * BN > 256 * 128 || (!(AK && BKc) && !KQ)) ? 1 : 2;
+    // k-major quad staging for the weight gradient (both operands k-major, f16x3)
+    struct RegsStd { float a[BM * 4 / NT][8]; float b[BN * 4 / NT][8]; };
+    struct RegsKQ { float q[4][8]; };
+    using Regs = std::conditional_t<KQ, RegsKQ, RegsStd>;
+    Regs rs[2];
     const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
-    auto load_ab = [&](int64_t k0) {
-        const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
-        if (full) {
-            x6_load<AK, BM, NT, true>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra, t);
-            x6_load<BKc, BN, NT, true>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb, t);
-        } else {
-            x6_load<AK, BM, NT, false>(Ab, g.lda, g.M, m0, k0, ke, a_vec, ra, t);
-            x6_load<BKc, BN, NT, false>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, rb, t);
-        }
-    };
-    auto store_ab = [&](int buf) {
-        x6_store<AK, BM, NT, PREC, ABL>(As[buf], ra, t, sa);
-        x6_store<BKc, BN, NT, PREC, ABL>(Bs[buf], rb, t, sb);
-    };
-    // Pipeline: slice t+1 is split and written to the free LDS buffer, slice t+2 is loaded
-    // into registers, then slice t is multiplied; one barrier per slice.
-    if (nk > 0) {
-        load_ab(kb);
-        store_ab(0);
-        if (nk > 1 && ABL != 2) load_ab(kb + X6_BK);
-    }
-    __syncthreads();
-
-    const int li = lane & 31, lh = lane >> 5;
-    for (int64_t kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk && ABL < 3) store_ab(cur ^ 1);
-        if (kt + 2 < nk && ABL != 2 && ABL < 3) load_ab(kb + (kt + 2) * X6_BK);
-#pragma unroll
-        for (int kk = 0; kk < X6_BK / 16; ++kk) {
-            uint4 a[TM][NP], b[TN][NP];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int row = wm * (BM / WM) + i * 32;
-#pragma unroll
-                for (int p = 0; p < NP; ++p) {
-                    if constexpr (ABL == 4) a[i][p] = make_uint4(row + p, kk, i, (int)kt);
-                    else a[i][p] = As[cur][p * BM * 4 + x6_pos(row + li, 2 * kk + lh)];
-                }
+    constexpr bool kStage = ABL != 3 && ABL != 4, kLoad = kStage && ABL != 2;
+    // the main loop is instantiated twice (interior tiles without guards, edge tiles with
+    // them) and selected once, so the hot loop carries no per-slice bounds branches
+    auto mainloop = [&](auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+        auto load_ab = [&](int64_t k0, Regs& r) {
+            const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
+            if constexpr (KQ) {
+                if (t < BM) kq_load<BM, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
+                else if (t < BM + BN) kq_load<BN, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+            } else {
+                x6_load<AK, BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
+                x6_load<BKc, BN, NT, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
             }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int row = wn * (BN / WN) + j * 32;
-#pragma unroll
-                for (int p = 0; p < NP; ++p) {
-                    if constexpr (ABL == 4) b[j][p] = make_uint4(row - p, kk, j, (int)kt);
-                    else b[j][p] = Bs[cur][p * BN * 4 + x6_pos(row + li, 2 * kk + lh)];
-                }
+        };
+        auto store_ab = [&](int buf, const Regs& r) {
+            if constexpr (KQ) {
+                if (t < BM) kq_store<BM>(As[buf], r.q, t, sa);
+                else if (t < BM + BN) kq_store<BN>(Bs[buf], r.q, t - BM, sb);
+            } else {
+                x6_store<AK, BM, NT, PREC, ABL>(As[buf], r.a, t, sa);
+                x6_store<BKc, BN, NT, PREC, ABL>(Bs[buf], r.b, t, sb);
             }
-            x6_mma<TM, TN, PREC, NP>(acc, a, b);
+        };
+        const int li = lane & 31, lh = lane >> 5;
+        auto mma_slice = [&](int cur, int64_t kt) {
+#pragma unroll
+            for (int kk = 0; kk < X6_BK / 16; ++kk) {
+                uint4 a[TM][NP], b[TN][NP];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm * (BM / WM) + i * 32;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        if constexpr (ABL == 4) a[i][p] = make_uint4(row + p, kk, i, (int)kt);
+                        else a[i][p] = As[cur][p * BM * 4 + x6_pos(row + li, 2 * kk + lh)];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn * (BN / WN) + j * 32;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        if constexpr (ABL == 4) b[j][p] = make_uint4(row - p, kk, j, (int)kt);
+                        else b[j][p] = Bs[cur][p * BN * 4 + x6_pos(row + li, 2 * kk + lh)];
+                    }
+                }
+                x6_mma<TM, TN, PREC, NP>(acc, a, b);
+            }
+        };
+        // one pipeline step: split slice kt+1 (register set S) into LDS buffer (kt+1)&1, refill
+        // set S with slice kt+1+PF, multiply slice kt, barrier. S = (kt+1) & 1 for PF = 2.
+        auto step = [&](int64_t kt, Regs& r) {
+            const int cur = (int)(kt & 1);
+            if (kt + 1 < nk && kStage) store_ab(cur ^ 1, r);
+            if (kt + 1 + PF < nk && kLoad) load_ab(kb + (kt + 1 + PF) * X6_BK, r);
+            // keep the staging (split VALU, LDS writes, global loads) out of the MFMA block
+            __builtin_amdgcn_sched_barrier(0);
+            mma_slice(cur, kt);
+            __syncthreads();
+        };
+        if (nk > 0) {
+            load_ab(kb, rs[0]);
+            store_ab(0, rs[0]);
+            if (nk > 1 && kLoad) load_ab(kb + X6_BK, rs[1]);
+            if (PF == 2 && nk > 2 && kLoad) load_ab(kb + 2 * X6_BK, rs[0]);
         }
         __syncthreads();
-    }
+        if constexpr (PF == 2) {
+            int64_t kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                step(kt, rs[1]);
+                step(kt + 1, rs[0]);
+            }
+            if (kt < nk) step(kt, rs[1]);
+        } else {
+            for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
+        }
+    };
+    if (full) mainloop(std::true_type{});
+    else mainloop(std::false_type{});
     // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
     x6_epilogue<TM, TN, ABL>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
@@ -464,8 +557,13 @@ static void launch_x6_t(int cfg, int abl, dim3 grid, hipStream_t s, const GemmAr
             case 2: launch_x6_a<PREC, TA, TB, 2>(cfg, grid, s, g); break;
             case 3: launch_x6_a<PREC, TA, TB, 3>(cfg, grid, s, g); break;
             case 4: launch_x6_a<PREC, TA, TB, 4>(cfg, grid, s, g); break;
-            default: launch_x6_a<PREC, TA, TB, 5>(cfg, grid, s, g); break;
+            case 5: launch_x6_a<PREC, TA, TB, 5>(cfg, grid, s, g); break;
+            case 6: launch_x6_a<PREC, TA, TB, 6>(cfg, grid, s, g); break;
+            default: launch_x6_a<PREC, TA, TB, 7>(cfg, grid, s, g); break;
         }
+    } else if constexpr (TA == 1 && TB == 0) {   // wgrad: ablation 7 (dword k-major staging) only
+        if (abl == 7) launch_x6_a<PREC, TA, TB, 7>(cfg, grid, s, g);
+        else launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);
     } else {
         launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);
     }

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o
                                                     const float* __restrict__ shift,
                                                     const float4* __restrict__ xprev, int skip, uint32_t thr,
                                                     float inv_keep, uint64_t seed, int64_t n4, int H4,
-                                                    float4* __restrict__ xn, uint32_t* __restrict__ amax) {
+                                                    float4* __restrict__ xn, uint32_t* __restrict__ amax, int nt) {
     uint32_t m = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         const int c = (int)(i % H4) * 4;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o
 #pragma unroll
             for (int k = 0; k < 4; ++k) y[k] = ((keep >> k) & 1u) ? y[k] * inv_keep : 0.f;
         }
-        xn[i] = make_float4(y[0], y[1], y[2], y[3]);
+        store4(reinterpret_cast<float*>(xn + i), y[0], y[1], y[2], y[3], nt);
 #pragma unroll
         for (int k = 0; k < 4; ++k) m = max(m, __float_as_uint(y[k]) & 0x7fffffffu);
     }
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sum_g2,
     const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
     int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
-    float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax) {
+    float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax, int nt) {
     const int lane = threadIdx.x & 63;
     uint32_t tmax = 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -341,10 +341,9 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
                 db[v][k] += out[k];
                 tmax = max(tmax, __float_as_uint(out[k]) & 0x7fffffffu);
             }
-            *reinterpret_cast<float4*>(dh + r * lddh + cpos[v]) = make_float4(out[0], out[1], out[2], out[3]);
+            store4(dh + r * lddh + cpos[v], out[0], out[1], out[2], out[3], nt);
             if (skip)
-                *reinterpret_cast<float4*>(gskip + r * H + cpos[v]) =
-                    make_float4(g1v[v][0], g1v[v][1], g1v[v][2], g1v[v][3]);
+                store4(gskip + r * H + cpos[v], g1v[v][0], g1v[v][1], g1v[v][2], g1v[v][3], nt);
         }
     }
     if (amax) block_amax(amax, tmax);
@@ -363,6 +362,10 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static int g_rows_nt = 0;
+void set_rows_nt(int on) { g_rows_nt = on ? 1 : 0; }
+int rows_nt() { return g_rows_nt; }
 
 }  // namespace bgnn
 
@@ -423,7 +426,7 @@ extern "C" int bgnn_sage_apply(const float* o, const float* scale, const float* 
     const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
     hipLaunchKernelGGL(k_sage_apply, dim3((unsigned)blocks), dim3(256), 0, s, (const float4*)o, scale, shift,
                        (const float4*)x_prev, skip, thr, inv_keep, seed, n4, H / 4, (float4*)x_next,
-                       reinterpret_cast<uint32_t*>(amax));
+                       reinterpret_cast<uint32_t*>(amax), rows_nt());
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
@@ -470,11 +473,11 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
     if (H > 256)
         hipLaunchKernelGGL(k_sage_bwd_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax));
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt());
     else
         hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax));
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt());
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

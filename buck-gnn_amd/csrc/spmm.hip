@@ -855,6 +855,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_SEG_U: return g_seg_u;
         case BGNN_TUNE_SEG_NT: return g_seg_nt;
         case BGNN_TUNE_GEMM_MODE: return gemm_mode();
+        case BGNN_TUNE_ROWS_NT: return rows_nt();
         default: return -1;
     }
 }
@@ -875,6 +876,7 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             g_seg_u = value;
             return BGNN_OK;
         case BGNN_TUNE_SEG_NT: g_seg_nt = value ? 1 : 0; return BGNN_OK;
+        case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: gemm mode must be 0 (f32), 1 (bf16x6) or 2 (f16x3)");
             set_gemm_mode(value);

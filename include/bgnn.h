@@ -65,6 +65,7 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (12), 8, 12, 16  */
 #define BGNN_TUNE_SEG_NT 4       /* non-temporal hints on stream-once rows (default 1)       */
 #define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (default) */
+#define BGNN_TUNE_ROWS_NT 6      /* non-temporal stores in sage_apply / sage_bwd_rows (0/1)   */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);

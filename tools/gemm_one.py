@@ -2,7 +2,9 @@
 """Run one GEMM (SAGE layer shape) repeatedly with a fixed kernel family / tile config, for
 rocprofv3 counter passes. Usage: tools/gemm_one.py MODE CFG SHAPE [REPS]
 MODE 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3; CFG as bgnn_gemm_set_cfg (100*k = ablation k);
-SHAPE in fwd, dgrad, wgrad."""
+SHAPE in fwd, dgrad, wgrad. Env GEMM_FLUSH=1 overwrites a 1 GiB buffer between launches
+(cold L2 / Infinity Cache, as inside a training step); GEMM_RELU=1 makes A non-negative with
+~half zeros (post-ReLU activations)."""
 import os
 import sys
 
@@ -26,11 +28,16 @@ def main():
     b = torch.randn((N, K) if tb else (K, N), device=dev)
     _lib.call("bgnn_set_tuning", 5, mode)
     _lib.call("bgnn_gemm_set_cfg", cfg)
+    if os.environ.get("GEMM_RELU") == "1":
+        a.clamp_(min=0)
     out = torch.empty(M, N, device=dev)
+    flush = torch.empty(1 << 28, device=dev) if os.environ.get("GEMM_FLUSH") == "1" else None
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for i in range(reps + 3):
         if i == 3:
             e0.record()
+        if flush is not None:
+            flush.fill_(float(i))
         fused.gemm(a, b, ta, tb, out=out)
     e1.record()
     torch.cuda.synchronize()
