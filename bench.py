@@ -6,10 +6,13 @@ Metric (BASELINE.json): graphs/sec of a full train step (fwd + bwd + Adam) of th
 per GPU (configs[1] = cfg2: 16 non-stiffened 71x71 quad+diagonal meshes with 13.33 %
 random virtual edges; N = 80,656 nodes, E = 715,872 directed edges per GPU).
 
-One step = the reference's inner-loop body (TRAIN_FINAL.py:253-298): graph structure
-built from edge_index (CSR + plans; rebuilt every step, as a new batch would need),
-forward, RelativeErrorLoss on denormalised eigenvalues, backward, gradient all-reduce
-(N > 1), Adam. Inputs (x, edge_index, batch, y) are resident in HBM before timing.
+One step = the reference's inner-loop body (TRAIN_FINAL.py:253-298): the next shuffled
+16-graph mini-batch gathered on the GPU from a device-resident GraphStore of 256 meshes per
+rank (features, edge_index, per-graph CSR; the reference collates it on the host with the
+PyG DataLoader, TRAIN_FINAL.py:1298), forward, RelativeErrorLoss on denormalised
+eigenvalues, backward, gradient all-reduce (N > 1), Adam. The dataset is resident in HBM
+before timing. --data static rebuilds the CSR of one fixed batch from edge_index every step
+instead; --data host collates on the host (PCIe-inclusive).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
@@ -57,11 +60,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
-    ap.add_argument("--data", default="static", choices=["static", "store", "host"],
-                    help="static: one resident 16-graph batch, graph structure rebuilt every step (default); "
-                         "store: a new shuffled 16-graph batch every step, gathered on the GPU from a resident "
-                         "GraphStore of --store-graphs meshes; host: the same batches collated on the host "
-                         "(PyG DataLoader path of the reference) and copied to the GPU inside the step")
+    ap.add_argument("--data", default="store", choices=["static", "store", "host"],
+                    help="store (default): a new shuffled 16-graph batch every step, gathered on the GPU from a "
+                         "resident GraphStore of --store-graphs meshes (the training loop's data path); "
+                         "static: one resident 16-graph batch, graph structure rebuilt from edge_index every "
+                         "step; host: the same batches as store collated on the host (PyG DataLoader path of "
+                         "the reference) and copied to the GPU inside the step")
     ap.add_argument("--store-graphs", type=int, default=256)
     return ap.parse_args()
 
