@@ -10,3 +10,9 @@ timeout -k 10 240 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/ben
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_$TAG" -o run -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$ROOT/gpurun_out/prof_bench_$TAG.json" 2>&1
+# PMC traffic of the bench's roofline kernels (separate counter-only passes)
+if [ "${PMC:-1}" = "1" ]; then
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$ROOT/gpurun_out/pmc_$TAG/fetch" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline > /dev/null 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$ROOT/gpurun_out/pmc_$TAG/write" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline > /dev/null 2>&1
+  cd "$ROOT" && python tools/traffic.py "gpurun_out/pmc_$TAG" "gpurun_out/traffic_$TAG.json" > /dev/null
+fi

@@ -22,7 +22,7 @@ from collections import defaultdict
 
 # bench roofline kernels: key -> kernel-name substring
 KERNELS = {
-    "gemm_fwd": "k_gemm_x6<0, 1, 256, 128",
+    "gemm_fwd_h3": "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>",   # f16x3 forward GEMM (256x256 tiles)
     "sage_fwd": "k_seg_sweep<2, 0, 1,",
 }
 
