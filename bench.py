@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3"])
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg5"])
     ap.add_argument("--model", default="GraphSage_addAggr")
     ap.add_argument("--gemm", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -67,6 +67,8 @@ def parse():
                          "step; host: the same batches as store collated on the host (PyG DataLoader path of "
                          "the reference) and copied to the GPU inside the step")
     ap.add_argument("--store-graphs", type=int, default=256)
+    ap.add_argument("--bf16", action="store_true",
+                    help="EA_GNN only: bf16 GEMM operands with f32 accumulation (BASELINE configs[4])")
     return ap.parse_args()
 
 
@@ -109,7 +111,8 @@ def main():
     dev = torch.device("cuda", local)
     fused.GEMM_BACKEND = args.gemm
 
-    # data: each rank owns its own 16 graphs (seeds 1000*rank + g); resident in HBM
+    # data: each rank owns its own bsz graphs (seeds 1000*rank + g); resident in HBM
+    bsz = synthetic.CONFIGS[args.config]["graphs"]
     batch_cpu = synthetic.make_config_batch(args.config, rank=rank)
     batch = batch_cpu.to(dev)
     torch.manual_seed(0)
@@ -118,6 +121,7 @@ def main():
                          model_name=args.model)
     state0 = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
+    model.ea_bf16 = bool(args.bf16)
     try:
         opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8, fused=True)
     except (RuntimeError, TypeError):
@@ -142,10 +146,10 @@ def main():
 
         def next_ids():
             nonlocal order
-            ids = list(itertools.islice(order, 16))
-            if len(ids) < 16:
+            ids = list(itertools.islice(order, bsz))
+            if len(ids) < bsz:
                 order = iter(rng.permutation(args.store_graphs))
-                ids = list(itertools.islice(order, 16))
+                ids = list(itertools.islice(order, bsz))
             return ids
 
         def step():
@@ -184,7 +188,7 @@ def main():
     N, E, H = batch.num_nodes, batch.num_edges, 512
     agg_ms = avg_ms("sage_fwd")
     agg_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
-    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9   # NaN when the model has no SAGE layer (EA_GNN)
     traffic = {}
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     if os.path.exists(tpath):
@@ -202,7 +206,7 @@ def main():
     gemm_basis = {2: "f16 dense MFMA 2500 TF / 3 f16 products per f32 product",
                   1: "bf16 dense MFMA 2500 TF / 6 bf16 products per f32 product"}.get(gmode, "f32 dense MFMA")
     gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
-    graphs = 16 * world * args.steps
+    graphs = bsz * world * args.steps
     out = {
         "metric": METRIC,
         "value": round(graphs / elapsed, 3),
@@ -214,19 +218,20 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if (args.bf16 and args.model.startswith("EA_GNN")) else "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.config}: 16 synthetic 71x71 quad+diagonal FE meshes per GPU"
+            "workload": f"{args.config}: {bsz} synthetic 71x71 quad+diagonal FE meshes per GPU"
                         + (" + super node" if args.config == "cfg3" else " + 13.33% random virtual edges")
-                        + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam; "
+                        + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam"
+                        + (", bf16 GEMM operands" if args.bf16 and args.model.startswith("EA_GNN") else "") + "; "
                         + {"static": "CSR rebuilt every step" if not args.cache_graph else "CSR cached across steps",
                            "store": f"new shuffled batch every step gathered on the GPU from a resident "
                                     f"GraphStore of {args.store_graphs} meshes",
                            "host": f"new shuffled batch every step collated on the host from {args.store_graphs} "
                                    f"meshes and copied to the GPU (reference DataLoader path)"}[args.data],
             "data_path": args.data,
-            "global_batch": 16 * world,
+            "global_batch": bsz * world,
             "nodes_per_gpu": N,
             "edges_per_gpu": E,
             "hidden": H,
@@ -266,7 +271,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(batch_cpu, state0, args.model, args.cpu_steps)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        def clean(o):   # NaN (a kernel the chosen model never launches) -> null: strict JSON
+            if isinstance(o, dict):
+                return {k: clean(v) for k, v in o.items()}
+            return None if isinstance(o, float) and o != o else o
+        print(json.dumps(clean(out)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

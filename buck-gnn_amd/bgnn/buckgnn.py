@@ -20,6 +20,7 @@ from typing import Optional
 import torch
 from torch import Tensor, nn
 
+from .ea import graphnet_block
 from .fused import mlp, sage_layer
 from .graph import Graph, SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
@@ -157,6 +158,9 @@ class BuckGNN(nn.Module):
             self.pool = SAGPooling(h, ratio=0.5)  # raises: out of scope
         # fused-path switch (tests compare both paths)
         self.use_fused = True
+        # EA_GNN GEMM precision on the fused path: False = f32-accurate (f16x3), True = bf16
+        # operands with f32 accumulation (BASELINE configs[4])
+        self.ea_bf16 = False
         self._step = 0
 
     # ------------------------------------------------------------------ pooling
@@ -236,22 +240,34 @@ class BuckGNN(nn.Module):
             x, x_amax = mlp(self.node_encoder, x, return_amax=True)   # GEMMs with fused bias+ReLU epilogues
         else:
             x = self.node_encoder(x)
+        ea_fused = name in ("EA_GNN", "EA_GNN_Shared") and self._fused_ok(x)
+        if ea_fused:
+            e = (mlp(self.edge_encoder, edge_attr) if edge_attr.size(0) >= 1024 and FUSED_ENCODER
+                 else self.edge_encoder(edge_attr))
         if name == "EA_GNN_Shared":
-            e = self.edge_encoder(edge_attr)
+            if not ea_fused:
+                e = self.edge_encoder(edge_attr)
             for i in range(self.num_layers):
                 x_prev, e_prev = x, e
-                x, e = self.shared_gn_block(x, edge_index, e)
+                if ea_fused:
+                    x, e = graphnet_block(self.shared_gn_block, x, e, edge_index, self.ea_bf16)
+                else:
+                    x, e = self.shared_gn_block(x, edge_index, e)
                 if 0 < i < self.num_layers - 1:
                     x, e = x + x_prev, e + e_prev
                 x, e = self.dropout(x), self.dropout(e)
         if name == "GraphSage_addAggr_Shared":
             x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax)
         elif name == "EA_GNN":
-            e = self.edge_encoder(edge_attr)
+            if not ea_fused:
+                e = self.edge_encoder(edge_attr)
             L = len(self.gn_blocks)
             for i, blk in enumerate(self.gn_blocks):
                 x_prev, e_prev = x, e
-                x, e = blk(x, edge_index, e)
+                if ea_fused:   # transform-first GraphNetBlock on bgnn GEMMs (bgnn/ea.py)
+                    x, e = graphnet_block(blk, x, e, edge_index, self.ea_bf16)
+                else:
+                    x, e = blk(x, edge_index, e)
                 if 0 < i < L - 1:
                     x, e = x + x_prev, e + e_prev
                 x, e = self.dropout(x), self.dropout(e)

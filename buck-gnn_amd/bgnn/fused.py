@@ -106,11 +106,12 @@ def absmax(x: torch.Tensor, out: torch.Tensor = None, accumulate: bool = False) 
 
 def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float = 0.0, alpha: float = 1.0,
          bias: torch.Tensor = None, relu: bool = False, a_amax: torch.Tensor = None,
-         b_amax: torch.Tensor = None, c_amax: torch.Tensor = None):
+         b_amax: torch.Tensor = None, c_amax: torch.Tensor = None, bf16: bool = False):
     """C = act(alpha * op(a) @ op(b) + beta * C + bias) (fp32, row-major operands, unit column
     stride). `a` and `out` may be Planes. a_amax / b_amax: optional device scalars holding
     max|a| / max|b| (the f16x3 operand scales; computed inside when absent); c_amax: optional
-    device scalar that max |C| is folded into (bgnn_gemm_f32_scaled)."""
+    device scalar that max |C| is folded into (bgnn_gemm_f32_scaled). bf16: round both operands
+    to bf16 (one MFMA product, f32 accumulation and output) instead of the f32-accurate split."""
     M = a.size(1) if trans_a else a.size(0)
     K = a.size(0) if trans_a else a.size(1)
     N = b.size(0) if trans_b else b.size(1)
@@ -143,11 +144,13 @@ def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float
     pa, lda, a_blk, a_ps = _operand(a)
     pb, ldb, _, _ = _operand(b)
     pc, ldc, c_blk, c_ps = _operand(out)
-    ws_bytes = _lib.query("bgnn_gemm_ws_bytes", M, N, K, int(trans_a), int(trans_b))
+    prec = 1 if bf16 else 0
+    ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, int(trans_a), int(trans_b), prec)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=b.device) if ws_bytes else None
     _lib.call("bgnn_gemm_f32_scaled", int(trans_a), int(trans_b), M, N, K, float(alpha), pa, lda, a_blk, a_ps,
               pb, ldb, float(beta), pc, ldc, c_blk, c_ps, None if bias is None else bias.data_ptr(), int(relu),
-              _ptr(a_amax), _ptr(b_amax), _ptr(c_amax), None if ws is None else ws.data_ptr(), ws_bytes, _stream())
+              _ptr(a_amax), _ptr(b_amax), _ptr(c_amax), prec, None if ws is None else ws.data_ptr(), ws_bytes,
+              _stream())
     return out
 
 
@@ -157,18 +160,22 @@ class LinearFn(torch.autograd.Function):
     GEMMs on the same kernel, sharing one max|g| pass (Models/BuckGNN.py:67-74 encoder)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool, x_amax):
+    def forward(ctx, x, weight, bias, relu: bool, x_amax, bf16: bool = False):
         x = x.contiguous()
         amax = torch.zeros(2, dtype=torch.float32, device=x.device)   # [max|W|, max|y|]
         w_amax, y_amax = amax[0:1], amax[1:2]
-        absmax(weight, w_amax, accumulate=True)
-        if x_amax is None:
-            x_amax = absmax(x)
-        y = gemm(x, weight.contiguous(), trans_a=False, trans_b=True, bias=bias, relu=relu, a_amax=x_amax,
-                 b_amax=w_amax, c_amax=y_amax)
+        if not bf16:   # (bf16 operands need no scales)
+            absmax(weight, w_amax, accumulate=True)
+            if x_amax is None:
+                x_amax = absmax(x)
+        y = gemm(x, weight.contiguous(), trans_a=False, trans_b=True, bias=bias, relu=relu,
+                 a_amax=None if bf16 else x_amax, b_amax=None if bf16 else w_amax,
+                 c_amax=None if bf16 else y_amax, bf16=bf16)
         ctx.relu = relu
+        ctx.bf16 = bf16
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device), x_amax, w_amax)
+        ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device),
+                              x_amax if x_amax is not None else torch.empty(0, device=x.device), w_amax)
         ctx.mark_non_differentiable(y_amax)
         return y, y_amax
 
@@ -178,24 +185,30 @@ class LinearFn(torch.autograd.Function):
         g = g.contiguous()
         if ctx.relu:
             g = g * (y > 0)
-        g_amax = absmax(g)
+        bf16 = ctx.bf16
+        g_amax = None if bf16 else absmax(g)
+        w_amax = None if bf16 else w_amax
+        x_amax = None if bf16 else x_amax
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (gemm(g, weight.t().contiguous(), trans_a=False, trans_b=True, a_amax=g_amax, b_amax=w_amax)
+            dx = (gemm(g, weight.t().contiguous(), trans_a=False, trans_b=True, a_amax=g_amax, b_amax=w_amax,
+                       bf16=bf16)
                   if DGRAD_WT else
-                  gemm(g, weight.contiguous(), trans_a=False, trans_b=False, a_amax=g_amax, b_amax=w_amax))
-        dw = gemm(g, x, trans_a=True, trans_b=False, a_amax=g_amax, b_amax=x_amax)
+                  gemm(g, weight.contiguous(), trans_a=False, trans_b=False, a_amax=g_amax, b_amax=w_amax,
+                       bf16=bf16))
+        dw = gemm(g, x, trans_a=True, trans_b=False, a_amax=g_amax, b_amax=x_amax, bf16=bf16)
         db = g.sum(0) if ctx.has_bias else None
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, relu: bool = False,
-           x_amax: torch.Tensor = None, return_amax: bool = False):
-    y, y_amax = LinearFn.apply(x, weight, bias, relu, x_amax)
+           x_amax: torch.Tensor = None, return_amax: bool = False, bf16: bool = False):
+    """act(x W^T + b) on the bgnn GEMM; bf16: bf16 operands, f32 accumulation and output."""
+    y, y_amax = LinearFn.apply(x, weight, bias, relu, x_amax, bf16)
     return (y, y_amax) if return_amax else y
 
 
-def mlp(seq: torch.nn.Sequential, x: torch.Tensor, return_amax: bool = False):
+def mlp(seq: torch.nn.Sequential, x: torch.Tensor, return_amax: bool = False, bf16: bool = False):
     """Run an nn.Sequential of Linear/ReLU through bgnn GEMMs, fusing each ReLU into the
     preceding Linear's epilogue (same parameters, same result as seq(x)). With return_amax,
     also returns max|output| (device scalar) when the last module is a Linear, else None."""
@@ -206,7 +219,7 @@ def mlp(seq: torch.nn.Sequential, x: torch.Tensor, return_amax: bool = False):
         m = mods[i]
         if isinstance(m, torch.nn.Linear):
             fuse = i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.ReLU)
-            x, amax = linear(x, m.weight, m.bias, fuse, x_amax=amax, return_amax=True)
+            x, amax = linear(x, m.weight, m.bias, fuse, x_amax=amax, return_amax=True, bf16=bf16)
             i += 2 if fuse else 1
         else:
             x = m(x)

@@ -336,8 +336,18 @@ struct Plan {
     int split;
 };
 
-static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk) {
+static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk,
+                      int precision = 0) {
     Plan p{};
+    if (precision == 1) {   // bf16 operands, f32 accumulation (the split kernel with one piece)
+        p.x6 = 1;
+        p.prec = 2;
+        p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, 1);
+        if (a_blk != 0 || c_blk != 0) p.cfg = 0;
+        p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
+        p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves, kX6Cfgs[p.cfg].blocks_per_cu});
+        return p;
+    }
     auto planes_ok = [&](int bm, int bn, int bk) {
         return (a_blk == 0 || a_blk % (ta ? bm : bk) == 0) && (c_blk == 0 || c_blk % bn == 0);
     };
@@ -374,6 +384,10 @@ extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta
     return ws_need(make_plan(M, N, K, ta, tb, 0, 0), M, N);
 }
 
+extern "C" size_t bgnn_gemm_ws_bytes_ex(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb, int32_t precision) {
+    return ws_need(make_plan(M, N, K, ta, tb, 0, 0, precision), M, N);
+}
+
 extern "C" int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out,
                                int32_t accumulate, void* stream) {
     BGNN_REQUIRE(rows >= 0 && cols >= 0 && (ld >= cols || rows <= 1), "absmax: bad shape");
@@ -391,8 +405,8 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
                                     const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
                                     int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
                                     int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
-                                    const float* b_amax, float* c_amax, void* ws, size_t ws_bytes,
-                                    void* stream) {
+                                    const float* b_amax, float* c_amax, int32_t precision, void* ws,
+                                    size_t ws_bytes, void* stream) {
     BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
     BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
     const int64_t a_inner = a_blk > 0 ? a_blk : (ta ? M : K);
@@ -400,8 +414,9 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm: bad ldb");
     BGNN_REQUIRE(ldc >= (c_blk > 0 ? c_blk : N) || M == 0, "gemm: bad ldc");
     BGNN_REQUIRE(a_blk >= 0 && c_blk >= 0, "gemm: negative plane block");
+    BGNN_REQUIRE(precision == 0 || precision == 1, "gemm: precision must be 0 (f32-accurate) or 1 (bf16)");
     if (M == 0 || N == 0) return BGNN_OK;
-    const Plan pl = make_plan(M, N, K, ta, tb, a_blk, c_blk);
+    const Plan pl = make_plan(M, N, K, ta, tb, a_blk, c_blk, precision);
     BGNN_REQUIRE((a_blk == 0 || a_blk % (ta ? pl.bm : pl.bk) == 0) && (c_blk == 0 || c_blk % pl.bn == 0),
                  "gemm: plane blocks (a_blk %lld, c_blk %lld) must be multiples of the %dx%dx%d tile",
                  (long long)a_blk, (long long)c_blk, pl.bm, pl.bn, pl.bk);
@@ -465,7 +480,7 @@ extern "C" int bgnn_gemm_f32_planes(int32_t ta, int32_t tb, int64_t M, int64_t N
                                     int64_t c_pstride, const float* bias, int32_t relu, void* ws, size_t ws_bytes,
                                     void* stream) {
     return bgnn_gemm_f32_scaled(ta, tb, M, N, K, alpha, A, lda, a_blk, a_pstride, B, ldb, beta, C, ldc, c_blk,
-                                c_pstride, bias, relu, nullptr, nullptr, nullptr, ws, ws_bytes, stream);
+                                c_pstride, bias, relu, nullptr, nullptr, nullptr, 0, ws, ws_bytes, stream);
 }
 
 extern "C" int bgnn_gemm_f32_ex(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,

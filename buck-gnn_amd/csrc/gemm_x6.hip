@@ -1,5 +1,7 @@
-// f32-accurate GEMMs on the gfx950 16-bit MFMAs, for the same SAGEConv linears as gemm.hip
-// (Models/BuckGNN.py:135-149; fwd, dgrad, wgrad shapes). Two split precisions (PREC):
+// GEMMs on the gfx950 16-bit MFMAs, for the same SAGEConv linears as gemm.hip
+// (Models/BuckGNN.py:135-149; fwd, dgrad, wgrad shapes) and the EA_GNN edge / node MLPs.
+// PREC 2 = bf16 operands (one round-to-nearest piece, one product, f32 accumulation; the
+// bf16 EA_GNN path of BASELINE configs[4]). Two f32-accurate split precisions:
 //
 // PREC 1 = f16x3 (default). Each operand is scaled by a power of two s = 2^k chosen from its
 // max |value| (max |a| * s in [2^14, 2^15), so nothing overflows the f16 range) and split
@@ -137,6 +139,13 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
         const int r = KCONTIG ? (idx >> 2) : (idx % R);
         const int c = KCONTIG ? (idx & 3) : (idx / R);
         const int pos = x6_pos(r, c);
+        if constexpr (PREC == 2) {   // bf16: one round-to-nearest piece
+            uint4 q0;
+            q0.x = pack_bf16(v[u][0], v[u][1]); q0.y = pack_bf16(v[u][2], v[u][3]);
+            q0.z = pack_bf16(v[u][4], v[u][5]); q0.w = pack_bf16(v[u][6], v[u][7]);
+            S[pos] = q0;
+            continue;
+        }
         if constexpr (PREC == 1) {
             uint4 q0, q1;
             if constexpr (ABL == 1) {
@@ -193,11 +202,18 @@ __device__ __forceinline__ void kq_load(const float* __restrict__ P, int64_t ld,
     }
 }
 
-template <int R>
+template <int R, int PREC>
 __device__ __forceinline__ void kq_store(uint4* __restrict__ S, const float (&v)[4][8], int q, float sc) {
     const int r4 = q % (R / 4), c = q / (R / 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+        if constexpr (PREC == 2) {
+            uint4 q0;
+            q0.x = pack_bf16(v[i][0], v[i][1]); q0.y = pack_bf16(v[i][2], v[i][3]);
+            q0.z = pack_bf16(v[i][4], v[i][5]); q0.w = pack_bf16(v[i][6], v[i][7]);
+            S[x6_pos(4 * r4 + i, c)] = q0;
+            continue;
+        }
         uint4 q0, q1;
         split2h(v[i][0] * sc, v[i][1] * sc, q0.x, q1.x);
         split2h(v[i][2] * sc, v[i][3] * sc, q0.y, q1.y);
@@ -223,6 +239,10 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             floatx16 t = acc[i][j];
+            if constexpr (PREC == 2) {   // bf16 operands: one product
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[i][0]), as_bf16x8(fb[j][0]), t, 0, 0, 0);
+                continue;
+            }
             if constexpr (PREC == 1) {   // f16x3: the two cross terms, then the leading product
                 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
                 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
@@ -377,7 +397,7 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
 template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int NT = 64 * WM * WN;
-    constexpr int NP = PREC == 1 ? 2 : 3;   // pieces per operand
+    constexpr int NP = PREC == 1 ? 2 : (PREC == 2 ? 1 : 3);   // pieces per operand
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
@@ -385,8 +405,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
     // epilogue as one [TM*32][32] f32 stage per wave
     constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
-    static_assert((2 * (A_U4 + B_U4)) * 16 >= WM * WN * TM * 32 * 32 * 4, "epilogue stage exceeds the LDS tiles");
-    __shared__ uint4 smem[2 * (A_U4 + B_U4)];
+    constexpr int TILE_U4 = 2 * (A_U4 + B_U4), STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
+    static_assert((TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
+    __shared__ uint4 smem[TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4];
     uint4 (*As)[A_U4] = reinterpret_cast<uint4 (*)[A_U4]>(smem);
     uint4 (*Bs)[B_U4] = reinterpret_cast<uint4 (*)[B_U4]>(smem + 2 * A_U4);
 
@@ -424,7 +445,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    constexpr bool KQ = !AK && !BKc && PREC == 1 && ABL != 7 && BM + BN <= NT && BM % 64 == 0 && BN % 64 == 0 &&
+    constexpr bool KQ = !AK && !BKc && PREC >= 1 && ABL != 7 && BM + BN <= NT && BM % 64 == 0 && BN % 64 == 0 &&
                         BM * BN >= 256 * 128;   // (128x128: measured slower than the dword path)
     // two register sets for the staged slices: slice kt+1 is split into LDS while slices kt+2
     // and kt+3 are in flight (prefetch distance 2; ABL 7 = distance 1 for measurement). The
@@ -455,8 +476,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         };
         auto store_ab = [&](int buf, const Regs& r) {
             if constexpr (KQ) {
-                if (t < BM) kq_store<BM>(As[buf], r.q, t, sa);
-                else if (t < BM + BN) kq_store<BN>(Bs[buf], r.q, t - BM, sb);
+                if (t < BM) kq_store<BM, PREC>(As[buf], r.q, t, sa);
+                else if (t < BM + BN) kq_store<BN, PREC>(Bs[buf], r.q, t - BM, sb);
             } else {
                 x6_store<AK, BM, NT, PREC, ABL>(As[buf], r.a, t, sa);
                 x6_store<BKc, BN, NT, PREC, ABL>(Bs[buf], r.b, t, sb);
@@ -578,7 +599,8 @@ static void launch_prec(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t
 }
 
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    if (prec == 1) launch_prec<1>(ta, tb, cfg, abl, grid, s, g);
+    if (prec == 2) launch_prec<2>(ta, tb, cfg, 0, grid, s, g);
+    else if (prec == 1) launch_prec<1>(ta, tb, cfg, abl, grid, s, g);
     else launch_prec<0>(ta, tb, cfg > 2 ? 1 : cfg, abl, grid, s, g);
 }
 

@@ -249,13 +249,19 @@ int bgnn_gemm_f32_ex(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int
  * exact max gives full accuracy, a larger value loses precision gradually, a smaller one is
  * undefined). NULL = computed here (one read pass). c_amax (optional, any mode): *c_amax =
  * max(*c_amax, max |C|) over the result (fused into the epilogue when possible), so the
- * result can feed the next GEMM without another pass. */
+ * result can feed the next GEMM without another pass. precision: 0 = f32-accurate (default
+ * family), 1 = bf16 operands with f32 accumulation. */
 int bgnn_gemm_f32_scaled(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                          float alpha, const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride,
                          const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
                          int64_t c_blk, int64_t c_pstride, const float* bias, int32_t relu,
                          const float* a_amax, const float* b_amax, float* c_amax,
-                         void* ws, size_t ws_bytes, void* stream);
+                         int32_t precision, void* ws, size_t ws_bytes, void* stream);
+/* Workspace of bgnn_gemm_f32_scaled for a given precision (0 = f32-accurate, the family of
+ * BGNN_TUNE_GEMM_MODE; 1 = bf16 operands rounded to nearest, one MFMA product, f32
+ * accumulation and output: the bf16 EA_GNN path of BASELINE configs[4]). */
+size_t bgnn_gemm_ws_bytes_ex(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b,
+                             int32_t precision);
 /* *out = max(accumulate ? *out : 0, max |x|) over a row-major [rows, cols] matrix (ld). */
 int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out,
                     int32_t accumulate, void* stream);

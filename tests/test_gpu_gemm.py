@@ -174,7 +174,7 @@ def test_absmax_and_supplied_maxima(dev):
     ws_bytes = _lib.query("bgnn_gemm_ws_bytes", 1000, 64, 96, 0, 1)
     ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
     _lib.call("bgnn_gemm_f32_scaled", 0, 1, 1000, 64, 96, 1.0, x.data_ptr(), 96, 0, 0, w.data_ptr(), 96, 0.0,
-              c2.data_ptr(), 64, 0, 0, None, 0, amax[0:].data_ptr(), amax[1:].data_ptr(), None, ws.data_ptr(),
+              c2.data_ptr(), 64, 0, 0, None, 0, amax[0:].data_ptr(), amax[1:].data_ptr(), None, 0, ws.data_ptr(),
               ws.numel(), s)
     torch.testing.assert_close(c1, c2, rtol=0, atol=0)
 
@@ -194,6 +194,23 @@ def test_gemm_c_amax(dev, mode, shape):
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     _lib.call("bgnn_gemm_f32_scaled", ta, tb, M, N, K, 1.0, a.data_ptr(), a.stride(0), 0, 0, b.data_ptr(), b.stride(0),
-              0.0, c.data_ptr(), N, 0, 0, bias.data_ptr(), 1, None, None, cm.data_ptr(), ws.data_ptr(), ws_bytes, s)
+              0.0, c.data_ptr(), N, 0, 0, bias.data_ptr(), 1, None, None, cm.data_ptr(), 0, ws.data_ptr(), ws_bytes, s)
     assert cm.item() == c.abs().max().item()
     assert bool((c >= 0).all())
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+def test_gemm_bf16_precision(dev, ta, tb):
+    """precision = 1: operands rounded to bf16, f32 accumulation -- equal to an fp64 product of the
+    bf16-rounded operands up to the f32 accumulation error."""
+    torch.manual_seed(10)
+    M, N, K = 1500, 384, 2000
+    a = torch.randn((K, M) if ta else (M, K), device=dev)
+    b = torch.randn((N, K) if tb else (K, N), device=dev)
+    c = fused.gemm(a, b, ta, tb, bf16=True)
+    A = a.bfloat16().double().cpu()
+    B = b.bfloat16().double().cpu()
+    A = A.t() if ta else A
+    B = B.t() if tb else B
+    r, mag = A @ B, A.abs() @ B.abs()
+    assert ((c.double().cpu() - r).abs() / mag).max().item() < 2e-6

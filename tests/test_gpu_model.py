@@ -75,3 +75,48 @@ def test_model_matches_reference_golden(dev, path, fused_path):
         pe, _ = model(x, ei, ea, batch)
     np.testing.assert_allclose(pe.cpu().numpy().reshape(-1), z["pred_eval"], **tol)
     np.testing.assert_allclose(captured["pooled"].cpu().numpy(), z["pooled_eval"], **tol)
+
+
+def test_ea_gnn_bf16_block_close_to_f32(dev):
+    """One EA_GNN GraphNetBlock (BASELINE configs[4]) with bf16 GEMM operands (f32 accumulation)
+    against the f32-accurate fused block on the same inputs. The reference is fp32-only, so the
+    bar is PyTorch's own bf16: the per-op block with autocast's bf16 Linear (bf16 operands and
+    outputs, f32 accumulation) run against the same f32 result. Each output and input gradient must stay within 1.5x of autocast's rel-L2
+    error (and really differ from f32, so the bf16 kernels ran)."""
+    from bgnn import synthetic as S
+    from bgnn.buckgnn import GraphNetBlock
+    from bgnn.ea import graphnet_block
+    b = S.make_batch(30, 3).to(dev)
+    torch.manual_seed(0)
+    H = 256
+    blk = GraphNetBlock(H).to(dev)
+    x0 = torch.randn(b.num_nodes, H, device=dev)
+    e0 = torch.randn(b.num_edges, H, device=dev)
+    gx, ge = torch.randn_like(x0), torch.randn_like(e0)
+
+    def run(fn):
+        x, e = x0.clone().requires_grad_(True), e0.clone().requires_grad_(True)
+        xo, eo = fn(x, e)
+        torch.autograd.backward([xo.float(), eo.float()], [gx, ge])
+        return [xo.detach().float(), eo.detach().float(), x.grad, e.grad]
+
+    ref = run(lambda x, e: graphnet_block(blk, x, e, b.edge_index, bf16=False))
+    ours = run(lambda x, e: graphnet_block(blk, x, e, b.edge_index, bf16=True))
+
+    def lin(v, m):   # autocast's bf16 Linear: bf16 operands and output, f32 accumulation
+        return torch.nn.functional.linear(v.bfloat16(), m.weight.bfloat16(), m.bias.bfloat16()).float()
+
+    def autocast_block(x, e):
+        row, col = b.edge_index
+        relu = torch.relu
+        e2 = lin(relu(lin(torch.cat([x[row], x[col], e], 1), blk.edge_mlp[0])), blk.edge_mlp[2])
+        m = lin(relu(lin(torch.cat([x[col], e2], 1), blk.node_mlp_phi[0])), blk.node_mlp_phi[2])
+        deg = torch.bincount(row, minlength=x.size(0)).clamp_min(1).float().unsqueeze(1)
+        agg = torch.zeros_like(x).index_add(0, row, m) / deg
+        out = lin(relu(lin(torch.cat([x, agg], 1), blk.node_mlp_gamma[0])), blk.node_mlp_gamma[2])
+        return out + lin(relu(lin(out, blk.node_mlp_beta[0])), blk.node_mlp_beta[2]), e2
+    torch_bf16 = run(autocast_block)
+    for name, r, o, t in zip(("x", "e", "dx", "de"), ref, ours, torch_bf16):
+        rel_ours = ((o - r).norm() / r.norm()).item()
+        rel_torch = ((t - r).norm() / r.norm()).item()
+        assert 1e-6 < rel_ours <= 1.5 * rel_torch + 1e-4, (name, rel_ours, rel_torch)
