@@ -80,6 +80,8 @@ SIGNATURES = {
                                      c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p, c_p, c_i32, c_p, c_sz,
                                      c_p]),
     "bgnn_gemm_ws_bytes_ex": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32, c_i32]),
+    "bgnn_gemm_gather_add": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i32,
+                                     c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_sz, c_p]),
     "bgnn_absmax_f32": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p]),
     "bgnn_gemm_f32_ex": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p,
                                  c_i64, c_p, c_i32, c_p, c_sz, c_p]),

@@ -19,15 +19,17 @@ are the same for every edge of a node, so they are computed per NODE and gathere
 which removes 2 of the 4 per-edge K = H products of the first layers (3H + 2H -> H + H) and
 leaves every per-edge GEMM at K = H. All GEMMs run on the bgnn split kernels
 (f32-accurate f16x3, or bf16 operands with f32 accumulation when `bf16=True`, the precision
-of BASELINE configs[4]); gathers are row index_selects, their backward and the scatter_mean
-are deterministic bgnn segment reductions over the edge index (no atomics).
+of BASELINE configs[4]). The gathers, the adds and the ReLU of h1 and m1 run in the GEMM
+epilogue (bgnn_gemm_gather_add); their backward and the scatter_mean are deterministic bgnn
+segment reductions over the edge index (no atomics).
 """
 from __future__ import annotations
 
 import torch
 
-from .fused import linear, mlp
-from .graph import SegmentIndex, _index_cache
+from . import _lib
+from .fused import gemm, linear, mlp
+from .graph import SegmentIndex, _index_cache, _stream
 from .ops import segment_reduce
 
 
@@ -70,6 +72,54 @@ def gather_add(a, p1, seg1, p2=None, seg2=None, relu=False):
     return _GatherAdd.apply(a, p1, seg1, p2, seg2, relu)
 
 
+class _LinearGatherReLU(torch.autograd.Function):
+    """out = ReLU(e W^T + b + p1[i1] (+ p2[i2])) as ONE bgnn GEMM whose epilogue gathers the
+    node rows (bgnn_gemm_gather_add): no [E, H] temporaries for the gathers, the adds or the
+    ReLU. Backward: g' = g masked by out > 0; de = g' W, dW = g'^T e, db = sum g', and
+    dp1 / dp2 = deterministic segment sums of g' by i1 / i2."""
+
+    @staticmethod
+    def forward(ctx, e, W, b, p1, seg1: SegmentIndex, p2, seg2: SegmentIndex, bf16: bool):
+        e = e.contiguous()
+        Wc = W.contiguous()
+        M, K = e.shape
+        N = Wc.size(0)
+        if p1.stride(1) != 1 or (p2 is not None and p2.stride(1) != 1):
+            raise ValueError("gather rows must have unit column stride")
+        out = torch.empty(M, N, dtype=torch.float32, device=e.device)
+        prec = 1 if bf16 else 0
+        ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, 0, 1, prec)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=e.device) if ws_bytes else None
+        _lib.call("bgnn_gemm_gather_add", 0, 1, M, N, K, e.data_ptr(), e.stride(0), Wc.data_ptr(), Wc.stride(0),
+                  out.data_ptr(), N, None if b is None else b.contiguous().data_ptr(), 1,
+                  p1.data_ptr(), seg1.index.data_ptr(), p1.stride(0),
+                  None if p2 is None else p2.data_ptr(), None if p2 is None else seg2.index.data_ptr(),
+                  0 if p2 is None else p2.stride(0), prec, None if ws is None else ws.data_ptr(), ws_bytes,
+                  _stream())
+        ctx.seg1, ctx.seg2, ctx.has2, ctx.bf16, ctx.has_bias = seg1, seg2, p2 is not None, bf16, b is not None
+        ctx.save_for_backward(e, W, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        e, W, out = ctx.saved_tensors
+        g = (g * (out > 0)).contiguous()
+        bf16 = ctx.bf16
+        de = gemm(g, W.t().contiguous(), trans_a=False, trans_b=True, bf16=bf16) if ctx.needs_input_grad[0] else None
+        dW = gemm(g, e, trans_a=True, trans_b=False, bf16=bf16)
+        db = g.sum(0) if ctx.has_bias else None
+        d1 = segment_reduce(g, ctx.seg1, "sum")
+        d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
+        return de, dW, db, d1, None, d2, None, None
+
+
+def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False):
+    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16)
+
+# the two-step form (linear, then _GatherAdd) is kept for A/B measurement
+FUSED_GATHER = True
+
+
 def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tensor, bf16: bool = False):
     """(x_out, e_out) of one GraphNetBlock `blk` (bgnn.buckgnn.GraphNetBlock: same parameters
     as the reference's) on the bgnn kernels."""
@@ -82,10 +132,16 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
     x = x.contiguous()
     # node-level blocks of the two concatenation Linears, one GEMM
     P = linear(x, torch.cat([W1[:, :H], W1[:, H:2 * H], Wp[:, :H]], 0), None, False, bf16=bf16)
-    h1 = gather_add(linear(e, W1[:, 2 * H:], b1, False, bf16=bf16), P[:, :H], seg_row, P[:, H:2 * H], seg_col,
-                    relu=True)
+    if FUSED_GATHER:
+        h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P[:, :H], seg_row, P[:, H:2 * H], seg_col, bf16=bf16)
+    else:
+        h1 = gather_add(linear(e, W1[:, 2 * H:], b1, False, bf16=bf16), P[:, :H], seg_row, P[:, H:2 * H],
+                        seg_col, relu=True)
     e_out = linear(h1, W2, b2, False, bf16=bf16)
-    m1 = gather_add(linear(e_out, Wp[:, H:], bp, False, bf16=bf16), P[:, 2 * H:], seg_col, relu=True)
+    if FUSED_GATHER:
+        m1 = linear_gather_relu(e_out, Wp[:, H:], bp, P[:, 2 * H:], seg_col, bf16=bf16)
+    else:
+        m1 = gather_add(linear(e_out, Wp[:, H:], bp, False, bf16=bf16), P[:, 2 * H:], seg_col, relu=True)
     msg = linear(m1, Wp2, bp2, False, bf16=bf16)
     agg = segment_reduce(msg, seg_row, "mean")
     out = mlp(blk.node_mlp_gamma, torch.cat([x, agg], 1), bf16=bf16)

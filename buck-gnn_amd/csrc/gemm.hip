@@ -497,3 +497,48 @@ extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64
     return bgnn_gemm_f32_planes(ta, tb, M, N, K, alpha, A, lda, 0, 0, B, ldb, beta, C, ldc, 0, 0, nullptr, 0, ws,
                                 ws_bytes, stream);
 }
+
+// act(op(A) op(B) + bias + add0[idx0[row]] (+ add1[idx1[row]])) with the gathered rows added in
+// the epilogue of the split kernels (no split-K). precision: 0 = f32-accurate (the split family of
+// BGNN_TUNE_GEMM_MODE; the f32 MFMA family is not supported here), 1 = bf16 operands.
+extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
+                                    int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                                    const float* bias, int32_t relu, const float* add0, const int64_t* idx0,
+                                    int64_t ld0, const float* add1, const int64_t* idx1, int64_t ld1,
+                                    int32_t precision, void* ws, size_t ws_bytes, void* stream) {
+    BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm_gather_add: bad transpose flags");
+    BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_gather_add: negative size");
+    BGNN_REQUIRE(precision == 0 || precision == 1, "gemm_gather_add: precision must be 0 or 1");
+    BGNN_REQUIRE(add0 != nullptr && idx0 != nullptr && ld0 >= N, "gemm_gather_add: add0/idx0/ld0 required");
+    BGNN_REQUIRE(add1 == nullptr || (idx1 != nullptr && ld1 >= N), "gemm_gather_add: bad add1/idx1/ld1");
+    BGNN_REQUIRE((ta == 0 && lda >= K) || (ta == 1 && lda >= M) || M == 0 || K == 0, "gemm_gather_add: bad lda");
+    BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm_gather_add: bad ldb");
+    BGNN_REQUIRE(ldc >= N || M == 0, "gemm_gather_add: bad ldc");
+    if (M == 0 || N == 0) return BGNN_OK;
+    const Plan pl = make_plan(M, N, K, ta, tb, 0, 0, precision);
+    BGNN_REQUIRE(pl.x6, "gemm_gather_add: needs the split GEMM family (BGNN_TUNE_GEMM_MODE 1 or 2)");
+    const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
+    BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm_gather_add: too many tiles");
+    hipStream_t s = as_stream(stream);
+    const bool h3 = pl.prec == 1;
+    const float* a_amax = nullptr;
+    const float* b_amax = nullptr;
+    if (h3) {
+        BGNN_REQUIRE(ws != nullptr && ws_bytes >= kAmaxHead, "gemm_gather_add: f16x3 needs bgnn_gemm_ws_bytes_ex()");
+        float* head_amax = static_cast<float*>(ws);
+        BGNN_HIP(hipMemsetAsync(ws, 0, 2 * sizeof(float), s));
+        launch_absmax(A, ta ? K : M, ta ? M : K, lda, 0, 0, head_amax, s);
+        BGNN_CHECK_LAUNCH();
+        launch_absmax(B, tb ? N : K, tb ? K : N, ldb, 0, 0, head_amax + 1, s);
+        BGNN_CHECK_LAUNCH();
+        a_amax = head_amax;
+        b_amax = head_amax + 1;
+    }
+    GemmArgs g{A, B, C, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, 0, 1, bias, relu,
+               0, 0, 0, 0, a_amax, b_amax, nullptr, add0, idx0, ld0, add1, idx1, ld1};
+    g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;
+    if (g.kchunk == 0) g.kchunk = pl.bk;
+    launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles, 1), s, g);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}

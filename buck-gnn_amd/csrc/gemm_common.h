@@ -23,6 +23,10 @@ struct GemmArgs {
     const float* a_amax;   // f16x3 (PREC 1): device max|A| and max|B|, which set the power-of-two
     const float* b_amax;   // operand scales
     float* c_amax;         // split kernels, no split-K: max |C| folded in here (NULL = off)
+    // split kernels, no split-K: C[r, :] += ga0[gi0[r], :] (+ ga1[gi1[r], :]) before the ReLU
+    // (EA_GNN's node-level blocks of the edge Linears, bgnn/ea.py); NULL = off
+    const float* ga0; const int64_t* gi0; int64_t ldg0;
+    const float* ga1; const int64_t* gi1; int64_t ldg1;
 };
 
 // Base pointer that makes plane-split storage addressable with global coordinates:

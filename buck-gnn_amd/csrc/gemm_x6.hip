@@ -292,7 +292,9 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
     uint32_t cmax = 0;
     // interior tile, no split-K, no beta, aligned: per-column-block bias and pointer, per-row
     // pointer increments only (the general path below recomputes everything per float4)
-    const bool fast = !split && vec && g.beta == 0.f && (!g.bias || bias_vec) && r0 + TM * 32 <= g.M &&
+    const bool gvec = (!g.ga0 || ((((uintptr_t)g.ga0 & 15) == 0) && g.ldg0 % 4 == 0)) &&
+                      (!g.ga1 || ((((uintptr_t)g.ga1 & 15) == 0) && g.ldg1 % 4 == 0));
+    const bool fast = !split && vec && gvec && g.beta == 0.f && (!g.bias || bias_vec) && r0 + TM * 32 <= g.M &&
                       c0 + TN * 32 <= g.N;
     const float iab = ia * ib;   // exact unless the two scales over/underflow together
     const bool one_mul = iab != 0.f && iab < 3.0e38f;
@@ -314,11 +316,20 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                 const float4 sv = *reinterpret_cast<const float4*>(stage + (q * 8 + rq) * 32 + c4);
                 float e[4] = {sv.x, sv.y, sv.z, sv.w};
                 const float b4[4] = {bv.x, bv.y, bv.z, bv.w};
+                float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+                if (g.ga0) {
+                    const int64_t row = r0 + q * 8 + rq;
+                    a0 = *reinterpret_cast<const float4*>(g.ga0 + g.gi0[row] * g.ldg0 + col);
+                    if (g.ga1) a1 = *reinterpret_cast<const float4*>(g.ga1 + g.gi1[row] * g.ldg1 + col);
+                }
+                const float x0[4] = {a0.x, a0.y, a0.z, a0.w}, x1[4] = {a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     float v = one_mul ? e[k] * iab : (e[k] * ia) * ib;
                     if (g.alpha != 1.f) v *= g.alpha;
                     if (g.bias) v += b4[k];
+                    if (g.ga0) v += x0[k];
+                    if (g.ga1) v += x1[k];
                     if (g.relu) v = fmaxf(v, 0.f);
                     e[k] = v;
                     cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
@@ -364,11 +375,23 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                         for (int k = 0; k < 4; ++k) bv[k] = col + k < g.N ? g.bias[col + k] : 0.f;
                     }
                 }
+                float x0[4] = {0.f, 0.f, 0.f, 0.f}, x1[4] = {0.f, 0.f, 0.f, 0.f};
+                if (g.ga0) {
+                    const float* s0 = g.ga0 + g.gi0[row] * g.ldg0 + col;
+                    const float* s1 = g.ga1 ? g.ga1 + g.gi1[row] * g.ldg1 + col : nullptr;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        x0[k] = col + k < g.N ? s0[k] : 0.f;
+                        x1[k] = (s1 && col + k < g.N) ? s1[k] : 0.f;
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     float v = e[k] * g.alpha;
                     if (g.beta != 0.f) v += g.beta * prev[k];
                     if (g.bias) v += bv[k];
+                    if (g.ga0) v += x0[k];
+                    if (g.ga1) v += x1[k];
                     if (g.relu) v = fmaxf(v, 0.f);
                     e[k] = v;
                     if (col + k < g.N) cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);

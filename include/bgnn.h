@@ -262,6 +262,15 @@ int bgnn_gemm_f32_scaled(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
  * accumulation and output: the bf16 EA_GNN path of BASELINE configs[4]). */
 size_t bgnn_gemm_ws_bytes_ex(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b,
                              int32_t precision);
+/* C = act(op(A) op(B) + bias + add0[idx0[r], :] (+ add1[idx1[r], :])) -- gathered row adds
+ * in the GEMM epilogue, no split-K (EA_GNN's edge Linears with their node-level blocks,
+ * Models/BuckGNN.py:553-560 via bgnn/ea.py). idx* are int64 row indices into add* (ld*).
+ * precision: 0 = f32-accurate split family, 1 = bf16 operands. ws: bgnn_gemm_ws_bytes_ex(). */
+int bgnn_gemm_gather_add(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                         const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                         const float* bias, int32_t relu, const float* add0, const int64_t* idx0, int64_t ld0,
+                         const float* add1, const int64_t* idx1, int64_t ld1, int32_t precision,
+                         void* ws, size_t ws_bytes, void* stream);
 /* *out = max(accumulate ? *out : 0, max |x|) over a row-major [rows, cols] matrix (ld). */
 int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out,
                     int32_t accumulate, void* stream);

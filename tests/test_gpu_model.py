@@ -120,3 +120,28 @@ def test_ea_gnn_bf16_block_close_to_f32(dev):
         rel_ours = ((o - r).norm() / r.norm()).item()
         rel_torch = ((t - r).norm() / r.norm()).item()
         assert 1e-6 < rel_ours <= 1.5 * rel_torch + 1e-4, (name, rel_ours, rel_torch)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_ea_fused_gather_epilogue_matches_two_step(dev, monkeypatch, bf16):
+    """The GEMM-epilogue gather (bgnn_gemm_gather_add) equals linear + index_select adds + ReLU:
+    outputs and every gradient (identical arithmetic order; the gathered rows are added after
+    the bias, as torch's a + p1[i] + p2[j])."""
+    from bgnn import ea
+    from bgnn import synthetic as S
+    from bgnn.buckgnn import GraphNetBlock
+    b = S.make_batch(30, 3).to(dev)
+    torch.manual_seed(1)
+    blk = GraphNetBlock(128).to(dev)
+    x0 = torch.randn(b.num_nodes, 128, device=dev)
+    e0 = torch.randn(b.num_edges, 128, device=dev)
+    res = []
+    for fused_gather in (False, True):
+        monkeypatch.setattr(ea, "FUSED_GATHER", fused_gather)
+        blk.zero_grad(set_to_none=True)
+        x, e = x0.clone().requires_grad_(True), e0.clone().requires_grad_(True)
+        xo, eo = ea.graphnet_block(blk, x, e, b.edge_index, bf16=bf16)
+        (xo.square().sum() + eo.sum()).backward()
+        res.append([xo.detach(), eo.detach(), x.grad, e.grad, blk.edge_mlp[0].weight.grad.clone()])
+    for a, c in zip(*res):
+        torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-5)
