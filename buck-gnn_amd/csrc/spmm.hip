@@ -400,14 +400,23 @@ __global__ __launch_bounds__(256) void k_seg_chunk(SegArgs A) {
     }
 }
 
-// Combine heavy rows: one wave (64 threads) per heavy row, chunks in order.
+// Combine heavy rows: one 256-thread block per heavy row (and column tile). For SUM / MEAN the
+// four waves sum four contiguous quarters of the row's chunks and wave 0 adds the quarter sums
+// in order: a fixed summation tree (deterministic, the same for every light-row kernel
+// variant) with 4x the memory parallelism of one wave walking 79 chunks of a super node
+// (cfg3: 44 us -> see DESIGN.md). MAX keeps one wave walking the chunks in order
+// (first-occurrence argmax).
 template <int VEC, int NV, int LPR, int OP, int EPI>
-__global__ __launch_bounds__(64) void k_seg_combine(SegArgs A) {
+__global__ __launch_bounds__(256) void k_seg_combine(SegArgs A) {
+    constexpr int W = (OP == OP_MAX) ? 1 : 4;
+    constexpr int TW = LPR * VEC * NV;   // columns of one column tile
+    __shared__ __attribute__((aligned(16))) float red[W][TW];
     const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
     const int h = blockIdx.x;
-    if (h >= A.n_heavy) return;
-    if (lane / LPR != 0) return;
-    const int cb = blockIdx.y * (LPR * VEC * NV);
+    if (h >= A.n_heavy) return;   // uniform over the block
+    const bool act = (lane / LPR == 0) && wave < W;
+    const int cb = blockIdx.y * TW;
     const int lir = lane % LPR;
     int cpos[NV];
     bool cok[NV];
@@ -415,29 +424,55 @@ __global__ __launch_bounds__(64) void k_seg_combine(SegArgs A) {
     const int64_t r = A.heavy_row[h];
     const int32_t deg = A.rowptr[r + 1] - A.rowptr[r];
     const int32_t c0 = A.heavy_chunk0[h], c1 = A.heavy_chunk0[h + 1];
+    const int32_t per = (c1 - c0 + W - 1) / W;
+    const int32_t qa = min(c1, c0 + wave * per), qb = min(c1, qa + per);
     Acc<VEC, NV, OP> acc;
     acc.init();
+    if (act) {
 #pragma unroll 8
-    for (int32_t c = c0; c < c1; ++c) {
+        for (int32_t c = qa; c < qb; ++c) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            if (!cok[v]) continue;
-            const Vec<VEC> p = ld<VEC>(A.partial + (int64_t)c * A.H + cpos[v]);
-            if constexpr (OP == OP_MAX) {
-                int32_t pa[VEC];
-                ldi<VEC>(A.partial_arg + (int64_t)c * A.H + cpos[v], pa);
+            for (int v = 0; v < NV; ++v) {
+                if (!cok[v]) continue;
+                const Vec<VEC> p = ld<VEC>(A.partial + (int64_t)c * A.H + cpos[v]);
+                if constexpr (OP == OP_MAX) {
+                    int32_t pa[VEC];
+                    ldi<VEC>(A.partial_arg + (int64_t)c * A.H + cpos[v], pa);
 #pragma unroll
-                for (int q = 0; q < VEC; ++q) {
-                    const bool better = p.f[q] > acc.a[v][q];
-                    acc.a[v][q] = better ? p.f[q] : acc.a[v][q];
-                    acc.g[v][q] = better ? pa[q] : acc.g[v][q];
+                    for (int q = 0; q < VEC; ++q) {
+                        const bool better = p.f[q] > acc.a[v][q];
+                        acc.a[v][q] = better ? p.f[q] : acc.a[v][q];
+                        acc.g[v][q] = better ? pa[q] : acc.g[v][q];
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) acc.a[v][q] += p.f[q];
                 }
-            } else {
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) acc.a[v][q] += p.f[q];
             }
         }
     }
+    if constexpr (W > 1) {
+        if (act) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (cok[v])
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) red[wave][cpos[v] - cb + q] = acc.a[v][q];
+        }
+        __syncthreads();
+        if (wave != 0) return;
+        if (act) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (cok[v])
+#pragma unroll
+                    for (int q = 0; q < VEC; ++q) {
+                        const int i = cpos[v] - cb + q;
+                        acc.a[v][q] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+                    }
+        }
+    }
+    if (wave != 0 || !act) return;
     if constexpr (EPI == EPI_SAGE) {
         float bs[NV][4], bq[NV][4];
 #pragma unroll
@@ -750,7 +785,7 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
                            A);
         BGNN_CHECK_LAUNCH();
         constexpr int MOP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MEAN ? OP_MEAN : OP_SUM);
-        hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles), dim3(64), 0, s, A);
+        hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles), dim3(256), 0, s, A);
         BGNN_CHECK_LAUNCH();
     }
     return BGNN_OK;
