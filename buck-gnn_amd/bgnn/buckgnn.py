@@ -210,12 +210,14 @@ class BuckGNN(nn.Module):
             graph = graph_for(edge_index, x.size(0))
             red = 1 if aggr == "mean" else 0
             amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
+            bufs = torch.zeros(L, 3, dtype=torch.float32, device=x.device)   # per-layer operand maxima, one fill
             for i in range(L):
                 conv = convs[i] if convs is not None else self.shared_graphsage_block
                 bn = bns[i] if bns is not None else None
                 skip = 0 < i < L - 1
                 x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
-                                     skip, p, self.training, self._seed(), x_amax=amax, return_amax=True)
+                                     skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
+                                     amax_buf=bufs[i])
             return x
         for i in range(L):
             x_prev = x

@@ -160,9 +160,10 @@ class LinearFn(torch.autograd.Function):
     GEMMs on the same kernel, sharing one max|g| pass (Models/BuckGNN.py:67-74 encoder)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool, x_amax, bf16: bool = False):
+    def forward(ctx, x, weight, bias, relu: bool, x_amax, bf16: bool = False, amax=None):
         x = x.contiguous()
-        amax = torch.zeros(2, dtype=torch.float32, device=x.device)   # [max|W|, max|y|]
+        if amax is None:   # [max|W|, max|y|], zeroed (callers batch these: one fill per MLP)
+            amax = torch.zeros(2, dtype=torch.float32, device=x.device)
         w_amax, y_amax = amax[0:1], amax[1:2]
         if not bf16:   # (bf16 operands need no scales)
             absmax(weight, w_amax, accumulate=True)
@@ -198,13 +199,14 @@ class LinearFn(torch.autograd.Function):
                        bf16=bf16))
         dw = gemm(g, x, trans_a=True, trans_b=False, a_amax=g_amax, b_amax=x_amax, bf16=bf16)
         db = g.sum(0) if ctx.has_bias else None
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, relu: bool = False,
-           x_amax: torch.Tensor = None, return_amax: bool = False, bf16: bool = False):
-    """act(x W^T + b) on the bgnn GEMM; bf16: bf16 operands, f32 accumulation and output."""
-    y, y_amax = LinearFn.apply(x, weight, bias, relu, x_amax, bf16)
+           x_amax: torch.Tensor = None, return_amax: bool = False, bf16: bool = False, amax_buf=None):
+    """act(x W^T + b) on the bgnn GEMM; bf16: bf16 operands, f32 accumulation and output.
+    amax_buf: optional zeroed 2-float device scratch for [max|W|, max|y|]."""
+    y, y_amax = LinearFn.apply(x, weight, bias, relu, x_amax, bf16, amax_buf)
     return (y, y_amax) if return_amax else y
 
 
@@ -215,11 +217,15 @@ def mlp(seq: torch.nn.Sequential, x: torch.Tensor, return_amax: bool = False, bf
     mods = list(seq)
     i = 0
     amax = None
+    n_lin = sum(isinstance(m, torch.nn.Linear) for m in mods)
+    bufs = torch.zeros(n_lin, 2, dtype=torch.float32, device=x.device)   # one fill for the whole MLP
+    k = 0
     while i < len(mods):
         m = mods[i]
         if isinstance(m, torch.nn.Linear):
             fuse = i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.ReLU)
-            x, amax = linear(x, m.weight, m.bias, fuse, x_amax=amax, return_amax=True, bf16=bf16)
+            x, amax = linear(x, m.weight, m.bias, fuse, x_amax=amax, return_amax=True, bf16=bf16, amax_buf=bufs[k])
+            k += 1
             i += 2 if fuse else 1
         else:
             x = m(x)
@@ -253,13 +259,15 @@ class SageLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_prev, x_amax, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
-                cfg: LayerConfig):
+                cfg: LayerConfig, amax=None):
         N, H = x_prev.shape
         dev = x_prev.device
         x_prev = x_prev.contiguous()
         wcat = torch.cat([w_l, w_r], 0).contiguous()             # [2H, H]
         # operand maxima: [0] = max|W|, [1] = max|x_next| (this layer's output), [2] = max|dz|
-        amax = torch.zeros(3, dtype=torch.float32, device=dev)
+        # (zeroed; the layer loop passes one slice of a single per-step fill)
+        if amax is None:
+            amax = torch.zeros(3, dtype=torch.float32, device=dev)
         w_amax, next_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
         absmax(wcat, w_amax, accumulate=True)
         if x_amax is None:
@@ -374,12 +382,12 @@ class SageLayerFn(torch.autograd.Function):
         dw_l, dw_r = dw[:H], dw[H:]
         has_affine = bn and gamma.numel() > 0
         return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
-               seed: int, x_amax: torch.Tensor = None, return_amax: bool = False):
+               seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None):
     """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
     x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
     spares the GEMM a pass over x_prev; return_amax: also return max|x_next|."""
@@ -400,8 +408,8 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
-                                bn_module.running_mean, bn_module.running_var, graph, cfg)
+                                bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf)
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
-        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg)
+        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf)
     return out if return_amax else out[0]
