@@ -62,7 +62,7 @@ class _GatherAdd(torch.autograd.Function):
         (out,) = ctx.saved_tensors
         g = g.contiguous()
         if ctx.relu:
-            g = g * (out > 0)
+            g = torch.ops.aten.threshold_backward(g, out, 0.0)   # one pass: g where out > 0
         d1 = segment_reduce(g, ctx.seg1, "sum")
         d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
         return g, d1, None, d2, None, None
@@ -103,7 +103,7 @@ class _LinearGatherReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         e, W, out = ctx.saved_tensors
-        g = (g * (out > 0)).contiguous()
+        g = torch.ops.aten.threshold_backward(g.contiguous(), out, 0.0)   # ReLU mask in one pass
         bf16 = ctx.bf16
         de = gemm(g, W.t().contiguous(), trans_a=False, trans_b=True, bf16=bf16) if ctx.needs_input_grad[0] else None
         dW = gemm(g, e, trans_a=True, trans_b=False, bf16=bf16)
@@ -115,6 +115,23 @@ class _LinearGatherReLU(torch.autograd.Function):
 
 def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False):
     return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16)
+
+class _ColumnBlocks(torch.autograd.Function):
+    """Split [N, k*H] into k column views whose backward is ONE concatenation of the k
+    gradients (autograd's slice backward would zero-fill and add k full [N, k*H] buffers)."""
+
+    @staticmethod
+    def forward(ctx, P, k: int):
+        ctx.k = k
+        H = P.size(1) // k
+        return tuple(P[:, i * H:(i + 1) * H] for i in range(k))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ref = next(g for g in gs if g is not None)
+        gs = [torch.zeros_like(ref) if g is None else g for g in gs]
+        return torch.cat(gs, 1), None
+
 
 # the two-step form (linear, then _GatherAdd) is kept for A/B measurement
 FUSED_GATHER = True
@@ -132,16 +149,17 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
     x = x.contiguous()
     # node-level blocks of the two concatenation Linears, one GEMM
     P = linear(x, torch.cat([W1[:, :H], W1[:, H:2 * H], Wp[:, :H]], 0), None, False, bf16=bf16)
+    P_row, P_col, Q = _ColumnBlocks.apply(P, 3)
     if FUSED_GATHER:
-        h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P[:, :H], seg_row, P[:, H:2 * H], seg_col, bf16=bf16)
+        h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=bf16)
     else:
-        h1 = gather_add(linear(e, W1[:, 2 * H:], b1, False, bf16=bf16), P[:, :H], seg_row, P[:, H:2 * H],
+        h1 = gather_add(linear(e, W1[:, 2 * H:], b1, False, bf16=bf16), P_row, seg_row, P_col,
                         seg_col, relu=True)
     e_out = linear(h1, W2, b2, False, bf16=bf16)
     if FUSED_GATHER:
-        m1 = linear_gather_relu(e_out, Wp[:, H:], bp, P[:, 2 * H:], seg_col, bf16=bf16)
+        m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=bf16)
     else:
-        m1 = gather_add(linear(e_out, Wp[:, H:], bp, False, bf16=bf16), P[:, 2 * H:], seg_col, relu=True)
+        m1 = gather_add(linear(e_out, Wp[:, H:], bp, False, bf16=bf16), Q, seg_col, relu=True)
     msg = linear(m1, Wp2, bp2, False, bf16=bf16)
     agg = segment_reduce(msg, seg_row, "mean")
     out = mlp(blk.node_mlp_gamma, torch.cat([x, agg], 1), bf16=bf16)

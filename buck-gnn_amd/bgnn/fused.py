@@ -185,7 +185,7 @@ class LinearFn(torch.autograd.Function):
         x, weight, y, x_amax, w_amax = ctx.saved_tensors
         g = g.contiguous()
         if ctx.relu:
-            g = g * (y > 0)
+            g = torch.ops.aten.threshold_backward(g, y, 0.0)   # ReLU mask in one pass
         bf16 = ctx.bf16
         g_amax = None if bf16 else absmax(g)
         w_amax = None if bf16 else w_amax
