@@ -125,3 +125,21 @@ def test_graph_store_requires_gpu():
     from bgnn import synthetic as S
     with pytest.raises(RuntimeError):
         bgnn.GraphStore([S.make_mesh_graph(5, seed=0)], device="cpu")
+
+
+def test_column_blocks_backward_is_one_concat():
+    """bgnn.ea._ColumnBlocks: the k column views of P, with an unused block's gradient zero."""
+    from bgnn.ea import _ColumnBlocks
+    P = torch.randn(7, 12, dtype=torch.float64, requires_grad=True)
+    a, b, c = _ColumnBlocks.apply(P, 3)
+    assert torch.equal(torch.cat([a, b, c], 1), P.detach())
+    w = torch.randn(7, 4, dtype=torch.float64)
+    ((a * w).sum() + (c * 2 * w).sum()).backward()
+    assert torch.equal(P.grad, torch.cat([w, torch.zeros_like(w), 2 * w], 1))
+
+
+def test_relu_mask_matches_reference_form():
+    """threshold_backward (the backward ReLU mask of bgnn.ea / bgnn.fused) == g * (out > 0)."""
+    g, out = torch.randn(64, 33), torch.randn(64, 33)
+    out[0, :5] = 0.0
+    assert torch.equal(torch.ops.aten.threshold_backward(g, out, 0.0), g * (out > 0))
