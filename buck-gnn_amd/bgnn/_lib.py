@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lock = threading.Lock()
 _lib = None
@@ -40,6 +40,13 @@ class CsrStruct(ctypes.Structure):
         ("n_chunks", c_i32),
         ("chunk", c_i32),
         ("_pad", c_i32),
+        ("gsrc", c_p),
+        ("gmask", c_p),
+        ("gcnt", c_p),
+        ("grow", c_p),
+        ("n_groups", c_i64),
+        ("group_rows", c_i32),
+        ("_pad2", c_i32),
     ]
 
 
@@ -60,7 +67,9 @@ SIGNATURES = {
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
                               c_p, c_p, c_p]),
-    "bgnn_sage_fwd_slots": (c_i32, [c_i64]),
+    "bgnn_sage_fwd_slots": (c_i32, [ctypes.POINTER(CsrStruct)]),
+    "bgnn_group_plan": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "bgnn_store_gather_groups": (c_i32, [c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64] + [c_p] * 14),
     "bgnn_sage_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p,
                               c_p, c_p]),
     "bgnn_bn_finalize": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,

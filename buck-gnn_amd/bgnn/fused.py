@@ -283,7 +283,7 @@ class SageLayerFn(torch.autograd.Function):
                 zl, zr, ldz = z, z[:, H:], 2 * H
         o = torch.empty(N, H, dtype=torch.float32, device=dev)
         nrm = torch.empty(N, dtype=torch.float32, device=dev)
-        slots = _lib.query("bgnn_sage_fwd_slots", N) + graph.fwd.plan.n_heavy
+        slots = _lib.query("bgnn_sage_fwd_slots", graph.fwd.ref())
         bn_part = torch.empty(slots, 2, H, dtype=torch.float32, device=dev)
         part = (torch.empty(graph.fwd.plan.n_chunks * H, dtype=torch.float32, device=dev)
                 if graph.fwd.plan.n_chunks else None)

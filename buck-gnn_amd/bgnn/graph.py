@@ -19,6 +19,11 @@ import torch
 from . import _lib
 
 DEFAULT_CHUNK = 64
+# Rows per row-group of the sum/mean aggregation kernels (bgnn_group_plan; 0 = no plans, the
+# per-row sweep kernel). Consecutive mesh rows share most neighbours: with 4 rows per group cfg2
+# fetches 5.5 source rows per target row instead of 8.9 (8 rows: 4.7, but twice the registers
+# and half the waves per CU; measured slower, tools/tune_agg.py).
+GROUP_ROWS = 4
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -73,22 +78,58 @@ def make_plan(rowptr: torch.Tensor, n_rows: int, nnz: int, chunk: int = DEFAULT_
 
 
 @dataclass
+class Groups:
+    """Row-group plan of a CSR (bgnn_group_plan): per group of at most `rows` consecutive rows,
+    its distinct source rows (gsrc) and the mask of the group rows using each (gmask). `grow`
+    (optional, [n_groups + 1]) holds each group's first row; None means g * rows."""
+
+    gsrc: torch.Tensor
+    gmask: torch.Tensor
+    gcnt: torch.Tensor
+    rows: int
+    grow: Optional[torch.Tensor] = None
+    n_groups: int = 0
+
+
+def enqueue_groups(rowptr: torch.Tensor, col: torch.Tensor, n_rows: int, nnz: int, chunk: int,
+                   rows: Optional[int] = None, grow: Optional[torch.Tensor] = None,
+                   n_groups: Optional[int] = None) -> Optional[Groups]:
+    """Launch bgnn_group_plan (asynchronous) or return None when plans are off / unsupported."""
+    rows = GROUP_ROWS if rows is None else rows
+    if rows <= 0 or chunk > 64 or n_rows == 0:
+        return None
+    dev = rowptr.device
+    G = int(n_groups) if grow is not None else (n_rows + rows - 1) // rows
+    gsrc = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    gmask = torch.empty(max(nnz, 1), dtype=torch.uint8, device=dev)
+    gcnt = torch.empty(max(G, 1), dtype=torch.int32, device=dev)
+    _lib.call("bgnn_group_plan", rowptr.data_ptr(), col.data_ptr(), n_rows, chunk, rows, _ptr(grow), G,
+              gsrc.data_ptr(), gmask.data_ptr(), gcnt.data_ptr(), _stream())
+    return Groups(gsrc, gmask, gcnt, rows, grow, G)
+
+
+@dataclass
 class Csr:
     rowptr: torch.Tensor
     col: torch.Tensor
     n_rows: int
     nnz: int
     plan: Plan
+    groups: Optional[Groups] = None
     _struct: Optional[_lib.CsrStruct] = field(default=None, repr=False)
 
     def struct(self) -> _lib.CsrStruct:
         if self._struct is None:
             p = self.plan
             assert p.n_heavy >= 0, "plan counts not resolved (call resolve())"
+            gr = self.groups
             self._struct = _lib.CsrStruct(
                 self.rowptr.data_ptr(), self.col.data_ptr(), p.heavy_row.data_ptr(),
                 p.heavy_chunk0.data_ptr(), p.chunk_heavy.data_ptr(), self.n_rows, self.nnz,
-                p.n_heavy, p.n_chunks, p.chunk, 0)
+                p.n_heavy, p.n_chunks, p.chunk, 0,
+                gr.gsrc.data_ptr() if gr else None, gr.gmask.data_ptr() if gr else None,
+                gr.gcnt.data_ptr() if gr else None, _ptr(gr.grow) if gr else None,
+                gr.n_groups if gr else 0, gr.rows if gr else 0, 0)
         return self._struct
 
     def ref(self):
@@ -130,8 +171,10 @@ class Graph:
         _lib.call("bgnn_graph_build", ei.data_ptr(), E, N, rowptr.data_ptr(), col.data_ptr(),
                   rowptr_t.data_ptr(), col_t.data_ptr(), perm_t.data_ptr(), ws.data_ptr(), ws.numel(),
                   meta.data_ptr(), _stream())
-        fwd = Csr(rowptr, col, N, E, enqueue_plan(rowptr, N, E, meta[1:3], chunk))
-        bwd = Csr(rowptr_t, col_t, N, E, enqueue_plan(rowptr_t, N, E, meta[3:5], chunk))
+        fwd = Csr(rowptr, col, N, E, enqueue_plan(rowptr, N, E, meta[1:3], chunk),
+                  enqueue_groups(rowptr, col, N, E, chunk))
+        bwd = Csr(rowptr_t, col_t, N, E, enqueue_plan(rowptr_t, N, E, meta[3:5], chunk),
+                  enqueue_groups(rowptr_t, col_t, N, E, chunk))
         return Graph(N, E, fwd, bwd, perm_t, edge_index, meta)
 
     def resolve(self, meta_host) -> "Graph":

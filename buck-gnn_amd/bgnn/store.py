@@ -26,8 +26,9 @@ import torch
 
 from . import _lib
 from .data import Batch, Data
-from .graph import (DEFAULT_CHUNK, Csr, Graph, Plan, SegmentIndex, _graph_cache, _index_cache, _stream,
-                    enqueue_plan)
+from . import graph as _graph
+from .graph import (DEFAULT_CHUNK, Csr, Graph, Groups, Plan, SegmentIndex, _graph_cache, _index_cache, _stream,
+                    enqueue_groups, enqueue_plan)
 
 _GROUP_EDGES = 1 << 30   # graphs are CSR-built in groups of < 2^30 edges (int32 positions)
 
@@ -109,6 +110,20 @@ class GraphStore:
         self.col_t = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
         self.perm_t = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
         heavy = torch.zeros(G, 4, dtype=torch.int64, device=dev)
+        # row-group plans (bgnn_group_plan), per graph: groups start at the graph's first node, so
+        # a batch's plan is the concatenation of its graphs' plans (bgnn_store_gather_groups)
+        R = _graph.GROUP_ROWS if chunk <= 64 else 0
+        self.group_rows = R
+        if R > 0:
+            self.n_groups = (n + R - 1) // R
+            self.group_off = np.concatenate([[0], np.cumsum(self.n_groups)])
+            sumG = int(self.group_off[-1])
+            self.gsrc = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
+            self.gmask = torch.empty(max(sumE, 1), dtype=torch.uint8, device=dev)
+            self.gsrc_t = torch.empty(max(sumE, 1), dtype=torch.int32, device=dev)
+            self.gmask_t = torch.empty(max(sumE, 1), dtype=torch.uint8, device=dev)
+            self.gcnt = torch.zeros(max(sumG, 1), dtype=torch.int32, device=dev)
+            self.gcnt_t = torch.zeros(max(sumG, 1), dtype=torch.int32, device=dev)
         g0 = 0
         while g0 < G:
             g1 = g0 + 1
@@ -142,6 +157,22 @@ class GraphStore:
             self.col_t[e0:e1] = (gr.bwd.col[:e1 - e0].to(torch.int64) - noff[gid_e]).to(torch.int32)
             self.perm_t[e0:e1] = (gr.perm_t[:e1 - e0].to(torch.int64) - eoff[gid_e]).to(torch.int32)
             ei_l[:, e0:e1] = (ei - noff[gid_e]).to(torch.int32)
+        R = self.group_rows
+        if R > 0 and n1 > n0:
+            # groups of R rows from each graph's first node (graph-local after the rebase below)
+            ng = self.n_groups[g0:g1]
+            k = np.arange(int(ng.sum())) - np.repeat(self.group_off[g0:g1] - self.group_off[g0], ng)
+            grow = np.concatenate([np.repeat(self.node_off[g0:g1] - n0, ng) + k * R, [n1 - n0]])
+            grow_d = torch.from_numpy(grow.astype(np.int32)).to(dev)
+            G0, G1 = int(self.group_off[g0]), int(self.group_off[g1])
+            for csr, gsrc, gmask, gcnt in ((gr.fwd, self.gsrc, self.gmask, self.gcnt),
+                                           (gr.bwd, self.gsrc_t, self.gmask_t, self.gcnt_t)):
+                p = enqueue_groups(csr.rowptr, csr.col, n1 - n0, e1 - e0, self.chunk, R, grow_d, G1 - G0)
+                gcnt[G0:G1] = p.gcnt[:G1 - G0]
+                if e1 > e0:
+                    # keys of a group lie inside its graph's edge range: graph-local source ids
+                    gsrc[e0:e1] = (p.gsrc[:e1 - e0].to(torch.int64) - noff[gid_e]).to(torch.int32)
+                    gmask[e0:e1] = p.gmask[:e1 - e0]
         hf, cf = _heavy_counts(gr.fwd.rowptr, gid_n, Gg, self.chunk)
         hb, cb = _heavy_counts(gr.bwd.rowptr, gid_n, Gg, self.chunk)
         heavy[g0:g1] = torch.stack([hf, cf, hb, cb], 1)
@@ -202,8 +233,9 @@ class GraphStore:
 
         # graph structure of the batch, registered for prepare()/SAGEConv/BuckGNN
         hv = self.heavy[ids].sum(0)
-        fwd = Csr(rowptr, col, Nb, Eb, self._plan(rowptr, Nb, Eb, int(hv[0]), int(hv[1])))
-        bwd = Csr(rowptr_t, col_t, Nb, Eb, self._plan(rowptr_t, Nb, Eb, int(hv[2]), int(hv[3])))
+        gf, gb = self._groups(ids, dn, de, ne, Nb, Eb)
+        fwd = Csr(rowptr, col, Nb, Eb, self._plan(rowptr, Nb, Eb, int(hv[0]), int(hv[1])), gf)
+        bwd = Csr(rowptr_t, col_t, Nb, Eb, self._plan(rowptr_t, Nb, Eb, int(hv[2]), int(hv[3])), gb)
         graph = Graph(Nb, Eb, fwd, bwd, perm_t, ei_b, None)
         _graph_cache.put(ei_b, (Nb, self.chunk), graph)
         # pooling segments: graph b owns positions [ptr[b], ptr[b+1])
@@ -217,6 +249,28 @@ class GraphStore:
         seg_b = Csr(self._arange(Nb + 1), batch.to(torch.int32), Nb, Nb, empty)
         _index_cache.put(batch, ("batch",), SegmentIndex(Nb, B, seg_f, seg_b, batch, None))
         return out
+
+    def _groups(self, ids, dn, de, ne, Nb, Eb):
+        """The batch's row-group plans (forward and transpose CSR) from the per-graph plans."""
+        R = self.group_rows
+        if R <= 0 or Nb == 0:
+            return None, None
+        dev = self.device
+        ng = self.n_groups[ids]
+        dg = np.concatenate([[0], np.cumsum(ng)])
+        Gb = int(dg[-1])
+        gt = np.stack([dn[:-1], self.edge_off[ids], de[:-1], ne, self.group_off[ids], dg[:-1], ng], 1)
+        gt_d = torch.from_numpy(np.ascontiguousarray(gt.astype(np.int64))).pin_memory().to(dev, non_blocking=True)
+        out = [torch.empty(max(Eb, 1), dtype=torch.int32, device=dev), torch.empty(max(Eb, 1), dtype=torch.uint8, device=dev),
+               torch.empty(max(Gb, 1), dtype=torch.int32, device=dev),
+               torch.empty(max(Eb, 1), dtype=torch.int32, device=dev), torch.empty(max(Eb, 1), dtype=torch.uint8, device=dev),
+               torch.empty(max(Gb, 1), dtype=torch.int32, device=dev)]
+        grow = torch.empty(Gb + 1, dtype=torch.int32, device=dev)
+        _lib.call("bgnn_store_gather_groups", gt_d.data_ptr(), len(ids), R, Nb, Gb, int(ne.max()), int(ng.max()),
+                  self.gsrc.data_ptr(), self.gmask.data_ptr(), self.gcnt.data_ptr(), self.gsrc_t.data_ptr(),
+                  self.gmask_t.data_ptr(), self.gcnt_t.data_ptr(), *[t.data_ptr() for t in out], grow.data_ptr(),
+                  _stream())
+        return (Groups(out[0], out[1], out[2], R, grow, Gb), Groups(out[3], out[4], out[5], R, grow, Gb))
 
     def _gather_rows(self, table_d, B, per_edge, max_rows, src, n_out):
         out = torch.empty((n_out,) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)

@@ -134,12 +134,150 @@ size_t scan_tmp_bytes(int64_t n) {
     return tmp;
 }
 
-
 }  // namespace
+
+// Row-group plan (bgnn.h, bgnn_group_plan): one wave per group of R consecutive rows, four
+// groups per 256-thread block, all in registers (lane k of register chunk c holds entry
+// 64c+k of the group). The group's light-row entries are concatenated in row order (row t =
+// bit t); an entry's key is (source, occurrence of that source earlier in the same row), so a
+// duplicate edge stays two entries. Keys are numbered by first appearance; each key gets the
+// mask of the rows that hold it. O(n^2 / 64) wave steps for n entries (n ~ 36 on meshes at
+// R = 4). The result depends only on the CSR (deterministic).
+template <int C>   // register chunks: R * chunk <= 64 * C
+__global__ __launch_bounds__(256) void k_group_plan(const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ col, int64_t N, int32_t chunk,
+                                                    int32_t R, const int32_t* __restrict__ grow, int64_t G,
+                                                    int32_t* __restrict__ gsrc, uint8_t* __restrict__ gmask,
+                                                    int32_t* __restrict__ gcnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= G) return;   // whole wave
+    const int64_t r0 = grow ? grow[g] : g * R;
+    const int rows = (int)min((int64_t)R, (grow ? (int64_t)grow[g + 1] : N) - r0);
+    const int32_t rp = lane <= rows ? rowptr[r0 + lane] : 0;
+    const int32_t base = __builtin_amdgcn_readfirstlane(__shfl(rp, 0));
+    // light rows' entry offsets inside the group
+    int off[9], rb[8];
+    off[0] = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        rb[t] = 0;
+        off[t + 1] = off[t];
+        if (t < rows) {
+            const int32_t b = __shfl(rp, t), d = __shfl(rp, t + 1) - b;
+            rb[t] = b;
+            if (d <= chunk) off[t + 1] += d;   // heavy row: chunk / combine kernels
+        }
+    }
+    const int n = off[8];
+    int32_t src[C], row[C], occ[C], fst[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int k = c * 64 + lane;
+        src[c] = -1;
+        row[c] = -1;
+        occ[c] = 0;
+        fst[c] = k;
+        if (k < n) {
+            int t = 0;
+#pragma unroll
+            for (int q = 1; q < 8; ++q) t = (k >= off[q]) ? q : t;   // off is non-decreasing
+            row[c] = t;
+            src[c] = col[rb[t] + (k - off[t])];
+        }
+    }
+    // occurrence of each entry's source earlier in the same row
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci) {
+        const int m = min(64, n - ci * 64);
+        for (int ii = 0; ii < m; ++ii) {
+            const int32_t si = __builtin_amdgcn_readlane(src[ci], ii);
+            const int32_t ti = __builtin_amdgcn_readlane(row[ci], ii);
+            const int i = ci * 64 + ii;
+#pragma unroll
+            for (int c = 0; c < C; ++c) occ[c] += (i < c * 64 + lane && ti == row[c] && si == src[c]) ? 1 : 0;
+        }
+    }
+    // first entry with the same key (same source, same occurrence number)
+#pragma unroll
+    for (int ci = C - 1; ci >= 0; --ci) {
+        const int m = min(64, n - ci * 64);
+        for (int ii = m - 1; ii >= 0; --ii) {   // descending: the last hit is the first entry
+            const int32_t si = __builtin_amdgcn_readlane(src[ci], ii);
+            const int32_t oi = __builtin_amdgcn_readlane(occ[ci], ii);
+            const int i = ci * 64 + ii;
+#pragma unroll
+            for (int c = 0; c < C; ++c) fst[c] = (i < c * 64 + lane && si == src[c] && oi == occ[c]) ? i : fst[c];
+        }
+    }
+    // number the keys by first appearance
+    int ent[C];
+    int cnt = 0;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int k = c * 64 + lane;
+        const bool fresh = k < n && fst[c] == k;
+        const uint64_t bal = __ballot(fresh);
+        ent[c] = cnt + (int)__popcll(bal & ((1ull << lane) - 1ull));
+        cnt += (int)__popcll(bal);
+    }
+    // row mask of each key: OR over the entries whose first entry it is
+    uint32_t msk[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) msk[c] = 0u;
+#pragma unroll
+    for (int ci = 0; ci < C; ++ci) {
+        const int m = min(64, n - ci * 64);
+        for (int ii = 0; ii < m; ++ii) {
+            const int32_t fi = __builtin_amdgcn_readlane(fst[ci], ii);
+            const int32_t ti = __builtin_amdgcn_readlane(row[ci], ii);
+#pragma unroll
+            for (int c = 0; c < C; ++c) msk[c] |= (fi == c * 64 + lane) ? (1u << ti) : 0u;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int k = c * 64 + lane;
+        if (k < n && fst[c] == k) {
+            gsrc[base + ent[c]] = src[c];
+            gmask[base + ent[c]] = (uint8_t)msk[c];
+        }
+    }
+    if (lane == 0) gcnt[g] = cnt;
+}
 
 }  // namespace bgnn
 
 using namespace bgnn;
+
+extern "C" int bgnn_group_plan(const int32_t* rowptr, const int32_t* col, int64_t n_rows, int32_t chunk,
+                               int32_t group_rows, const int32_t* grow, int64_t n_groups, int32_t* gsrc,
+                               uint8_t* gmask, int32_t* gcnt, void* stream) {
+    BGNN_REQUIRE(group_rows >= 1 && group_rows <= 8, "group_plan: group_rows must be in [1, 8]");
+    BGNN_REQUIRE(chunk >= 1 && chunk <= 64, "group_plan: chunk must be in [1, 64]");
+    BGNN_REQUIRE(n_rows >= 0 && n_rows < (int64_t(1) << 31), "group_plan: bad n_rows");
+    const int64_t G = grow ? n_groups : (n_rows + group_rows - 1) / group_rows;
+    BGNN_REQUIRE(G >= 0 && G < (int64_t(1) << 31), "group_plan: bad n_groups");
+    if (n_rows == 0 || G == 0) return BGNN_OK;
+    BGNN_REQUIRE(rowptr && col && gsrc && gmask && gcnt, "group_plan: null pointer");
+    const unsigned blocks = (unsigned)((G + 3) / 4);
+    const int refs = group_rows * chunk;
+    hipStream_t s = as_stream(stream);
+    if (refs <= 64)
+        hipLaunchKernelGGL(k_group_plan<1>, dim3(blocks), dim3(256), 0, s, rowptr, col, n_rows, chunk, group_rows,
+                           grow, G, gsrc, gmask, gcnt);
+    else if (refs <= 128)
+        hipLaunchKernelGGL(k_group_plan<2>, dim3(blocks), dim3(256), 0, s, rowptr, col, n_rows, chunk, group_rows,
+                           grow, G, gsrc, gmask, gcnt);
+    else if (refs <= 256)
+        hipLaunchKernelGGL(k_group_plan<4>, dim3(blocks), dim3(256), 0, s, rowptr, col, n_rows, chunk, group_rows,
+                           grow, G, gsrc, gmask, gcnt);
+    else
+        hipLaunchKernelGGL(k_group_plan<8>, dim3(blocks), dim3(256), 0, s, rowptr, col, n_rows, chunk, group_rows,
+                           grow, G, gsrc, gmask, gcnt);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
 
 extern "C" size_t bgnn_graph_build_ws_bytes(int64_t E, int64_t N) {
     (void)N;

@@ -53,6 +53,13 @@ struct SegArgs {
     int32_t light_slots;
     int32_t nt;         // stream-once data (z_r rows, output rows) with non-temporal hints
     uint32_t* amax;     // plain epilogue: max |out| folded in (f32 bits, atomic max; NULL = off)
+    // row-group plan (bgnn_group_plan): NULL = none
+    const int32_t* gsrc;
+    const uint8_t* gmask;
+    const int32_t* gcnt;
+    const int32_t* grow;    // first row of each group (NULL = g * group_rows)
+    int64_t n_groups;
+    int32_t group_rows;
 };
 
 // fold a lane's running max |out| into *amax: wave max, then one atomic per wave
@@ -686,10 +693,216 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Row-group kernel (SUM / MEAN / MEANT, one full row per lane set, VEC = 4, LPR = 64): the
+// production light-row kernel when the CSR carries a row-group plan (bgnn_group_plan).
+//
+// A wave reduces R consecutive rows at once. The plan lists every distinct source row of the
+// group once, with an R-bit mask of the rows that use it: on a mesh, rows i..i+R-1 share most
+// of their neighbours (i±1, the i±n bands), so a group of 8 fetches ~37 source rows instead of
+// ~71 (cfg2). Each fetched row is added to the accumulators of the rows in its mask (a select
+// per row and column: VALU, hidden under the loads). Groups are swept per XCD like rows in
+// k_seg_sweep. Per row, the entries are summed in plan order (deterministic; for the group's
+// first row it is CSR order), so results match the sweep kernel to rounding, not bitwise.
+template <int NV, int OP, int EPI, int R, int U>
+__global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const Sweep sw = sweep_rows(A.n_groups, wave);
+    int cpos[NV];
+    bool cok[NV];
+    lane_cols<4, NV, 64>(0, lane, A.H, cpos, cok);
+    __shared__ __attribute__((aligned(16))) float red[(EPI == EPI_SAGE) ? 4 : 1][2][(EPI == EPI_SAGE) ? 512 : 4];
+    __shared__ __attribute__((aligned(16))) float sbias[(EPI == EPI_SAGE) ? 512 : 4];
+    if constexpr (EPI == EPI_SAGE) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (cok[v]) {
+                *reinterpret_cast<float4*>(&red[wave][0][cpos[v]]) = make_float4(0.f, 0.f, 0.f, 0.f);
+                *reinterpret_cast<float4*>(&red[wave][1][cpos[v]]) = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        for (int c = threadIdx.x; c < A.H; c += 256) sbias[c] = A.bias[c];
+        __syncthreads();
+    }
+    const int32_t chunk = A.chunk;
+    uint32_t tmax = 0;
+
+    for (int t0 = 0; t0 < sw.T; t0 += 64) {
+        const int ng = min(64, sw.T - t0);
+        // heads of the next 64 groups of this wave: first row, row count, first CSR position
+        // and key count
+        int32_t hr = 0, hn = 0, hb = 0, hc = 0;
+        if (lane < ng) {
+            const int64_t gl = sw.first + (int64_t)sw.W * (t0 + lane);
+            if (A.grow) {
+                hr = A.grow[gl];
+                hn = A.grow[gl + 1] - hr;
+            } else {
+                hr = (int32_t)(gl * R);
+                hn = (int32_t)min((int64_t)R, A.n_rows - hr);
+            }
+            hb = A.rowptr[hr];
+            hc = A.gcnt[gl];
+        }
+        // prefetch of a group: its rows' rowptr (lane t <= R) and its first 64 keys
+        int32_t rp_n, sl_n;
+        uint32_t ml_n;
+        {
+            const int64_t r0 = __builtin_amdgcn_readlane(hr, 0);
+            rp_n = lane <= R ? A.rowptr[min(r0 + lane, A.n_rows)] : 0;
+            const int32_t b = __builtin_amdgcn_readlane(hb, 0), c = __builtin_amdgcn_readlane(hc, 0);
+            sl_n = lane < c ? A.gsrc[b + lane] : 0;
+            ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
+        }
+        for (int k = 0; k < ng; ++k) {
+            const int64_t r0 = __builtin_amdgcn_readlane(hr, k);
+            const int rows = __builtin_amdgcn_readlane(hn, k);
+            const int32_t base = __builtin_amdgcn_readlane(hb, k), cnt = __builtin_amdgcn_readlane(hc, k);
+            const int32_t rp = rp_n, sl0 = sl_n;
+            const uint32_t ml0 = ml_n;
+            if (k + 1 < ng) {
+                const int64_t r1 = __builtin_amdgcn_readlane(hr, k + 1);
+                rp_n = lane <= R ? A.rowptr[min(r1 + lane, A.n_rows)] : 0;
+                const int32_t b = __builtin_amdgcn_readlane(hb, k + 1), c = __builtin_amdgcn_readlane(hc, k + 1);
+                sl_n = lane < c ? A.gsrc[b + lane] : 0;
+                ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
+            }
+            float a[R][NV][4];
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) a[t][v][q] = 0.f;
+            for (int32_t eb = 0; eb < cnt; eb += 64) {
+                const int n = min(64, cnt - eb);
+                int32_t sl = sl0;
+                uint32_t ml = ml0;
+                if (eb > 0) {
+                    sl = lane < n ? A.gsrc[base + eb + lane] : 0;
+                    ml = lane < n ? (uint32_t)A.gmask[base + eb + lane] : 0u;
+                }
+                for (int u0 = 0; u0 < n; u0 += U) {
+                    int32_t j[U];
+                    uint32_t m[U];
+                    float w[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool ok = u0 + u < n;
+                        const int kk = ok ? u0 + u : u0;   // masked slots re-read the first row (L1 hit)
+                        j[u] = __builtin_amdgcn_readlane(sl, kk);
+                        m[u] = ok ? (uint32_t)__builtin_amdgcn_readlane((int)ml, kk) : 0u;
+                        w[u] = 1.f;
+                        if constexpr (OP == OP_MEANT) {
+                            const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
+                            w[u] = inv_deg(d);
+                        }
+                    }
+                    Vec<4> val[U][NV];
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int v = 0; v < NV; ++v)
+                            val[u][v] = ld<4>(A.x + (int64_t)j[u] * A.ldx + (cok[v] ? cpos[v] : 0));
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int t = 0; t < R; ++t) {
+                            const bool on = (m[u] >> t) & 1u;
+#pragma unroll
+                            for (int v = 0; v < NV; ++v)
+#pragma unroll
+                                for (int q = 0; q < 4; ++q) {
+                                    const float x = (OP == OP_MEANT) ? __fmul_rn(val[u][v].f[q], w[u]) : val[u][v].f[q];
+                                    a[t][v][q] += on ? x : 0.f;
+                                }
+                        }
+                }
+            }
+            if constexpr (EPI == EPI_SAGE) {
+                Vec<4> zr[R][NV];
+#pragma unroll
+                for (int t = 0; t < R; ++t) {
+                    const int64_t r = r0 + (t < rows ? t : 0);
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) zr[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
+                }
+#pragma unroll
+                for (int t = 0; t < R; ++t) {
+                    const int64_t r = r0 + t;
+                    const int32_t rb = __builtin_amdgcn_readlane(rp, t);
+                    const int32_t deg = __builtin_amdgcn_readlane(rp, t + 1) - rb;
+                    if (t >= rows || deg > chunk) continue;   // heavy row: chunk + combine
+                    const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
+                    float h[NV][4];
+                    float ss = 0.f;
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        const float4 bv = cok[v] ? *reinterpret_cast<const float4*>(&sbias[cpos[v]])
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            h[v][q] = cok[v] ? sage_h(a[t][v][q], sc, zr[t][v].f[q], bb[q]) : 0.f;
+                            ss = fmaf(h[v][q], h[v][q], ss);
+                        }
+                    }
+                    ss = group_sum(ss, kWave);
+                    const float nr = sqrtf(ss);
+                    const float d = fmaxf(nr, 1e-12f);
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        if (!cok[v]) continue;
+                        Vec<4> o;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) o.f[q] = h[v][q] / d;
+                        st_nt(A.out + r * A.ldo + cpos[v], o);
+                        float4* ps = reinterpret_cast<float4*>(&red[wave][0][cpos[v]]);
+                        float4* pq = reinterpret_cast<float4*>(&red[wave][1][cpos[v]]);
+                        float4 s1 = *ps, s2 = *pq;
+                        s1.x += o.f[0]; s1.y += o.f[1]; s1.z += o.f[2]; s1.w += o.f[3];
+                        s2.x += o.f[0] * o.f[0]; s2.y += o.f[1] * o.f[1];
+                        s2.z += o.f[2] * o.f[2]; s2.w += o.f[3] * o.f[3];
+                        *ps = s1;
+                        *pq = s2;
+                    }
+                    if (lane == 0) A.nrm[r] = nr;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < R; ++t) {
+                    const int64_t r = r0 + t;
+                    const int32_t rb = __builtin_amdgcn_readlane(rp, t);
+                    const int32_t deg = __builtin_amdgcn_readlane(rp, t + 1) - rb;
+                    if (t >= rows || deg > chunk) continue;
+                    Acc<4, NV, OP> acc;
+#pragma unroll
+                    for (int v = 0; v < NV; ++v)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) acc.a[v][q] = a[t][v][q];
+                    store_plain<4, NV, OP>(A, acc, r, deg, cpos, cok, tmax);
+                }
+            }
+        }
+    }
+    if constexpr (EPI == EPI_PLAIN) amax_flush_wave(A.amax, tmax);
+
+    if constexpr (EPI == EPI_SAGE) {
+        __syncthreads();
+        float* dst = A.bn_partial + (int64_t)blockIdx.x * 2 * A.H;
+        for (int c = threadIdx.x; c < A.H; c += 256) {
+            dst[c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+            dst[A.H + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 constexpr int kMaxLightBlocks = 1024;
 
 // Tuning knobs (process-wide; defaults are the production choice; see bgnn_set_tuning).
-static int g_seg_kernel = 0;     // 0 = sweep kernel where applicable, 1 = blocked kernel
+static int g_seg_kernel = 0;     // 0 = auto (row-group kernel where planned, else sweep), 1 = blocked,
+                                 // 2 = sweep
+static int g_grp_blocks = 1024;  // row-group kernel grid (4 blocks of 4 waves per CU)
 static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
 static int g_seg_nt = 1;         // non-temporal hints on stream-once data (default on: +8 % fwd)
 static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto = 12:
@@ -740,13 +953,34 @@ inline int64_t sweep_grid(int64_t n_rows) {
     return blocks < 8 ? 8 : blocks;
 }
 
+inline int64_t group_grid(int64_t G) {
+    int64_t want = (G + 3) / 4;                      // at most one group per wave
+    int64_t blocks = g_grp_blocks;
+    if (want < blocks) blocks = want;
+    blocks = (blocks + 7) / 8 * 8;
+    return blocks < 8 ? 8 : blocks;
+}
+
+// Whether launch_all runs the row-group kernel for this CSR / reduce.
+inline bool use_group(const SegArgs& A, int op, int vec, int lpr) {
+    return g_seg_kernel == 0 && A.gcnt != nullptr && vec == 4 && lpr == 64 && A.chunk <= 64 &&
+           (op == OP_SUM || op == OP_MEAN || op == OP_MEANT);
+}
+
+inline int64_t light_blocks_sage(const SegArgs& A) {
+    return use_group(A, OP_SUM, 4, 64) ? group_grid(A.n_groups) : sweep_grid(A.n_rows);
+}
+
 template <int VEC, int NV, int LPR, int OP, int EPI>
 int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* blocks_out) {
     int64_t rpb = 0;
+    const bool group = use_group(A, OP, VEC, LPR) && ctiles == 1;   // one wave holds a whole row
     // the sweep kernel needs one row per wave and every light row's list in one vector load
-    const bool sweep = (VEC == 4 && LPR == 64 && g_seg_kernel == 0 && A.chunk <= 64);
+    const bool sweep = (VEC == 4 && LPR == 64 && g_seg_kernel != 1 && A.chunk <= 64);
     int64_t blocks;
-    if (sweep || EPI == EPI_SAGE) {   // SAGE: slot count = bgnn_sage_fwd_slots() for either kernel
+    if (group) {
+        blocks = group_grid(A.n_groups);
+    } else if (sweep || EPI == EPI_SAGE) {   // SAGE: slot count = bgnn_sage_fwd_slots() for either kernel
         blocks = sweep_grid(A.n_rows);
         rpb = (A.n_rows + blocks - 1) / blocks;
     } else {
@@ -757,7 +991,17 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     if (blocks_out) *blocks_out = blocks;
     A.light_slots = (int32_t)blocks;
     if (A.n_rows > 0) {
-        if constexpr (VEC == 4 && LPR == 64) {
+        if constexpr (VEC == 4 && LPR == 64 && (OP == OP_SUM || OP == OP_MEAN || OP == OP_MEANT)) {
+            if (group) {
+                if (A.group_rows == 8)
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 8>), dim3((unsigned)blocks), dim3(256), 0, s, A);
+                else
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8>), dim3((unsigned)blocks), dim3(256), 0, s, A);
+                BGNN_CHECK_LAUNCH();
+            }
+        }
+        if (group) {
+        } else if constexpr (VEC == 4 && LPR == 64) {
             if (sweep) {
                 const int u = g_seg_u ? g_seg_u : 12;
                 if (u == 8)
@@ -819,6 +1063,14 @@ inline SegArgs args_from_csr(const bgnn_csr_t* c) {
     A.n_heavy = c->n_heavy;
     A.n_chunks = c->n_chunks;
     A.chunk = c->chunk > 0 ? c->chunk : 0x7fffffff;
+    if (c->gsrc && c->gmask && c->gcnt && (c->group_rows == 4 || c->group_rows == 8)) {
+        A.gsrc = c->gsrc;
+        A.gmask = c->gmask;
+        A.gcnt = c->gcnt;
+        A.group_rows = c->group_rows;
+        A.grow = c->grow;
+        A.n_groups = c->grow ? c->n_groups : (c->n_rows + c->group_rows - 1) / c->group_rows;
+    }
     return A;
 }
 
@@ -881,7 +1133,11 @@ extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, con
     }
 }
 
-extern "C" int32_t bgnn_sage_fwd_slots(int64_t n_rows) { return (int32_t)sweep_grid(n_rows); }
+extern "C" int32_t bgnn_sage_fwd_slots(const bgnn_csr_t* csr) {
+    if (!csr) return -1;
+    const SegArgs A = args_from_csr(csr);
+    return (int32_t)(light_blocks_sage(A) + (csr->n_chunks > 0 ? csr->n_heavy : 0));
+}
 
 extern "C" int32_t bgnn_get_tuning(int32_t knob) {
     switch (knob) {
@@ -891,6 +1147,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_SEG_NT: return g_seg_nt;
         case BGNN_TUNE_GEMM_MODE: return gemm_mode();
         case BGNN_TUNE_ROWS_NT: return rows_nt();
+        case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
         default: return -1;
     }
 }
@@ -898,7 +1155,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
 extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
     switch (knob) {
         case BGNN_TUNE_SEG_KERNEL:
-            BGNN_REQUIRE(value == 0 || value == 1, "set_tuning: kernel must be 0 (sweep) or 1 (blocked)");
+            BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: kernel must be 0 (auto), 1 (blocked) or 2 (sweep)");
             g_seg_kernel = value;
             return BGNN_OK;
         case BGNN_TUNE_SEG_BLOCKS:
@@ -911,6 +1168,10 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             g_seg_u = value;
             return BGNN_OK;
         case BGNN_TUNE_SEG_NT: g_seg_nt = value ? 1 : 0; return BGNN_OK;
+        case BGNN_TUNE_GROUP_BLOCKS:
+            BGNN_REQUIRE(value >= 8 && value <= 65536, "set_tuning: group blocks out of range");
+            g_grp_blocks = value;
+            return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: gemm mode must be 0 (f32), 1 (bf16x6) or 2 (f16x3)");

@@ -58,6 +58,37 @@ __global__ __launch_bounds__(256) void k_store_graph(const int64_t* __restrict__
     }
 }
 
+// row-group plans: gtable[b] = {dst_node, src_edge, dst_edge, n_edges, src_group, dst_group, n_groups}
+__global__ __launch_bounds__(256) void k_store_groups(const int64_t* __restrict__ gtable, int B, int R, int64_t Nb,
+                                                      int64_t Gb, const int32_t* __restrict__ gsrc,
+                                                      const uint8_t* __restrict__ gmask,
+                                                      const int32_t* __restrict__ gcnt,
+                                                      const int32_t* __restrict__ gsrc_t,
+                                                      const uint8_t* __restrict__ gmask_t,
+                                                      const int32_t* __restrict__ gcnt_t, int32_t* __restrict__ gsrc_o,
+                                                      uint8_t* __restrict__ gmask_o, int32_t* __restrict__ gcnt_o,
+                                                      int32_t* __restrict__ gsrc_t_o, uint8_t* __restrict__ gmask_t_o,
+                                                      int32_t* __restrict__ gcnt_t_o, int32_t* __restrict__ grow_o) {
+    const int b = blockIdx.y;
+    const int64_t* t = gtable + 7 * (int64_t)b;
+    const int64_t dn = t[0], se = t[1], de = t[2], ne = t[3], sg = t[4], dg = t[5], ng = t[6];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // positions past a group's keys hold unwritten values: rebased too, never read
+    for (int64_t e = t0; e < ne; e += stride) {
+        gsrc_o[de + e] = (int32_t)((uint32_t)gsrc[se + e] + (uint32_t)dn);
+        gsrc_t_o[de + e] = (int32_t)((uint32_t)gsrc_t[se + e] + (uint32_t)dn);
+        gmask_o[de + e] = gmask[se + e];
+        gmask_t_o[de + e] = gmask_t[se + e];
+    }
+    for (int64_t k = t0; k < ng; k += stride) {
+        gcnt_o[dg + k] = gcnt[sg + k];
+        gcnt_t_o[dg + k] = gcnt_t[sg + k];
+        grow_o[dg + k] = (int32_t)(dn + k * R);
+    }
+    if (b == B - 1 && t0 == 0) grow_o[Gb] = (int32_t)Nb;
+}
+
 // copy the node (or edge) rows of each graph: a contiguous block per graph
 __global__ __launch_bounds__(256) void k_store_rows16(const int64_t* __restrict__ table, int per_edge,
                                                       const uint4* __restrict__ src, int64_t row_vec,
@@ -113,6 +144,26 @@ extern "C" int bgnn_store_gather_graph(const int64_t* table, int32_t B, int64_t 
     hipLaunchKernelGGL(k_store_graph, dim3(blocks_for(work, B), B), dim3(256), 0, s, table, B, Nb, Eb, ei, ld_ei,
                        rowptr, col, rowptr_t, col_t, perm_t, ei_out, rowptr_out, col_out, rowptr_t_out, col_t_out,
                        perm_t_out, batch_out);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_store_gather_groups(const int64_t* gtable, int32_t B, int32_t group_rows, int64_t Nb, int64_t Gb,
+                                        int64_t max_edges, int64_t max_groups, const int32_t* gsrc,
+                                        const uint8_t* gmask, const int32_t* gcnt, const int32_t* gsrc_t,
+                                        const uint8_t* gmask_t, const int32_t* gcnt_t, int32_t* gsrc_out,
+                                        uint8_t* gmask_out, int32_t* gcnt_out, int32_t* gsrc_t_out,
+                                        uint8_t* gmask_t_out, int32_t* gcnt_t_out, int32_t* grow_out, void* stream) {
+    BGNN_REQUIRE(B > 0 && B <= 65535, "store_gather_groups: batch of %d graphs unsupported", B);
+    BGNN_REQUIRE(group_rows >= 1 && group_rows <= 8, "store_gather_groups: group_rows must be in [1, 8]");
+    BGNN_REQUIRE(gtable && gcnt && gcnt_t && gcnt_out && gcnt_t_out && grow_out, "store_gather_groups: null");
+    BGNN_REQUIRE(max_edges == 0 || (gsrc && gmask && gsrc_t && gmask_t && gsrc_out && gmask_out && gsrc_t_out &&
+                                    gmask_t_out),
+                 "store_gather_groups: null edge arrays");
+    const int64_t work = max_edges > max_groups ? max_edges : max_groups;
+    hipLaunchKernelGGL(k_store_groups, dim3(blocks_for(work, B), B), dim3(256), 0, as_stream(stream), gtable, B,
+                       group_rows, Nb, Gb, gsrc, gmask, gcnt, gsrc_t, gmask_t, gcnt_t, gsrc_out, gmask_out, gcnt_out,
+                       gsrc_t_out, gmask_t_out, gcnt_t_out, grow_out);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 2
+#define BGNN_ABI_VERSION 3
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -60,12 +60,15 @@ const char* bgnn_last_error_string(void);
 /* Process-wide tuning knobs for A/B measurement (tools/, tests). The defaults are
  * the production choice; results are identical for every setting, only speed
  * changes. Not thread-safe against concurrent launches. */
-#define BGNN_TUNE_SEG_KERNEL 1   /* 0 = XCD-sweep light-row kernel (default), 1 = blocked */
+#define BGNN_TUNE_SEG_KERNEL 1   /* light rows: 0 = auto (row-group kernel where the CSR has a
+                                    row-group plan and the reduce is sum/mean, else the XCD
+                                    sweep), 1 = blocked, 2 = XCD sweep                       */
 #define BGNN_TUNE_SEG_BLOCKS 2   /* sweep grid in blocks (default 1024)                   */
 #define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (12), 8, 12, 16  */
 #define BGNN_TUNE_SEG_NT 4       /* non-temporal hints on stream-once rows (default 1)       */
 #define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (default) */
 #define BGNN_TUNE_ROWS_NT 6      /* non-temporal stores in sage_apply / sage_bwd_rows (0/1)   */
+#define BGNN_TUNE_GROUP_BLOCKS 7 /* row-group kernel grid in blocks (default 1024)            */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);
@@ -88,6 +91,16 @@ typedef struct bgnn_csr {
     int32_t n_chunks;
     int32_t chunk;               /* edges per chunk; rows with deg > chunk are heavy */
     int32_t _pad;
+    /* Optional row-group plan (bgnn_group_plan; all NULL / 0 = none). Used by the sum/mean
+     * aggregation kernels: a wave reduces up to `group_rows` consecutive rows and fetches each
+     * distinct source row of the group once. */
+    const int32_t* gsrc;         /* [nnz]                                      */
+    const uint8_t* gmask;        /* [nnz]                                      */
+    const int32_t* gcnt;         /* [n_groups]                                 */
+    const int32_t* grow;         /* [n_groups + 1] first row of each group; NULL = g * group_rows */
+    int64_t n_groups;            /* with grow; else ceil(n_rows / group_rows)  */
+    int32_t group_rows;
+    int32_t _pad2;
 } bgnn_csr_t;
 
 /* Workspace for bgnn_graph_build (bytes). */
@@ -122,6 +135,19 @@ int bgnn_heavy_plan(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t 
                     int32_t* heavy_row, int32_t* heavy_chunk0, int32_t* chunk_heavy,
                     int32_t* dev_counts, void* ws, size_t ws_bytes, void* stream);
 
+/* Row-group plan of a CSR (R = group_rows <= 8, chunk <= 64). Group g = rows
+ * [grow[g], grow[g+1]) (at most R rows; grow = NULL: rows [g*R, g*R+R), n_groups =
+ * ceil(n_rows / R)). For each group: the light rows' (deg <= chunk) entries, concatenated in
+ * row order, keyed by (source, occurrence of that source earlier in the same row) -- a
+ * duplicate edge stays two keys -- numbered by first appearance; with r0 = the group's first
+ * row, gsrc[rowptr[r0] + k] = source of key k and gmask[rowptr[r0] + k] = bit t set iff row
+ * r0+t holds key k, for k < gcnt[g]. Each row's entries then appear in key order (the row's
+ * own CSR order for the group's first row). gsrc / gmask have nnz elements (only each group's
+ * own CSR range is written), gcnt n_groups. Deterministic, asynchronous, one wave per group. */
+int bgnn_group_plan(const int32_t* rowptr, const int32_t* col, int64_t n_rows, int32_t chunk,
+                    int32_t group_rows, const int32_t* grow, int64_t n_groups,
+                    int32_t* gsrc, uint8_t* gmask, int32_t* gcnt, void* stream);
+
 /* ------------------------------------------------------------------------
  * Generic segment reduce (SpMM with a 0/1 or 1/deg matrix):
  *   out[r, :] = REDUCE_{e in row r} x[col[e], :]
@@ -154,9 +180,10 @@ int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t*
  *   o_i = h_i / max(||h_i||_2, 1e-12)        (SAGEConv normalize=True)
  *   BatchNorm statistics of o (train mode) as per-block partial sums.
  * Outputs: o [N, H], nrm [N] = ||h_i||, bn_partial [n_slots, 2, H] with
- *   n_slots = bgnn_sage_fwd_slots(N) + n_heavy.
+ *   n_slots = bgnn_sage_fwd_slots(csr) (light-row blocks of the kernel that will run, plus
+ *   one slot per heavy row).
  * ---------------------------------------------------------------------- */
-int32_t bgnn_sage_fwd_slots(int64_t n_rows);
+int32_t bgnn_sage_fwd_slots(const bgnn_csr_t* csr);
 int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldzl, const float* zr, int64_t ldzr,
                   const float* bias, int32_t H, int32_t reduce, float* o, float* nrm,
                   float* bn_partial, float* partial, void* stream);
@@ -302,6 +329,19 @@ int bgnn_store_gather_graph(const int64_t* table, int32_t B, int64_t Nb, int64_t
                             int64_t* edge_index_out, int32_t* rowptr_out, int32_t* col_out,
                             int32_t* rowptr_t_out, int32_t* col_t_out, int32_t* perm_t_out,
                             int64_t* batch_out, void* stream);
+/* Row-group plans of the batch from per-graph plans (groups aligned to graph starts, built
+ * once by bgnn_group_plan with grow): gtable device int64 [B][7] = {dst_node, src_edge,
+ * dst_edge, n_edges, src_group, dst_group, n_groups} per batch graph. Copies gsrc (+dst_node),
+ * gmask over each graph's edge range and gcnt over its groups, for the forward and the
+ * transpose CSR, and writes the batch's grow[G+1] (graph b's group k starts at
+ * dst_node + k * group_rows; grow[G] = Nb). */
+int bgnn_store_gather_groups(const int64_t* gtable, int32_t B, int32_t group_rows, int64_t Nb, int64_t Gb,
+                             int64_t max_edges, int64_t max_groups,
+                             const int32_t* gsrc, const uint8_t* gmask, const int32_t* gcnt,
+                             const int32_t* gsrc_t, const uint8_t* gmask_t, const int32_t* gcnt_t,
+                             int32_t* gsrc_out, uint8_t* gmask_out, int32_t* gcnt_out,
+                             int32_t* gsrc_t_out, uint8_t* gmask_t_out, int32_t* gcnt_t_out,
+                             int32_t* grow_out, void* stream);
 /* Copy each batch graph's node rows (per_edge = 0) or edge rows (per_edge = 1) of a
  * row-major store array (row_bytes per row, a multiple of 4) into the batch array. */
 int bgnn_store_gather_rows(const int64_t* table, int32_t B, int32_t per_edge, int64_t max_rows,

@@ -17,6 +17,52 @@ def np_csr(keys, vals, n):
     return np.cumsum(rowptr), vals[order], order
 
 
+def np_groups(rowptr, col, n, chunk, R, grow=None):
+    """Host restatement of bgnn_group_plan's rule (include/bgnn.h): per group of at most R rows
+    (rows [g*R, g*R+R), or [grow[g], grow[g+1])), the light rows' entries keyed by (source,
+    occurrence within the row), numbered by first appearance, with the mask of the rows holding
+    each key."""
+    if grow is None:
+        grow = list(range(0, n, R)) + [n]
+    G = len(grow) - 1
+    gsrc, gmask, gcnt = {}, {}, np.zeros(G, dtype=np.int64)
+    for g in range(G):
+        keys, src, mask = {}, [], []
+        for t in range(grow[g + 1] - grow[g]):
+            r = grow[g] + t
+            b, e = int(rowptr[r]), int(rowptr[r + 1])
+            if e - b > chunk:
+                continue
+            occ = {}
+            for q in range(b, e):
+                s_ = int(col[q])
+                k = (s_, occ.get(s_, 0))
+                occ[s_] = k[1] + 1
+                if k not in keys:
+                    keys[k] = len(src)
+                    src.append(s_)
+                    mask.append(0)
+                mask[keys[k]] |= 1 << t
+        base = int(rowptr[grow[g]])
+        for i, (s_, m) in enumerate(zip(src, mask)):
+            gsrc[base + i], gmask[base + i] = s_, m
+        gcnt[g] = len(src)
+    return gsrc, gmask, gcnt
+
+
+def check_groups(csr, n, chunk):
+    gr = csr.groups
+    if gr is None:
+        return
+    rp, col = csr.rowptr.cpu().numpy(), csr.col.cpu().numpy()
+    grow = gr.grow.cpu().tolist() if gr.grow is not None else None
+    gsrc, gmask, gcnt = np_groups(rp, col, n, chunk, gr.rows, grow)
+    assert np.array_equal(gr.gcnt.cpu().numpy(), gcnt)
+    got_s, got_m = gr.gsrc.cpu().numpy(), gr.gmask.cpu().numpy()
+    for pos, s_ in gsrc.items():
+        assert got_s[pos] == s_ and got_m[pos] == gmask[pos], pos
+
+
 def check_graph(ei_np, n, dev, chunk=64):
     ei = torch.from_numpy(ei_np).to(dev)
     g = Graph.build(ei, n, chunk=chunk)
@@ -40,6 +86,9 @@ def check_graph(ei_np, n, dev, chunk=64):
     assert p.n_chunks == int(nch.sum())
     c0 = np.concatenate([[0], np.cumsum(nch)])
     assert np.array_equal(p.heavy_chunk0[:len(heavy) + 1].cpu().numpy(), c0)
+    # row-group plans of both CSRs
+    check_groups(g.fwd, n, chunk)
+    check_groups(g.bwd, n, chunk)
     return g
 
 
@@ -78,3 +127,36 @@ def test_segment_index_unsorted(dev):
     rp, col, _ = np_csr(idx, np.arange(len(idx)), 6)
     assert np.array_equal(s.fwd.rowptr.cpu().numpy(), rp)
     assert np.array_equal(s.fwd.col[:len(idx)].cpu().numpy(), col)
+
+
+@pytest.mark.parametrize("rows", [4, 8])
+def test_group_plan_meshes(dev, rows):
+    from bgnn import graph as G
+    old = G.GROUP_ROWS
+    G.GROUP_ROWS = rows
+    try:
+        b = S.make_batch(23, 3)
+        g = check_graph(b.edge_index.numpy(), b.num_nodes, dev)
+        assert g.fwd.groups is not None and g.fwd.groups.rows == rows
+        # fewer fetched source rows than edges (neighbours shared inside a group)
+        assert int(g.fwd.groups.gcnt.sum()) < 0.75 * b.num_edges
+    finally:
+        G.GROUP_ROWS = old
+
+
+def test_group_plan_explicit_group_starts(dev):
+    """bgnn_group_plan with caller-given group starts (groups of 1..R rows, as the GraphStore
+    uses to align groups with graph starts), against the host restatement."""
+    from bgnn.graph import Csr, enqueue_groups
+    rng = np.random.default_rng(7)
+    n, E, R = 500, 6000, 8
+    ei = rng.integers(0, n, size=(2, E))
+    ei[:, :40] = ei[:, 40:80]                  # duplicate edges
+    g = Graph.build(torch.from_numpy(ei).to(dev), n, chunk=32)
+    sizes = rng.integers(1, R + 1, size=n)
+    starts = np.concatenate([[0], np.cumsum(sizes)])
+    grow = starts[starts < n].tolist() + [n]
+    grow_d = torch.tensor(grow, dtype=torch.int32, device=dev)
+    for csr in (g.fwd, g.bwd):
+        gr = enqueue_groups(csr.rowptr, csr.col, n, E, 32, R, grow_d, len(grow) - 1)
+        check_groups(Csr(csr.rowptr, csr.col, n, E, csr.plan, gr), n, 32)

@@ -1,6 +1,6 @@
 """GPU: the inference driver (bgnn.evaluate, INFERENCE.py's buckling metrics) over
-host-collated batches and GraphStore batches gives identical predictions and the
-metrics of a direct computation."""
+host-collated batches and GraphStore batches gives the same predictions (to fp32 rounding:
+the two paths group aggregation rows differently) and the metrics of a direct computation."""
 import numpy as np
 import pytest
 import torch
@@ -21,7 +21,7 @@ def test_evaluate_matches_direct_computation(dev):
     r1 = bgnn.evaluate(model, host, scaler, device=dev)
     store = bgnn.GraphStore(gs, dev)
     r2 = bgnn.evaluate(model, store.loader(4), scaler)
-    assert torch.equal(r1["predictions"], r2["predictions"])
+    torch.testing.assert_close(r1["predictions"], r2["predictions"], rtol=1e-5, atol=1e-6)
     assert r1["graphs"] == r2["graphs"] == 6
     # direct: eval forward, denormalise, |(true - pred) / true| in percent
     model.eval()

@@ -125,43 +125,46 @@ def test_full_size_cfg3_properties(dev):
         torch.testing.assert_close(ax[r].double(), ref, rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("knobs", [(1, 0), (0, 8), (0, 12), (0, 16)],
+def _variant_graph(dev, graph):
+    if graph == "mesh_super":
+        b = S.make_batch(25, 3, super_node=True)
+        return b.edge_index.to(dev), b.num_nodes
+    n = 3000
+    gen = torch.Generator().manual_seed(11)
+    return torch.randint(0, n, (2, 24 * n), generator=gen).to(dev), n
+
+
+def _run_all_reduces(g, x, gy):
+    out = {}
+    for r in ("sum", "mean", "max"):
+        xx = x.clone().requires_grad_(True)
+        y = bgnn.aggregate(xx, g, r)
+        y.backward(gy)
+        out[r] = (y.detach(), xx.grad)
+    return out
+
+
+@pytest.mark.parametrize("knobs", [(1, 0), (2, 8), (2, 12), (2, 16)],
                          ids=["blocked", "sweep8", "sweep12", "sweep16"])
 @pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
 def test_kernel_variants_bit_identical(dev, knobs, graph):
-    """Every light-row kernel variant (tuning knobs) gives bit-identical aggregation results,
-    forward and transpose (backward), on meshes with super nodes and on a dense random graph."""
+    """The per-row light-row kernels (blocked, XCD sweep with U = 8/12/16 neighbours per batch)
+    give bit-identical aggregation results, forward and transpose (backward), on meshes with
+    super nodes and on a dense random graph."""
     from bgnn import _lib
-    if graph == "mesh_super":
-        b = S.make_batch(25, 3, super_node=True)
-        ei, n = b.edge_index.to(dev), b.num_nodes
-    else:
-        n = 3000
-        gen = torch.Generator().manual_seed(11)
-        ei = torch.randint(0, n, (2, 24 * n), generator=gen).to(dev)
+    ei, n = _variant_graph(dev, graph)
     g = Graph.build(ei, n)
     torch.manual_seed(3)
     x = torch.randn(n, 512, device=dev)
     gy = torch.randn(n, 512, device=dev)
-
-    def run():
-        out = {}
-        for r in ("sum", "mean", "max"):
-            xx = x.clone().requires_grad_(True)
-            y = bgnn.aggregate(xx, g, r)
-            y.backward(gy)
-            out[r] = (y.detach(), xx.grad)
-        return out
-
     old = (_lib.query("bgnn_get_tuning", 1), _lib.query("bgnn_get_tuning", 3))
-    ref = None
     try:
-        _lib.call("bgnn_set_tuning", 1, 0)
+        _lib.call("bgnn_set_tuning", 1, 2)
         _lib.call("bgnn_set_tuning", 3, 8)
-        ref = run()
+        ref = _run_all_reduces(g, x, gy)
         _lib.call("bgnn_set_tuning", 1, knobs[0])
         _lib.call("bgnn_set_tuning", 3, knobs[1])
-        got = run()
+        got = _run_all_reduces(g, x, gy)
         for r in ("sum", "mean", "max"):
             assert torch.equal(got[r][0], ref[r][0]), (r, "fwd")
             assert torch.equal(got[r][1], ref[r][1]), (r, "bwd")
@@ -170,7 +173,43 @@ def test_kernel_variants_bit_identical(dev, knobs, graph):
         _lib.call("bgnn_set_tuning", 3, old[1])
 
 
-@pytest.mark.parametrize("kernel", [0, 1], ids=["sweep", "blocked"])
+@pytest.mark.parametrize("rows", [4, 8])
+@pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
+def test_group_kernel_matches_sweep(dev, rows, graph):
+    """The row-group kernel (default for sum/mean with a row-group plan) sums each row's entries
+    in plan order: equal to the per-row sweep kernel to fp32 rounding, deterministic run to run,
+    and the first row of every group is bit-identical (plan order = CSR order there)."""
+    from bgnn import _lib
+    from bgnn import graph as Gm
+    ei, n = _variant_graph(dev, graph)
+    old_rows = Gm.GROUP_ROWS
+    Gm.GROUP_ROWS = rows
+    try:
+        g = Graph.build(ei, n)
+    finally:
+        Gm.GROUP_ROWS = old_rows
+    assert g.fwd.groups is not None and g.bwd.groups is not None
+    torch.manual_seed(5)
+    x = torch.randn(n, 512, device=dev)
+    gy = torch.randn(n, 512, device=dev)
+    old = _lib.query("bgnn_get_tuning", 1)
+    try:
+        _lib.call("bgnn_set_tuning", 1, 2)
+        ref = _run_all_reduces(g, x, gy)
+        _lib.call("bgnn_set_tuning", 1, 0)
+        got = _run_all_reduces(g, x, gy)
+        again = _run_all_reduces(g, x, gy)
+    finally:
+        _lib.call("bgnn_set_tuning", 1, old)
+    first = torch.arange(0, n, rows, device=dev)
+    for r in ("sum", "mean", "max"):
+        for k in (0, 1):
+            assert torch.equal(got[r][k], again[r][k]), (r, k)
+            torch.testing.assert_close(got[r][k], ref[r][k], rtol=1e-5, atol=1e-5)
+        assert torch.equal(got[r][0][first], ref[r][0][first]), r
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2], ids=["group", "blocked", "sweep"])
 @pytest.mark.parametrize("reduce", [0, 1])
 def test_spmm_bwd_folds_max_abs(dev, kernel, reduce):
     """bgnn_spmm_bwd's optional amax output is max |gx| over light rows and the super-node

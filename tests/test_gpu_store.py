@@ -41,6 +41,24 @@ def csr_equal(a, b):
     assert torch.equal(a.plan.chunk_heavy[:nc], b.plan.chunk_heavy[:nc])
 
 
+def groups_equal(a, b, rowptr):
+    """Same row-group plan: same group starts, counts and keys in every group's range."""
+    assert (a is None) == (b is None)
+    if b is None:
+        return
+    assert a.n_groups == b.n_groups and a.rows == b.rows
+    assert torch.equal(a.gcnt[:b.n_groups], b.gcnt[:b.n_groups])
+    if b.grow is not None:
+        assert torch.equal(a.grow, b.grow)
+    rp, cnt = rowptr.cpu(), b.gcnt.cpu()
+    starts = b.grow.cpu() if b.grow is not None else torch.arange(b.n_groups) * b.rows
+    for g in range(b.n_groups):
+        lo = int(rp[int(starts[g])])
+        hi = lo + int(cnt[g])
+        assert torch.equal(a.gsrc[lo:hi], b.gsrc[lo:hi])
+        assert torch.equal(a.gmask[lo:hi], b.gmask[lo:hi])
+
+
 @pytest.mark.parametrize("ids", [[0, 1, 2, 3, 4, 5, 6, 7, 8], [6, 2, 2, 8, 0], [7], [5, 7, 3]])
 def test_store_batch_matches_host_collation(dev, ids):
     gs = dataset()
@@ -57,6 +75,17 @@ def test_store_batch_matches_host_collation(dev, ids):
     csr_equal(g.fwd, r.fwd)
     csr_equal(g.bwd, r.bwd)
     assert torch.equal(g.perm_t[:r.num_edges], r.perm_t[:r.num_edges])
+    # row-group plans: groups start at every graph's first node; the gathered per-graph plans
+    # equal a plan built on the collated CSR with the same group starts
+    from bgnn.graph import enqueue_groups
+    gf = g.fwd.groups
+    assert gf is not None and gf.grow is not None
+    R, ptr = gf.rows, ref.ptr.cpu().tolist()
+    want = [p + k * R for p, q in zip(ptr[:-1], ptr[1:]) for k in range((q - p + R - 1) // R)] + [ptr[-1]]
+    assert gf.grow.cpu().tolist() == want
+    for mine, csr in ((g.fwd, r.fwd), (g.bwd, r.bwd)):
+        want_g = enqueue_groups(csr.rowptr, csr.col, r.num_nodes, r.num_edges, 16, R, gf.grow, gf.n_groups)
+        groups_equal(mine.groups, want_g, csr.rowptr)
     seg = _index_cache.peek(b.batch, ("batch",))
     rs = SegmentIndex.build(ref.batch, len(ids), chunk=16)
     csr_equal(seg.fwd, rs.fwd)
@@ -89,6 +118,11 @@ def test_store_rejects_bad_ids(dev):
 
 @pytest.mark.parametrize("super_node", [False, True])
 def test_train_step_on_store_batch_equals_host_batch(dev, super_node):
+    """A train step on a store batch equals one on the host-collated batch. The graph structure is
+    bit-identical; the row-group plans start groups at graph starts on the store path and every
+    R rows on the host path, so the aggregation sums in a different order: loss and gradients
+    agree to fp32 rounding (compared before the optimizer update, whose first Adam step would
+    amplify sign flips of near-zero gradients)."""
     gs = [S.make_mesh_graph(20, seed=s, super_node=super_node) for s in range(4)]
     store = bgnn.GraphStore(gs, dev)
     results = []
@@ -97,10 +131,18 @@ def test_train_step_on_store_batch_equals_host_batch(dev, super_node):
         torch.manual_seed(0)
         model = bgnn.BuckGNN(16, 5, hidden_channels=128, num_layers=6, dropout_rate=0.0,
                              model_name="GraphSage_addAggr").to(dev).train()
-        opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8)
+
+        class NoStep:
+            def zero_grad(self, set_to_none=True):
+                model.zero_grad(set_to_none=set_to_none)
+
+            def step(self):
+                pass
+
         batch = store.batch([0, 1, 2, 3]) if use_store else Batch.from_data_list(gs).to(dev)
-        loss = bgnn.train_step(model, batch, opt, bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5))
-        results.append((float(loss), [p.detach().clone() for p in model.parameters()]))
-    assert results[0][0] == results[1][0]
+        loss = bgnn.train_step(model, batch, NoStep(), bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5))
+        results.append((float(loss), [p.grad.detach().clone() for p in model.parameters() if p.grad is not None]))
+    assert results[0][0] == pytest.approx(results[1][0], rel=1e-5)
+    assert len(results[0][1]) == len(results[1][1])
     for a, b in zip(results[0][1], results[1][1]):
-        assert torch.equal(a, b)
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()) + 1e-12)

@@ -68,7 +68,18 @@ def test_size_queries_need_no_gpu():
     from bgnn import _lib
 
     assert _lib.query("bgnn_graph_build_ws_bytes", 1000, 100) > 0
-    assert _lib.query("bgnn_sage_fwd_slots", 80656) == 1024
+    # light-row blocks of the kernel that will run + one slot per heavy row
+    def csr(n_rows, nnz, n_heavy, n_chunks, group_rows=0, n_groups=0, grow=None):
+        plan = 1 if group_rows else None
+        return _lib.CsrStruct(rowptr=1, col=1, heavy_row=1, heavy_chunk0=1, chunk_heavy=1, n_rows=n_rows, nnz=nnz,
+                              n_heavy=n_heavy, n_chunks=n_chunks, chunk=64, gsrc=plan, gmask=plan, gcnt=plan,
+                              grow=grow, n_groups=n_groups, group_rows=group_rows)
+
+    q = lambda c: _lib.query("bgnn_sage_fwd_slots", ctypes.byref(c))   # noqa: E731
+    assert q(csr(80656, 715872, 0, 0)) == 1024                       # sweep kernel: 1024 blocks
+    assert q(csr(80672, 792992, 16, 1264, group_rows=4)) == 1024 + 16   # row-group kernel + heavy rows
+    assert q(csr(1000, 8000, 0, 0, group_rows=4)) == 64              # 250 groups, one per wave
+    assert q(csr(1000, 8000, 0, 0, group_rows=4, n_groups=40, grow=1)) == 16   # explicit group starts
     # f16x3 (default): a 256-B head for the operand maxima, plus split-K slabs where used
     assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 256    # forward: no split-K
     assert _lib.query("bgnn_gemm_ws_bytes", 1024, 512, 80656, 1, 0) > 256     # wgrad: split-K

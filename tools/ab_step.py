@@ -30,7 +30,7 @@ def apply(setting):
 
 def main():
     settings = sys.argv[1:] or ["bgnn.fused.GEMM_BACKEND='hip'"]
-    rounds, steps = 5, 8
+    rounds, steps = int(os.environ.get("AB_ROUNDS", "5")), 8
     dev = torch.device("cuda", 0)
     batch = synthetic.make_config_batch(os.environ.get("AB_CONFIG", "cfg2")).to(dev)
     torch.manual_seed(0)
@@ -39,8 +39,11 @@ def main():
     opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8, fused=True)
     crit, norm = bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5)
 
+    clear = os.environ.get("AB_CLEAR", "1") == "1"   # 0: keep the graph structure cached
+
     def step():
-        bgnn.clear_caches()
+        if clear:
+            bgnn.clear_caches()
         bgnn.train_step(model, batch, opt, crit, norm)
 
     res = {s: [] for s in settings}
