@@ -45,8 +45,18 @@ FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.m
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md)
 X6_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6   # f32-equivalent ceiling of the 6-product bf16 split GEMM
 H3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 3   # f32-equivalent ceiling of the 3-product f16 split GEMM (f16 = bf16 rate)
-TRAFFIC_FILE = "traffic_r01.json"
-METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"
+TRAFFIC_FILE = "traffic_r02.json"
+METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"   # BASELINE.json
+
+
+def metric_name(model: str, bsz: int) -> str:
+    """BASELINE.json's metric for the SAGE models at batch 16; EA_GNN (configs[4]) is named for
+    what it measures."""
+    if model.startswith("EA_GNN"):
+        return f"graphs/sec (fwd+bwd) 6-block {model} (GraphNetBlock) h=512, ~5k-node meshes, batch {bsz}"
+    if bsz == 16:
+        return METRIC
+    return f"graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch {bsz}"
 
 
 def parse():
@@ -67,6 +77,9 @@ def parse():
                          "step; host: the same batches as store collated on the host (PyG DataLoader path of "
                          "the reference) and copied to the GPU inside the step")
     ap.add_argument("--store-graphs", type=int, default=256)
+    ap.add_argument("--lr", type=float, default=None,
+                    help="Adam learning rate (default 1e-2, TRAIN_FINAL.py:37; EA_GNN 1e-3: at 1e-2 the h=512 "
+                         "EA_GNN diverges in the reference too, tests/test_gpu_ea_train.py)")
     ap.add_argument("--bf16", action="store_true",
                     help="EA_GNN only: bf16 GEMM operands with f32 accumulation (BASELINE configs[4])")
     return ap.parse_args()
@@ -122,10 +135,12 @@ def main():
     state0 = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
     model.ea_bf16 = bool(args.bf16)
+    is_ea = args.model.startswith("EA_GNN")
+    lr = args.lr if args.lr is not None else (1e-3 if is_ea else 1e-2)
     try:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8, fused=True)
+        opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-8, fused=True)
     except (RuntimeError, TypeError):
-        opt = torch.optim.Adam(model.parameters(), lr=1e-2, weight_decay=1e-8)
+        opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-8)
     crit = bgnn.RelativeErrorLoss()
     norm = bgnn.EigenvalueScaler(center=1.0, scale=0.5)
     ar = bgnn.GradAllReduce(model) if world > 1 else None
@@ -188,7 +203,15 @@ def main():
     N, E, H = batch.num_nodes, batch.num_edges, 512
     agg_ms = avg_ms("sage_fwd")
     agg_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
-    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9   # NaN when the model has no SAGE layer (EA_GNN)
+    agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
+    # transpose aggregation (bgnn_spmm_bwd): SURVEY.md §8d's per-layer aggregation bytes
+    bwd_ms = avg_ms("spmm_bwd")
+    bwd_bytes = 2 * N * H * 4 + 4 * E + 4 * (N + 1)
+    bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
+    seg_kernel = _lib.query("bgnn_get_tuning", 1)
+    from bgnn import graph as _graph
+    agg_name = "k_seg_group<2,0,{e},4,8> (row groups of 4, deduplicated source rows)" if (
+        seg_kernel == 0 and _graph.GROUP_ROWS == 4) else "k_seg_sweep<2,0,{e},12>"
     traffic = {}
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     if os.path.exists(tpath):
@@ -208,7 +231,7 @@ def main():
     gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
     graphs = bsz * world * args.steps
     out = {
-        "metric": METRIC,
+        "metric": metric_name(args.model, bsz),
         "value": round(graphs / elapsed, 3),
         "unit": "graphs/s",
         "n_gpus": world,
@@ -254,7 +277,8 @@ def main():
             "launches": len(timers.get("gemm_fwd", [])),
         },
         "roofline_hbm": {
-            "kernel": "bgnn_sage_fwd (k_seg_sweep<2,0,1,8>, SAGE epilogue [+chunk/combine for super nodes])",
+            "kernel": "bgnn_sage_fwd: " + agg_name.format(e=1)
+                      + ", SAGE epilogue (+chunk/combine for super nodes)",
             "bound": "hbm",
             "achieved": round(agg_gbs, 1),
             "peak": HBM_PEAK_GBS,
@@ -265,9 +289,26 @@ def main():
             "avg_launch_ms": round(agg_ms, 5),
             "launches": len(timers.get("sage_fwd", [])),
         },
-        "spmm_bwd_avg_ms": round(avg_ms("spmm_bwd"), 5),
+        "roofline_agg_bwd": {
+            "kernel": "bgnn_spmm_bwd (transpose aggregation): " + agg_name.format(e=0),
+            "bound": "hbm",
+            "achieved": round(bwd_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("spmm_bwd"),
+            "algorithmic_bytes": bwd_bytes,
+            "avg_launch_ms": round(bwd_ms, 5),
+            "launches": len(timers.get("spmm_bwd", [])),
+        },
+        "lr": lr,
         "final_loss": loss_v,
     }
+    if is_ea:
+        # the SAGE kernels above never run for EA_GNN: no roofline blocks for them
+        out["roofline"] = None
+        for k in ("roofline_hbm", "roofline_agg_bwd"):
+            out.pop(k)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(batch_cpu, state0, args.model, args.cpu_steps)
     if rank == 0:

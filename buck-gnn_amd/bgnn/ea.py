@@ -113,8 +113,18 @@ class _LinearGatherReLU(torch.autograd.Function):
         return de, dW, db, d1, None, d2, None, None
 
 
+def _epilogue_gather_available() -> bool:
+    """bgnn_gemm_gather_add runs on the split GEMM family (f16x3 / bf16x6); the f32-MFMA family
+    (BGNN_TUNE_GEMM_MODE = 0) and the torch.mm A/B backend take the two-step form."""
+    from . import fused
+    return fused.GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) != 0
+
+
 def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False):
+    if not _epilogue_gather_available():
+        return gather_add(linear(e, W, b, False, bf16=bf16), p1, seg1, p2, seg2, relu=True)
     return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16)
+
 
 class _ColumnBlocks(torch.autograd.Function):
     """Split [N, k*H] into k column views whose backward is ONE concatenation of the k
@@ -123,12 +133,15 @@ class _ColumnBlocks(torch.autograd.Function):
     @staticmethod
     def forward(ctx, P, k: int):
         ctx.k = k
+        ctx.set_materialize_grads(False)   # unused blocks arrive as None: no zero-filled buffers
         H = P.size(1) // k
         return tuple(P[:, i * H:(i + 1) * H] for i in range(k))
 
     @staticmethod
     def backward(ctx, *gs):
-        ref = next(g for g in gs if g is not None)
+        ref = next((g for g in gs if g is not None), None)
+        if ref is None:
+            return None, None
         gs = [torch.zeros_like(ref) if g is None else g for g in gs]
         return torch.cat(gs, 1), None
 

@@ -580,7 +580,10 @@ const int kNumX6Cfgs = 5;
 
 template <int PREC, int TA, int TB, int ABL>
 static void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    if constexpr (PREC == 1) {
+    // 256x256 tiles (cfg 3, 4): f16x3 and bf16 (one or two pieces fit the LDS; bf16x6's three do
+    // not, make_plan never picks them for it). The tile here must be the plan's tile
+    // (bgnn_gemm_f32_scaled sizes the grid from it).
+    if constexpr (PREC >= 1) {
         if (cfg == 3) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); return; }
         if (cfg == 4) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL>), grid, dim3(512), 0, s, g); return; }
     }

@@ -10,6 +10,7 @@ Follows, line for line in meaning:
   pooling super*     Models/BuckGNN.py:248-271,277-293
   loss               Utils/Losses.py:755-761 on Normalizer.py:207-215 denormalised values
   step               TRAIN_FINAL.py:190 (Adam lr, wd), :253-298 (fwd, loss, zero_grad, bwd, step)
+  EA_GNN loop        Models/BuckGNN.py:375-387 with GraphNetBlock :528-566 (edge encoder :76-82)
 The SAGEConv arithmetic is oracle.pyg_ref (gather -> index_add -> lin_l + lin_r -> normalize).
 """
 from __future__ import annotations
@@ -89,6 +90,34 @@ def forward(sd: Dict[str, Tensor], model_name: str, x: Tensor, edge_index: Tenso
             raise ValueError(pooling)
     pred = _mlp(sd, "decoder", pooled).squeeze()
     return (pred, nodes) if return_nodes else pred
+
+
+def graphnet_block(sd: Dict[str, Tensor], pre: str, x: Tensor, edge_index: Tensor, e: Tensor):
+    """GraphNetBlock.forward (Models/BuckGNN.py:552-566): concatenation MLPs on gathered node
+    rows, scatter_mean of the messages at row = edge_index[0]."""
+    row, col = edge_index[0], edge_index[1]
+    e = _mlp(sd, pre + ".edge_mlp", torch.cat([x[row], x[col], e], 1))
+    m = _mlp(sd, pre + ".node_mlp_phi", torch.cat([x[col], e], 1))
+    deg = torch.zeros(x.size(0), dtype=x.dtype, device=x.device).index_add_(
+        0, row, torch.ones(row.numel(), dtype=x.dtype, device=x.device))
+    agg = torch.zeros(x.size(0), m.size(1), dtype=m.dtype, device=m.device).index_add_(0, row, m)
+    agg = agg / deg.clamp_min(1).unsqueeze(1)
+    x = _mlp(sd, pre + ".node_mlp_gamma", torch.cat([x, agg], 1))
+    return x + _mlp(sd, pre + ".node_mlp_beta", x), e
+
+
+def ea_forward(sd: Dict[str, Tensor], x: Tensor, edge_index: Tensor, edge_attr: Tensor, batch: Optional[Tensor],
+               training: bool, dropout: float = 0.0, num_layers: int = 6) -> Tensor:
+    """EA_GNN forward (Models/BuckGNN.py:323,375-387,515-516) with mean pooling."""
+    x = _mlp(sd, "node_encoder", x)
+    e = _mlp(sd, "edge_encoder", edge_attr)
+    for i in range(num_layers):
+        x_prev, e_prev = x, e
+        x, e = graphnet_block(sd, f"gn_blocks.{i}", x, edge_index, e)
+        if 0 < i < num_layers - 1:
+            x, e = x + x_prev, e + e_prev
+        x, e = F.dropout(x, dropout, training), F.dropout(e, dropout, training)
+    return _mlp(sd, "decoder", global_mean_pool(x, batch)).squeeze()
 
 
 def relative_error_loss(pred: Tensor, target: Tensor, eps: float = 1e-8) -> Tensor:

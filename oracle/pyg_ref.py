@@ -24,7 +24,8 @@ def scatter(src: Tensor, index: Tensor, dim_size: int, reduce: str) -> Tensor:
         return src.new_zeros(out_shape).index_add_(0, index, src)
     if reduce == "mean":
         s = src.new_zeros(out_shape).index_add_(0, index, src)
-        cnt = torch.zeros(dim_size, dtype=src.dtype).index_add_(0, index, torch.ones(index.numel(), dtype=src.dtype))
+        cnt = torch.zeros(dim_size, dtype=src.dtype, device=src.device).index_add_(
+            0, index, torch.ones(index.numel(), dtype=src.dtype, device=src.device))
         return s / cnt.clamp_min(1).view(-1, *([1] * (src.dim() - 1)))
     if reduce == "max":
         idx = index.view(-1, *([1] * (src.dim() - 1))).expand_as(src)

@@ -199,15 +199,22 @@ def test_gemm_c_amax(dev, mode, shape):
     assert bool((c >= 0).all())
 
 
-@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-def test_gemm_bf16_precision(dev, ta, tb):
+@pytest.mark.parametrize("ta,tb,mnk", [(False, True, (1500, 384, 2000)), (False, False, (1500, 384, 2000)),
+                                       (True, False, (1500, 384, 2000)),
+                                       # shapes whose plan picks the 256x256 tiles (cfg 3/4): the EA_GNN
+                                       # node-block GEMM (N >= 1024) and a split-K weight gradient
+                                       (False, True, (4500, 1536, 512)), (True, False, (512, 256, 20000))])
+def test_gemm_bf16_precision(dev, ta, tb, mnk):
     """precision = 1: operands rounded to bf16, f32 accumulation -- equal to an fp64 product of the
-    bf16-rounded operands up to the f32 accumulation error."""
+    bf16-rounded operands up to the f32 accumulation error, over EVERY output element (the output
+    is pre-filled with NaN: an element the kernel never writes fails)."""
     torch.manual_seed(10)
-    M, N, K = 1500, 384, 2000
+    M, N, K = mnk
     a = torch.randn((K, M) if ta else (M, K), device=dev)
     b = torch.randn((N, K) if tb else (K, N), device=dev)
-    c = fused.gemm(a, b, ta, tb, bf16=True)
+    c = torch.full((M, N), float("nan"), device=dev)
+    fused.gemm(a, b, ta, tb, out=c, bf16=True)
+    assert bool(torch.isfinite(c).all())
     A = a.bfloat16().double().cpu()
     B = b.bfloat16().double().cpu()
     A = A.t() if ta else A

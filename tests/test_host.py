@@ -138,6 +138,23 @@ def test_column_blocks_backward_is_one_concat():
     assert torch.equal(P.grad, torch.cat([w, torch.zeros_like(w), 2 * w], 1))
 
 
+def test_column_blocks_unused_blocks_get_no_buffers():
+    """An unused block's gradient arrives as None (no materialized zeros); the only used block
+    still yields the full-width gradient, and P gets no gradient through unused outputs."""
+    from bgnn.ea import _ColumnBlocks
+    P = torch.randn(5, 9, dtype=torch.float64, requires_grad=True)
+    a, b, c = _ColumnBlocks.apply(P, 3)
+    (3 * b).sum().backward()
+    assert torch.equal(P.grad, torch.cat([torch.zeros(5, 3), torch.full((5, 3), 3.0), torch.zeros(5, 3)], 1).double())
+    # every block unused by the loss: backward returns None for P (no StopIteration)
+    Q = torch.randn(4, 6, requires_grad=True)
+    x, y = _ColumnBlocks.apply(Q, 2)
+    z = torch.randn(1, requires_grad=True)
+    (z * 2).sum().backward(inputs=[z])
+    out = _ColumnBlocks.backward(type("Ctx", (), {"k": 2})(), None, None)
+    assert out == (None, None)
+
+
 def test_relu_mask_matches_reference_form():
     """threshold_backward (the backward ReLU mask of bgnn.ea / bgnn.fused) == g * (out > 0)."""
     g, out = torch.randn(64, 33), torch.randn(64, 33)

@@ -133,3 +133,35 @@ def test_oracle_matches_reference_golden(path):
     with torch.no_grad():
         pe = R.forward(step, meta["model_name"], x, ei, batch, False, meta["pooling"], 0.0)
     np.testing.assert_allclose(pe.numpy().reshape(-1), z["pred_eval"], rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("path", [p for p in golden_files() if "ea_gnn" in p], ids=os.path.basename)
+def test_ea_oracle_matches_reference_golden(path):
+    """oracle.buckgnn_ref.ea_forward (EA_GNN, Models/BuckGNN.py:375-387,528-566) against the
+    golden vectors of the reference's own EA_GNN: prediction, loss, every gradient."""
+    z, meta = load_case(path)
+    assert meta["model_name"] == "EA_GNN"
+    sd = oracle_state(meta, reference_shapes(meta))
+    x = torch.from_numpy(z["x"])
+    ei = torch.from_numpy(z["edge_index"])
+    ea = torch.from_numpy(z["edge_attr"])
+    batch = torch.from_numpy(z["batch"])
+    y = torch.from_numpy(z["y"])
+    step = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    pred = R.ea_forward(step, x, ei, ea, batch, True, 0.0, meta["num_layers"])
+    loss = R.relative_error_loss(pred, y)
+    loss.backward()
+    np.testing.assert_allclose(pred.detach().numpy().reshape(-1), z["pred_train"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(loss.item(), float(z["loss_train"]), rtol=2e-5, atol=2e-5)
+    n = 0
+    for k in z.files:
+        if k.startswith("grad/"):
+            np.testing.assert_allclose(step[k[5:]].grad.numpy(), z[k], rtol=1e-4, atol=1e-5, err_msg=k)
+            n += 1
+        elif k.startswith("gradsum/"):
+            np.testing.assert_allclose(grad_checksum(step[k[8:]].grad.numpy()), z[k], rtol=1e-3, atol=1e-4, err_msg=k)
+            n += 1
+    assert n > 0
+    with torch.no_grad():
+        pe = R.ea_forward(step, x, ei, ea, batch, False, 0.0, meta["num_layers"])
+    np.testing.assert_allclose(pe.numpy().reshape(-1), z["pred_eval"], rtol=2e-5, atol=2e-5)

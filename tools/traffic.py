@@ -20,10 +20,11 @@ import statistics
 import sys
 from collections import defaultdict
 
-# bench roofline kernels: key -> kernel-name substring
+# bench roofline kernels: key -> kernel-name substrings (either matches)
 KERNELS = {
-    "gemm_fwd_h3": "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>",   # f16x3 forward GEMM (256x256 tiles)
-    "sage_fwd": "k_seg_sweep<2, 0, 1,",
+    "gemm_fwd_h3": ("k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>",),   # f16x3 forward GEMM (256x256 tiles)
+    "sage_fwd": ("k_seg_group<2, 0, 1,", "k_seg_sweep<2, 0, 1,"),   # fused SAGE forward aggregation
+    "spmm_bwd": ("k_seg_group<2, 0, 0,", "k_seg_sweep<2, 0, 0,"),   # transpose aggregation
 }
 
 
@@ -36,7 +37,7 @@ def per_launch(pass_dir, counter):
             vals[r["Kernel_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     out = {}
     for key, pat in KERNELS.items():
-        xs = [v for name, d in vals.items() if pat in name for v in d.values()]
+        xs = [v for name, d in vals.items() if any(p in name for p in pat) for v in d.values()]
         if xs:
             out[key] = statistics.median(xs) * 1024.0
     return out
@@ -51,7 +52,7 @@ def main():
            "kernels": {}}
     for key in KERNELS:
         if key in fetch and key in write:
-            res["kernels"][key] = {"kernel_pattern": KERNELS[key], "fetch_bytes": 2 * fetch[key],
+            res["kernels"][key] = {"kernel_pattern": list(KERNELS[key]), "fetch_bytes": 2 * fetch[key],
                                    "write_bytes": write[key], "bytes_per_launch": 2 * fetch[key] + write[key]}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
