@@ -29,6 +29,8 @@ from .ops import segment_reduce
 # run the node encoder on bgnn GEMMs (fused bias+ReLU) instead of torch nn.Linear
 # (with the bf16x6 GEMM: 14.79 vs 14.82 ms/step, tools/ab_step.py)
 FUSED_ENCODER = True
+# fold the node encoder's last Linear into the first fused SAGE layer (BuckGNN._foldable_encoder)
+FOLD_ENCODER = True
 
 _SAGE_VARIANTS = {
     # model_name: (ModuleList attribute, aggr, has BatchNorm)
@@ -202,11 +204,23 @@ class BuckGNN(nn.Module):
     def _fused_ok(self, x: Tensor) -> bool:
         return self.use_fused and x.is_cuda and self.hidden_channels % 4 == 0 and self.hidden_channels <= 512
 
+    def _sage_fused(self, x: Tensor, aggr: str) -> bool:
+        return self._fused_ok(x) and aggr in ("add", "sum", "mean")
+
+    def _foldable_encoder(self, x: Tensor) -> bool:
+        """The node encoder's last Linear can be folded into the first fused SAGE layer (which
+        has no skip connection): the encoder output x0 = h W^T + b feeds only that layer's
+        transform [W_l;W_r], so z = h ([W_l;W_r] W)^T + [W_l;W_r] b (fused.sage_layer w_in)."""
+        enc = self.node_encoder
+        return (FOLD_ENCODER and FUSED_ENCODER and isinstance(enc, nn.Sequential) and len(enc) >= 2
+                and isinstance(enc[-1], nn.Linear) and enc[-1].out_features == self.hidden_channels
+                and x.size(0) >= 1024 and self.num_layers >= 1)
+
     def _sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, aggr: str, skip_last_excluded: bool,
-                   x_amax: Optional[Tensor] = None):
+                   x_amax: Optional[Tensor] = None, x_in: Optional[nn.Linear] = None):
         L = len(convs) if convs is not None else self.num_layers
         p = self.dropout.p
-        if self._fused_ok(x) and aggr in ("add", "sum", "mean"):
+        if self._sage_fused(x, aggr):
             graph = graph_for(edge_index, x.size(0))
             red = 1 if aggr == "mean" else 0
             amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
@@ -215,10 +229,14 @@ class BuckGNN(nn.Module):
                 conv = convs[i] if convs is not None else self.shared_graphsage_block
                 bn = bns[i] if bns is not None else None
                 skip = 0 < i < L - 1
+                fold = x_in if i == 0 else None
                 x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
                                      skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
-                                     amax_buf=bufs[i])
+                                     amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
+                                     b_in=None if fold is None else fold.bias)
             return x
+        if x_in is not None:   # (only reached when the caller folded the encoder's last Linear)
+            x = x_in(x)
         for i in range(L):
             x_prev = x
             conv = convs[i] if convs is not None else self.shared_graphsage_block
@@ -238,7 +256,13 @@ class BuckGNN(nn.Module):
                                                                            device=x.device)
             real_node_batch = batch[is_real_node] if batch is not None else None
         x_amax = None   # max|x| after the encoder (f16x3 operand scale of the first SAGE GEMM)
-        if self._fused_ok(x) and x.size(0) >= 1024 and FUSED_ENCODER:
+        x_in = None     # the encoder's last Linear when it is folded into the first SAGE layer
+        sage = _SAGE_VARIANTS.get(name, (None, "add", None))[1] if name != "GraphSage_addAggr_Shared" else "add"
+        if (name in _SAGE_VARIANTS or name == "GraphSage_addAggr_Shared") and self._sage_fused(x, sage) \
+                and self._foldable_encoder(x):
+            x_in = self.node_encoder[-1]
+            x, x_amax = mlp(self.node_encoder[:-1], x, return_amax=True)
+        elif self._fused_ok(x) and x.size(0) >= 1024 and FUSED_ENCODER:
             x, x_amax = mlp(self.node_encoder, x, return_amax=True)   # GEMMs with fused bias+ReLU epilogues
         else:
             x = self.node_encoder(x)
@@ -259,7 +283,7 @@ class BuckGNN(nn.Module):
                     x, e = x + x_prev, e + e_prev
                 x, e = self.dropout(x), self.dropout(e)
         if name == "GraphSage_addAggr_Shared":
-            x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax)
+            x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax, x_in)
         elif name == "EA_GNN":
             if not ea_fused:
                 e = self.edge_encoder(edge_attr)
@@ -275,7 +299,7 @@ class BuckGNN(nn.Module):
                 x, e = self.dropout(x), self.dropout(e)
         elif name in _SAGE_VARIANTS:
             attr, aggr, _ = _SAGE_VARIANTS[name]
-            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax)
+            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax, x_in)
         elif name in ("GraphSage_addAggr_woBatchNorm", "GraphSage_MLP"):
             getattr(self, "sage_blocks_add")  # AttributeError, as in the reference (:405,473)
         elif name == "GraphSage_sumAggr_woBatchNorm":

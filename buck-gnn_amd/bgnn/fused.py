@@ -259,27 +259,41 @@ class SageLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_prev, x_amax, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
-                cfg: LayerConfig, amax=None):
-        N, H = x_prev.shape
+                cfg: LayerConfig, amax=None, w_in=None, b_in=None):
         dev = x_prev.device
         x_prev = x_prev.contiguous()
+        H = w_l.size(0)
+        N = x_prev.size(0)
         wcat = torch.cat([w_l, w_r], 0).contiguous()             # [2H, H]
         # operand maxima: [0] = max|W|, [1] = max|x_next| (this layer's output), [2] = max|dz|
         # (zeroed; the layer loop passes one slice of a single per-step fill)
         if amax is None:
             amax = torch.zeros(3, dtype=torch.float32, device=dev)
         w_amax, next_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
-        absmax(wcat, w_amax, accumulate=True)
+        folded = w_in is not None
+        if folded:
+            # the encoder's last Linear folded into this layer's transform (x_prev = its input h):
+            # x = h W_in^T + b_in never materialised; z = x [W_l;W_r]^T = h Wf^T + bf with
+            # Wf = [W_l;W_r] W_in [2H, K_in], bf = [W_l;W_r] b_in
+            if cfg.skip:
+                raise ValueError("sage_layer: a folded input transform needs a layer without skip")
+            wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False)
+            bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False).view(-1)
+            absmax(wf, w_amax, accumulate=True)
+            wmat = wf
+        else:
+            absmax(wcat, w_amax, accumulate=True)
+            wmat, bf = wcat, None
         if x_amax is None:
             x_amax = absmax(x_prev)
-        planes = Z_PLANES and H % PLANE_TILE == 0
+        planes = Z_PLANES and H % PLANE_TILE == 0 and not folded
         with _timed("gemm_fwd"):
             if planes:   # z = [z_l ; z_r] as two dense [N, H] planes
                 z = torch.empty(2, N, H, dtype=torch.float32, device=dev)
-                gemm(x_prev, wcat, trans_a=False, trans_b=True, out=Planes(z), a_amax=x_amax, b_amax=w_amax)
+                gemm(x_prev, wmat, trans_a=False, trans_b=True, out=Planes(z), a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z[0], z[1], H
             else:        # interleaved [N, 2H]
-                z = gemm(x_prev, wcat, trans_a=False, trans_b=True, a_amax=x_amax, b_amax=w_amax)
+                z = gemm(x_prev, wmat, trans_a=False, trans_b=True, bias=bf, a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z, z[:, H:], 2 * H
         o = torch.empty(N, H, dtype=torch.float32, device=dev)
         nrm = torch.empty(N, dtype=torch.float32, device=dev)
@@ -312,6 +326,8 @@ class SageLayerFn(torch.autograd.Function):
                   float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), s)
         ctx.graph = graph
         ctx.cfg = cfg
+        ctx.folded = folded
+        ctx.fold = (w_in, b_in, wf) if folded else None
         ctx.save_for_backward(x_prev, o, nrm, wcat, gamma if gamma is not None else torch.empty(0, device=dev),
                               scale if scale is not None else torch.empty(0, device=dev),
                               shift if shift is not None else torch.empty(0, device=dev),
@@ -328,6 +344,7 @@ class SageLayerFn(torch.autograd.Function):
         graph: Graph = ctx.graph
         g = g.contiguous()
         N, H = o.shape
+        planes = DZ_PLANES and H % PLANE_TILE == 0
         dev = o.device
         s = _stream()
         bn = cfg.bn
@@ -345,7 +362,6 @@ class SageLayerFn(torch.autograd.Function):
                 sum_g2, sum_g2xhat = sums[0], sums[1]
             else:
                 sum_g2 = sum_g2xhat = torch.zeros(H, dtype=torch.float32, device=dev)
-        planes = DZ_PLANES and H % PLANE_TILE == 0
         if planes:   # dz = [dz_l ; dh] as two dense [N, H] planes
             dzt = torch.empty(2, N, H, dtype=torch.float32, device=dev)
             dz, dzl, dh, lddz = Planes(dzt), dzt[0], dzt[1], H
@@ -370,6 +386,21 @@ class SageLayerFn(torch.autograd.Function):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
                       dh.data_ptr(), lddz, H, cfg.reduce, None, dzl.data_ptr(), lddz, _ptr(part),
                       dz_amax.data_ptr(), s)
+        has_affine = bn and gamma.numel() > 0
+        if ctx.folded:
+            # x = h W_in^T + b_in folded in: dh = dz Wf; dWf = dz^T h; dbf = column sums of dz;
+            # then dWcat = dWf W_in^T + dbf b_in^T (= dz^T x), dW_in = Wcat^T dWf, db_in = Wcat^T dbf
+            w_in, b_in, wf = ctx.fold
+            wf_t = wf.t().contiguous() if DGRAD_WT else wf
+            dx = gemm(dz, wf_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
+            dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, K_in]
+            dbf = torch.cat([dz.t[0].sum(0) if planes else dz[:, :H].sum(0), db])          # Σ dz_l ; Σ dh
+            dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)                 # [2H, H]
+            dw.add_(torch.outer(dbf, b_in))
+            dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                           # [H, K_in]
+            db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)      # [H]
+            return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
+                    None, None, None, None, None, dw_in, db_in)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
         wcat_t = wcat.t().contiguous() if DGRAD_WT else wcat
@@ -380,19 +411,24 @@ class SageLayerFn(torch.autograd.Function):
             dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
         dw = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)      # [2H, H]
         dw_l, dw_r = dw[:H], dw[H:]
-        has_affine = bn and gamma.numel() > 0
         return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
-               seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None):
+               seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None,
+               w_in: torch.Tensor = None, b_in: torch.Tensor = None):
     """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
     x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
-    spares the GEMM a pass over x_prev; return_amax: also return max|x_next|."""
+    spares the GEMM a pass over x_prev; return_amax: also return max|x_next|.
+    w_in / b_in: fold a preceding Linear into this layer (x_prev is then that Linear's INPUT h,
+    and the layer computes on x = h W_in^T + b_in without materialising x); only for a layer
+    without skip connection (the reference's first SAGE layer after the node encoder)."""
     require_cuda(x_prev, w_l, b_l, w_r, what="sage_layer")
-    H = x_prev.size(1)
+    H = w_l.size(0)
+    if w_in is None and x_prev.size(1) != H:
+        raise ValueError(f"sage_layer: x has {x_prev.size(1)} features, the layer {H}")
     if H % 4 or H > 512:
         raise ValueError(f"sage_layer: fused path needs H % 4 == 0 and H <= 512 (got {H})")
     if reduce not in (0, 1):
@@ -408,8 +444,9 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
-                                bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf)
+                                bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in)
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
-        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf)
+        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
+                                w_in, b_in)
     return out if return_amax else out[0]
