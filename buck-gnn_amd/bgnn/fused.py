@@ -376,9 +376,13 @@ class SageLayerFn(torch.autograd.Function):
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
                   float(cfg.p), cfg.seed, int(cfg.skip), N, H, dh.data_ptr(), lddz, _ptr(gskip),
-                  part_db.data_ptr(), dz_amax.data_ptr(), s)
-        db = torch.empty(H, dtype=torch.float32, device=dev)
-        _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
+                  part_db.data_ptr(), dz_amax.data_ptr(), graph.fwd.rowptr.data_ptr() if ctx.folded else None,
+                  (2 if cfg.reduce == 1 else 1) if ctx.folded else 0, s)
+        db = torch.empty(2 if ctx.folded else 1, H, dtype=torch.float32, device=dev)
+        # db[0] = sum of dh (db_l); folded input transform: db[1] = column sums of dz_l = A^T dh
+        _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db[0].data_ptr(),
+                  db[1].data_ptr() if ctx.folded else None, 0, s)
+        db, db_zl = db[0], (db[1] if ctx.folded else None)
         # dz_l = A^T dh (transpose CSR; MEAN scales by the target's in-degree)
         bw = graph.bwd
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
@@ -394,7 +398,7 @@ class SageLayerFn(torch.autograd.Function):
             wf_t = wf.t().contiguous() if DGRAD_WT else wf
             dx = gemm(dz, wf_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
             dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, K_in]
-            dbf = torch.cat([dz.t[0].sum(0) if planes else dz[:, :H].sum(0), db])          # Σ dz_l ; Σ dh
+            dbf = torch.cat([db_zl, db])                                                    # Σ dz_l ; Σ dh
             dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)                 # [2H, H]
             dw.add_(torch.outer(dbf, b_in))
             dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                           # [H, K_in]

@@ -291,7 +291,9 @@ inline int choose_split(int64_t M, int64_t N, int64_t K, const GemmCfg& c) {
     int64_t s = (slots + tiles - 1) / tiles;
     const int64_t smax = K / 256;   // keep >= 256 of K per slice
     if (s > smax) s = smax;
-    if (s > 64) s = 64;
+    // skinny weight gradients (a handful of tiles, K = node count) need many slices to fill the
+    // chip: the encoder's 64x128 / 16x64 wgrads ran on 64 workgroups at the old cap of 64
+    if (s > 512) s = 512;
     return s < 1 ? 1 : (int)s;
 }
 

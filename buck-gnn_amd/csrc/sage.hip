@@ -252,7 +252,8 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sum_g2,
     const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
     int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
-    float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax, int nt) {
+    float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax, int nt,
+    const int32_t* __restrict__ w_rowptr, int w_mode) {
     const int lane = threadIdx.x & 63;
     uint32_t tmax = 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -287,11 +288,11 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
             }
         }
     }
-    float db[NV][4];
+    float db[NV][4], dw[NV][4];   // sums of dh and of w_r * dh (w_mode: row weights from w_rowptr)
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) db[v][k] = 0.f;
+        for (int k = 0; k < 4; ++k) db[v][k] = dw[v][k] = 0.f;
 
     for (int64_t r = r0 + wave; r < r1; r += 4) {
         float ov[NV][4], dov[NV][4], g1v[NV][4];
@@ -331,6 +332,11 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
         const float n = nrm[r];
         const bool through = n >= 1e-12f;
         const float rn = through ? 1.f / n : 1e12f;
+        float wr = 0.f;
+        if (w_mode) {
+            const int32_t d = w_rowptr[r + 1] - w_rowptr[r];
+            wr = (w_mode == 1) ? (float)d : (d > 0 ? 1.f : 0.f);
+        }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if (!cok[v]) continue;
@@ -339,6 +345,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
             for (int k = 0; k < 4; ++k) {
                 out[k] = through ? (dov[v][k] - ov[v][k] * dot) * rn : dov[v][k] * rn;
                 db[v][k] += out[k];
+                dw[v][k] = fmaf(wr, out[k], dw[v][k]);
                 tmax = max(tmax, __float_as_uint(out[k]) & 0x7fffffffu);
             }
             store4(dh + r * lddh + cpos[v], out[0], out[1], out[2], out[3], nt);
@@ -347,17 +354,20 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
         }
     }
     if (amax) block_amax(amax, tmax);
-    __shared__ __attribute__((aligned(16))) float red[4][512];
+    __shared__ __attribute__((aligned(16))) float red[4][2][512];
 #pragma unroll
     for (int v = 0; v < NV; ++v)
         if (cok[v])
 #pragma unroll
-            for (int k = 0; k < 4; ++k) red[wave][cpos[v] + k] = db[v][k];
+            for (int k = 0; k < 4; ++k) {
+                red[wave][0][cpos[v] + k] = db[v][k];
+                red[wave][1][cpos[v] + k] = dw[v][k];
+            }
     __syncthreads();
     float* dst = part + (int64_t)lb * 2 * H;
     for (int c = threadIdx.x; c < H; c += 256) {
-        dst[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-        dst[H + c] = 0.f;
+        dst[c] = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+        dst[H + c] = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
     }
 }
 
@@ -458,8 +468,10 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
                                   const float* shift, const float* gamma, const float* mean, const float* invstd,
                                   const float* sum_g2, const float* sum_g2xhat, float p, uint64_t seed,
                                   int32_t skip, int64_t n_rows, int32_t H, float* dh, int64_t lddh, float* gskip,
-                                  float* partial_db, float* amax, void* stream) {
+                                  float* partial_db, float* amax, const int32_t* w_rowptr, int32_t w_mode,
+                                  void* stream) {
     BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 512, "sage_bwd_rows: H=%d unsupported", H);
+    BGNN_REQUIRE(w_mode >= 0 && w_mode <= 2 && (w_mode == 0 || w_rowptr), "sage_bwd_rows: bad row weights");
     BGNN_REQUIRE(lddh >= H && lddh % 4 == 0, "sage_bwd_rows: bad lddh");
     BGNN_REQUIRE(!skip || gskip, "sage_bwd_rows: skip requires gskip");
     BGNN_REQUIRE(!mean || (invstd && sum_g2 && sum_g2xhat), "sage_bwd_rows: BN stats incomplete");
@@ -473,11 +485,11 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
     if (H > 256)
         hipLaunchKernelGGL(k_sage_bwd_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt());
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode);
     else
         hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt());
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

@@ -226,7 +226,11 @@ int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
 /* Backward pass 2 (row-wise): BatchNorm input-gradient, then the L2-normalize
  * backward, giving dh [N, H] (ld = lddh). If skip, writes dropout'(g) into
  * gskip [N, H] (the skip branch's gradient, the initial value of dL/dx_prev).
- * Partial sums of dh (for db_l) go to partial_db [slots, 2, H] (second half 0).
+ * Partial sums go to partial_db [slots, 2, H]: [.][0] = sum of dh rows (for db_l), [.][1] =
+ * sum of w_r * dh_r with row weights w_r from w_rowptr (w_mode 1: w_r = rowptr[r+1]-rowptr[r],
+ * the in-degree; 2: [in-degree > 0]; 0: no weights, the half is 0). With the forward CSR and
+ * the layer's reduce (1 for sum, 2 for mean) that is the column sum of dz_l = A^T dh, the bias
+ * gradient of a Linear folded into the layer (fused.sage_layer w_in).
  * sum_g2 / sum_g2xhat are the reduced stats of pass 1 (NULL when BatchNorm is off).
  * amax (optional): *amax = max(*amax, max |dh|). */
 int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
@@ -235,7 +239,8 @@ int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
                        const float* sum_g2, const float* sum_g2xhat,
                        float p, uint64_t seed, int32_t skip,
                        int64_t n_rows, int32_t H, float* dh, int64_t lddh,
-                       float* gskip, float* partial_db, float* amax, void* stream);
+                       float* gskip, float* partial_db, float* amax,
+                       const int32_t* w_rowptr, int32_t w_mode, void* stream);
 
 /* ------------------------------------------------------------------------
  * fp32 GEMM (f32 operands, f32 result, f32 accumulation):
