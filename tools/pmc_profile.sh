@@ -3,9 +3,10 @@
 # tracing domains mixed in). Usage: tools/pmc_profile.sh OUTDIR -- python script.py args...
 # Each pass writes OUTDIR/passN/*counter_collection.csv; summarise with tools/pmc_summary.py.
 set -e
-OUT=$1; shift
+OUT=$(realpath -m "$1"); shift
 [ "$1" == "--" ] && shift
 export TMPDIR=/tmp
+ROOT=$(pwd)
 PASSES=(
   "FETCH_SIZE GRBM_GUI_ACTIVE"
   "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"
@@ -17,5 +18,5 @@ i=0
 for p in "${PASSES[@]}"; do
   i=$((i+1))
   mkdir -p "$OUT/pass$i"
-  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $p --output-format csv -d "$OUT/pass$i" -o run -- "$@" > "$OUT/pass$i/stdout.log" 2>&1)
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $p --output-format csv -d "$OUT/pass$i" -o run -- "$@" > "$OUT/pass$i/stdout.log" 2>&1) || true
 done

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--variants", default="4x2x8x1,8x2x8x1")
     ap.add_argument("--blocks", default="256,512,1024")
+    ap.add_argument("--flush", action="store_true", help="write 1 GiB between launches (cold caches)")
     ap.add_argument("--qvariants", default="0x4x1x12x1024,0x4x1x12x2048,0x4x1x16x2048,0x2x1x12x1024,0x2x1x12x2048,"
                     "1x4x4x12x1024,1x4x4x12x2048,1x4x8x12x1024,1x4x8x12x2048,1x4x8x16x1024,1x2x4x12x1024,"
                     "1x2x8x12x1024,1x2x4x12x512")
@@ -146,8 +147,11 @@ def main():
         for bl in args.blocks.split(","):
             runs[f"grp{v}_b{bl}"] = mk(v, int(bl))
     times = {k: [] for k in runs}
+    junk = torch.empty(1 << 28, device=dev) if args.flush else None
     for rnd in range(args.rounds + 2):
         for k, fn in runs.items():
+            if junk is not None:
+                junk.fill_(1.0)
             ev, out = fn()
             torch.cuda.synchronize()
             if rnd >= 2:

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--variants", default="sweep12,group8_b512,group8_b768,group8_b1024,group4_b512,group4_b1024")
     ap.add_argument("--no-virtual", action="store_true", help="cfg2 meshes without the random virtual edges")
+    ap.add_argument("--flush", action="store_true",
+                    help="write 1 GiB between launches (cold L2 / Infinity Cache, as inside a train step)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.no_virtual:
@@ -102,10 +104,13 @@ def main():
     variants = args.variants.split(",")
     times = {(v, k): [] for v in variants for k in ("fwd", "bwd")}
     ref = {}
+    junk = torch.empty(1 << 28, device=dev) if args.flush else None
     for rnd in range(args.rounds + 2):
         for v in variants:
             set_variant(v)
             for k, fn in (("fwd", run_fwd), ("bwd", run_bwd)):
+                if junk is not None:
+                    junk.fill_(1.0)
                 ev, outs = fn()
                 torch.cuda.synchronize()
                 if rnd >= 2:
