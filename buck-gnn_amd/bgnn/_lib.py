@@ -79,6 +79,8 @@ SIGNATURES = {
     "bgnn_rows_slots": (c_i32, [c_i64]),
     "bgnn_sage_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i64, c_i32, c_p, c_p]),
     "bgnn_reduce_partials": (c_i32, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p]),
+    "bgnn_linear_bwd_prep_slots": (c_i32, []),
+    "bgnn_linear_bwd_prep": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
                                    c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),

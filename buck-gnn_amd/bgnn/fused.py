@@ -38,6 +38,11 @@ Z_PLANES = False
 DZ_PLANES = False
 # dgrad B operand: transposed copy of [W_l;W_r] (K-contiguous loads) instead of strided reads
 DGRAD_WT = True
+# folded input transform: the weight-by-weight products (Wf = Wcat W_in, its gradients; no node
+# dimension, <= 0.3 GFLOP each) on torch.mm instead of bgnn_gemm (A/B switch; default bgnn:
+# both are f32-class, torch.mm saved ~1 % of the step but shifts the BN-amplified gradient
+# rounding noise, tools/fold_ab.py)
+FOLD_WEIGHTS_TORCH = False
 
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
@@ -184,10 +189,29 @@ class LinearFn(torch.autograd.Function):
     def backward(ctx, g, _g_amax):
         x, weight, y, x_amax, w_amax = ctx.saved_tensors
         g = g.contiguous()
-        if ctx.relu:
-            g = torch.ops.aten.threshold_backward(g, y, 0.0)   # ReLU mask in one pass
         bf16 = ctx.bf16
-        g_amax = None if bf16 else absmax(g)
+        C = g.size(1)
+        db = None
+        if C % 4 == 0 and 4 <= C <= 1024 and 256 % (C // 4) == 0:
+            # ReLU mask, bias-gradient partials and max|g| in one pass (bgnn_linear_bwd_prep)
+            gm = torch.empty_like(g) if ctx.relu else g
+            slots = _lib.query("bgnn_linear_bwd_prep_slots")
+            part = torch.empty(slots, 2, C, dtype=torch.float32, device=g.device)
+            g_amax = torch.zeros(1, dtype=torch.float32, device=g.device)
+            s = _stream()
+            _lib.call("bgnn_linear_bwd_prep", g.data_ptr(), y.data_ptr() if ctx.relu else None, g.size(0), C,
+                      gm.data_ptr() if ctx.relu else None, part.data_ptr(), g_amax.data_ptr(), s)
+            if ctx.has_bias:
+                db = torch.empty(C, dtype=torch.float32, device=g.device)
+                _lib.call("bgnn_reduce_partials", part.data_ptr(), slots, C, db.data_ptr(), None, 0, s)
+            g = gm
+            if bf16:
+                g_amax = None
+        else:
+            if ctx.relu:
+                g = torch.ops.aten.threshold_backward(g, y, 0.0)   # ReLU mask in one pass
+            g_amax = None if bf16 else absmax(g)
+            db = g.sum(0) if ctx.has_bias else None
         w_amax = None if bf16 else w_amax
         x_amax = None if bf16 else x_amax
         dx = None
@@ -198,7 +222,6 @@ class LinearFn(torch.autograd.Function):
                   gemm(g, weight.contiguous(), trans_a=False, trans_b=False, a_amax=g_amax, b_amax=w_amax,
                        bf16=bf16))
         dw = gemm(g, x, trans_a=True, trans_b=False, a_amax=g_amax, b_amax=x_amax, bf16=bf16)
-        db = g.sum(0) if ctx.has_bias else None
         return dx, dw, db, None, None, None, None
 
 
@@ -277,8 +300,12 @@ class SageLayerFn(torch.autograd.Function):
             # Wf = [W_l;W_r] W_in [2H, K_in], bf = [W_l;W_r] b_in
             if cfg.skip:
                 raise ValueError("sage_layer: a folded input transform needs a layer without skip")
-            wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False)
-            bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False).view(-1)
+            if FOLD_WEIGHTS_TORCH:
+                wf = torch.mm(wcat, w_in)
+                bf = torch.mv(wcat, b_in)
+            else:
+                wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False)
+                bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False).view(-1)
             absmax(wf, w_amax, accumulate=True)
             wmat = wf
         else:
@@ -399,10 +426,15 @@ class SageLayerFn(torch.autograd.Function):
             dx = gemm(dz, wf_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
             dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, K_in]
             dbf = torch.cat([db_zl, db])                                                    # Σ dz_l ; Σ dh
-            dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)                 # [2H, H]
-            dw.add_(torch.outer(dbf, b_in))
-            dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                           # [H, K_in]
-            db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)      # [H]
+            if FOLD_WEIGHTS_TORCH:
+                dw = torch.addmm(torch.outer(dbf, b_in), dwf, w_in.t())                    # [2H, H]
+                dw_in = torch.mm(wcat.t(), dwf)                                            # [H, K_in]
+                db_in = torch.mv(wcat.t(), dbf)                                            # [H]
+            else:
+                dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)             # [2H, H]
+                dw.add_(torch.outer(dbf, b_in))
+                dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                       # [H, K_in]
+                db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)  # [H]
             return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
                     None, None, None, None, None, dw_in, db_in)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev

@@ -214,7 +214,26 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
         }
 }
 
-__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ ws, int split, int64_t M,
+// Split-K stage 1 for many slabs over a small C (the skinny weight gradients: a few thousand
+// outputs, up to 512 slabs): slab group g of `per` slabs is summed into its first slab, in
+// place (each thread reads its element of the group's slabs before writing it; no other
+// thread touches that element). Coalesced over the elements; fixed summation order.
+__global__ __launch_bounds__(256) void k_splitk_stage1(float* __restrict__ ws, int split, int64_t total, int per) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int s0 = blockIdx.y * per, s1 = min(split, s0 + per);
+    if (i >= total || s0 >= s1) return;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = s0;
+    for (; k + 4 <= s1; k += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += ws[(int64_t)(k + u) * total + i];
+    }
+    for (; k < s1; ++k) acc[0] += ws[(int64_t)k * total + i];
+    ws[(int64_t)s0 * total + i] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+
+// C = act(alpha * sum of the slabs s = 0, stride, 2 stride, ... < split + beta C + bias)
+__global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__ ws, int split, int stride, int64_t M,
                                                        int64_t N, float alpha, float beta, float* __restrict__ C,
                                                        int64_t ldc, const float* __restrict__ bias, int relu,
                                                        int64_t c_blk, int64_t c_pstride) {
@@ -222,7 +241,7 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(const float* __restrict__
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         float s = 0.f;
-        for (int k = 0; k < split; ++k) s += ws[(int64_t)k * total + i];
+        for (int k = 0; k < split; k += stride) s += ws[(int64_t)k * total + i];
         const int64_t r = i / N, c = i % N;
         float v = alpha * s;
         float* Cp = c_blk > 0 ? C + (c / c_blk) * (c_pstride - c_blk) : C;
@@ -254,8 +273,13 @@ static int g_gemm_abl = 0;    // ablation (measurement only)
 static int g_gemm_mode = 2;   // 0 = f32 MFMA kernel, 1 = bf16x6, 2 = f16x3 (gemm_x6.hip, default:
                               // half the MFMAs of bf16x6, error below the f32 MFMA's; tools/tune_gemm.py)
 
+static int g_gemm_staging = -1;   // f16x3 staging: -1 register-staged, else gemm_h3g.hip variant
+
 void set_gemm_mode(int mode) { g_gemm_mode = mode; }
 int gemm_mode() { return g_gemm_mode; }
+void set_gemm_staging(int v) { g_gemm_staging = v; }
+int gemm_staging() { return g_gemm_staging; }
+
 
 // bf16x6 / f16x3 tile choice (tools/tune_gemm.py)
 // f16x3 (MI355X, tools/gemm_one.py under rocprofv3, cfg2 SAGE shapes): fwd 80656x1024x512
@@ -287,7 +311,15 @@ inline int pick_cfg(int64_t M, int64_t N, int64_t K, int ta, int tb) {
 inline int choose_split(int64_t M, int64_t N, int64_t K, const GemmCfg& c) {
     const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     const int64_t slots = 256 * c.blocks_per_cu;          // resident workgroups on the chip
-    if (tiles >= slots / 2 || K < 4 * 256) return 1;
+    if (tiles >= slots / 2) return 1;
+    if (K < 4 * 256) {
+        // a handful of tiles over a few hundred of K (the folded layer's weight-by-weight
+        // products: 8 tiles, K = 512): >= 64-deep slices, so dozens of workgroups share them
+        if (tiles > 16 || K < 128) return 1;
+        int64_t s = (slots + tiles - 1) / tiles;
+        if (s > K / 64) s = K / 64;
+        return s < 1 ? 1 : (int)s;
+    }
     int64_t s = (slots + tiles - 1) / tiles;
     const int64_t smax = K / 256;   // keep >= 256 of K per slice
     if (s > smax) s = smax;
@@ -374,6 +406,12 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
     return p;
 }
 
+// the LDS-DMA staged f16x3 kernel for tall K-contiguous products (fwd / dgrad of the SAGE
+// layers, the EA_GNN edge MLPs) when the staging knob selects it and the shape qualifies
+static bool use_h3g(const Plan& p, int ta, int tb, const GemmArgs& g) {
+    return g_gemm_staging >= 0 && p.x6 && p.prec == 1 && g.M >= 4096 && g.N >= 256 && h3g_ok(g, ta, tb);
+}
+
 // workspace: [256 B operand-max head (f16x3)] [split-K slabs]
 constexpr size_t kAmaxHead = 256;
 
@@ -456,7 +494,8 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     kc = (kc + pl.bk - 1) / pl.bk * pl.bk;
     g.kchunk = kc > 0 ? kc : pl.bk;
     dim3 grid((unsigned)tiles, split);
-    if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
+    if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, M, N), s, g);
+    else if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
     else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
     else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
     else if (ta == 1 && tb == 0) launch_cfg<1, 0>(pl.cfg, grid, s, g);
@@ -465,8 +504,23 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     if (split > 1) {
         int64_t blocks = (M * N + 255) / 256;
         if (blocks > 4096) blocks = 4096;
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)slabs, split, M, N,
-                           alpha, beta, C, ldc, bias, relu, c_blk, c_pstride);
+        // few outputs, many slabs: sum slab groups first so the reduction spreads over >= ~512
+        // workgroups instead of one serial sum per output element (encoder wgrads: 100 -> ~10 us)
+        int stride = 1;
+        const int64_t eb = (M * N + 255) / 256;
+        if (split >= 16 && eb < 512) {
+            int64_t groups = (512 + eb - 1) / eb;
+            if (groups > split / 4) groups = split / 4;
+            if (groups >= 2) {
+                stride = (int)((split + groups - 1) / groups);
+                groups = (split + stride - 1) / stride;
+                hipLaunchKernelGGL(k_splitk_stage1, dim3((unsigned)eb, (unsigned)groups), dim3(256), 0, s, slabs, split,
+                                   M * N, stride);
+                BGNN_CHECK_LAUNCH();
+            }
+        }
+        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)slabs, split, stride,
+                           M, N, alpha, beta, C, ldc, bias, relu, c_blk, c_pstride);
         BGNN_CHECK_LAUNCH();
     }
     if (c_amax != nullptr && !c_amax_fused) {
@@ -540,7 +594,8 @@ extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N
                0, 0, 0, 0, a_amax, b_amax, nullptr, add0, idx0, ld0, add1, idx1, ld1};
     g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;
     if (g.kchunk == 0) g.kchunk = pl.bk;
-    launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles, 1), s, g);
+    if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, M, N), s, g);
+    else launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles, 1), s, g);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

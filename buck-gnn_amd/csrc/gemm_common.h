@@ -47,6 +47,13 @@ struct X6Cfg {
 extern const X6Cfg kX6Cfgs[];
 extern const int kNumX6Cfgs;
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
+// f16x3 with LDS-DMA staging (gemm_h3g.hip): h3g_ok = the shape and operands qualify (ta 0,
+// tb 1, dense 16-B aligned A and B, K % 32 == 0, no split-K, scales supplied); launches
+// variant `variant` on the grid of h3g_tiles(variant, M, N) output tiles
+bool h3g_ok(const GemmArgs& g, int ta, int tb);
+int64_t h3g_tiles(int variant, int64_t M, int64_t N);
+void launch_h3g(int variant, int64_t tiles, hipStream_t s, const GemmArgs& g);
+constexpr int kNumH3gVariants = 2;
 // folds max |P| over the rows x cols matrix (ld; plane-split by blk / pstride when blk > 0)
 // into *out (f32 bits, unsigned atomic max; *out must hold a non-negative value)
 void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64_t blk, int64_t pstride,

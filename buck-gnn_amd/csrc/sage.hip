@@ -381,6 +381,76 @@ int rows_nt() { return g_rows_nt; }
 
 using namespace bgnn;
 
+// ---------------------------------------------------------------------------
+// Output-gradient prep of a dense Linear (the encoder MLP's LinearFn.backward,
+// Models/BuckGNN.py:67-74) in one pass over g [N, C]: the fused ReLU's mask
+// (g_out = y > 0 ? g : 0; y = NULL: no mask, g_out = NULL: not written), per-block column sums for the bias gradient
+// (part[blk][0][c], the layout bgnn_reduce_partials reads) and max|g_out| folded into *amax.
+// C4 = C / 4 threads per row (a power of two dividing 256), 256 / C4 rows per block step; the
+// column sums are reduced over the block's threads in a fixed order.
+constexpr int kPrepBlocks = 1024;
+
+__global__ __launch_bounds__(256) void k_linear_bwd_prep(const float4* __restrict__ g, const float4* __restrict__ y,
+                                                         int64_t N, int C4, float4* __restrict__ gout,
+                                                         float* __restrict__ part, uint32_t* __restrict__ amax) {
+    __shared__ float4 red[256];
+    const int t = threadIdx.x;
+    const int rpi = 256 / C4;
+    const int c4 = t % C4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * rpi + t / C4; r < N; r += (int64_t)gridDim.x * rpi) {
+        float4 v = g[r * C4 + c4];
+        if (y) {
+            const float4 q = y[r * C4 + c4];
+            v.x = q.x > 0.f ? v.x : 0.f;
+            v.y = q.y > 0.f ? v.y : 0.f;
+            v.z = q.z > 0.f ? v.z : 0.f;
+            v.w = q.w > 0.f ? v.w : 0.f;
+        }
+        if (gout) gout[r * C4 + c4] = v;
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+        m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                       max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+    }
+    red[t] = acc;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    if ((t & 63) == 0 && m) atomicMax(amax, m);
+    __syncthreads();
+    if (t < C4) {
+        float4 s4 = red[t];
+        for (int k = 1; k < rpi; ++k) {
+            const float4 q = red[t + k * C4];
+            s4.x += q.x;
+            s4.y += q.y;
+            s4.z += q.z;
+            s4.w += q.w;
+        }
+        reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * (4 * C4))[t] = s4;
+    }
+}
+
+extern "C" int32_t bgnn_linear_bwd_prep_slots(void) { return kPrepBlocks; }
+
+extern "C" int bgnn_linear_bwd_prep(const float* g, const float* y, int64_t N, int32_t C, float* g_out,
+                                    float* partial, float* amax, void* stream) {
+    BGNN_REQUIRE(g && partial && amax && N >= 0, "linear_bwd_prep: null pointer or negative size");
+    BGNN_REQUIRE(y == nullptr || g_out != nullptr, "linear_bwd_prep: a ReLU mask needs g_out");
+    BGNN_REQUIRE(C >= 4 && C <= 1024 && C % 4 == 0 && (256 % (C / 4)) == 0,
+                 "linear_bwd_prep: C = %d must be 4 * a power of two <= 1024", C);
+    BGNN_REQUIRE((((uintptr_t)g | (uintptr_t)(g_out ? g_out : g) | (uintptr_t)partial | (uintptr_t)(y ? y : g)) & 15) == 0,
+                 "linear_bwd_prep: pointers must be 16-B aligned");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_linear_bwd_prep, dim3(kPrepBlocks), dim3(256), 0, s, reinterpret_cast<const float4*>(g),
+                       reinterpret_cast<const float4*>(y), N, C / 4, reinterpret_cast<float4*>(g_out), partial,
+                       reinterpret_cast<uint32_t*>(amax));
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
 extern "C" int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H, float* out0, float* out1,
                                     int32_t accumulate, void* stream) {
     BGNN_REQUIRE(partial && H > 0 && n_slots >= 0, "reduce_partials: bad args");

@@ -18,6 +18,7 @@
 // `chunk`-edge pieces in k_seg_chunk, then combined in chunk order
 // (k_seg_combine) — deterministic, no atomics.
 #include "common.h"
+#include "gemm_common.h"
 
 namespace bgnn {
 
@@ -1148,6 +1149,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_GEMM_MODE: return gemm_mode();
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
+        case BGNN_TUNE_GEMM_STAGING: return gemm_staging();
         default: return -1;
     }
 }
@@ -1176,6 +1178,12 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: gemm mode must be 0 (f32), 1 (bf16x6) or 2 (f16x3)");
             set_gemm_mode(value);
+            return BGNN_OK;
+        case BGNN_TUNE_GEMM_STAGING:
+            BGNN_REQUIRE((value >= -1 && value < kNumH3gVariants) || (value > 10 && value < 15) || value == 24,
+                         "set_tuning: gemm staging must be -1 (registers) or an LDS-DMA variant 0..%d",
+                         kNumH3gVariants - 1);
+            set_gemm_staging(value);
             return BGNN_OK;
         default: return fail(BGNN_E_ARG, "set_tuning: unknown knob %d", knob);
     }

@@ -69,6 +69,9 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (default) */
 #define BGNN_TUNE_ROWS_NT 6      /* non-temporal stores in sage_apply / sage_bwd_rows (0/1)   */
 #define BGNN_TUNE_GROUP_BLOCKS 7 /* row-group kernel grid in blocks (default 1024)            */
+#define BGNN_TUNE_GEMM_STAGING 8 /* f16x3 operand staging: -1 = registers (gemm_x6), 0..1 =
+                                    LDS-DMA kernel variant (gemm_h3g) for tall K-contiguous
+                                    products                                                 */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);
@@ -220,6 +223,15 @@ int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, cons
 /* Reduce [n_slots, 2, H] partials (fp64) into out0[H], out1[H] (either may be NULL;
  * accumulate=1 adds into the outputs). The partial buffer is used as scratch and
  * its contents are undefined afterwards (also for bgnn_bn_finalize). */
+/* Output-gradient prep of a dense Linear with fused ReLU (LinearFn.backward of the encoder
+ * MLP; replaces torch's threshold_backward, g.sum(0) and a max|g| pass, Models/BuckGNN.py:67-74):
+ * g_out = y > 0 ? g : 0 (y NULL: no mask; g_out may then be NULL: not written), column partial sums of g_out into
+ * partial[bgnn_linear_bwd_prep_slots()][2][C] (first half of each slot; reduce them with
+ * bgnn_reduce_partials), max|g_out| folded into *amax (f32 bits, unsigned atomic max; *amax must
+ * hold a non-negative value). Row-major [N, C], C = 4 * a power of two <= 1024, 16-B aligned. */
+int32_t bgnn_linear_bwd_prep_slots(void);
+int bgnn_linear_bwd_prep(const float* g, const float* y, int64_t N, int32_t C, float* g_out,
+                         float* partial, float* amax, void* stream);
 int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
                          float* out0, float* out1, int32_t accumulate, void* stream);
 

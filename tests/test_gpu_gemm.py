@@ -221,3 +221,55 @@ def test_gemm_bf16_precision(dev, ta, tb, mnk):
     B = B.t() if tb else B
     r, mag = A @ B, A.abs() @ B.abs()
     assert ((c.double().cpu() - r).abs() / mag).max().item() < 2e-6
+
+
+STAGING = 8   # BGNN_TUNE_GEMM_STAGING
+
+
+def _staged(a, b, v, **kw):
+    """fused.gemm under staging knob v (-1 = register-staged gemm_x6, >= 0 = LDS-DMA variant),
+    output pre-filled with NaN (an element the kernel never writes fails)."""
+    old = _lib.query("bgnn_get_tuning", STAGING)
+    _lib.call("bgnn_set_tuning", STAGING, v)
+    try:
+        out = kw.pop("out", None)
+        c = torch.full((a.size(0), b.size(0)), float("nan"), device=a.device) if out is None else out
+        fused.gemm(a, b, False, True, out=c, **kw)
+        return c
+    finally:
+        _lib.call("bgnn_set_tuning", STAGING, old)
+
+
+@pytest.mark.parametrize("mnk", [(4096, 256, 32), (5000, 1000, 512), (10082, 1024, 512), (4500, 512, 1024),
+                                 (4097, 300, 96)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gemm_lds_dma_staging_bit_identical(dev, mnk, variant):
+    """The LDS-DMA staged f16x3 kernel (gemm_h3g.hip) splits the same operand pieces and issues
+    the same MFMAs in the same order as the register-staged one: bit-identical C (ragged M / N
+    edge tiles included), with bias + ReLU + c_amax in the epilogue and beta accumulation."""
+    M, N, K = mnk
+    torch.manual_seed(M + N + K + variant)
+    a = torch.randn(M, K, device=dev)
+    b = torch.randn(N, K, device=dev) * 0.05
+    bias = torch.randn(N, device=dev)
+    c_ref = _staged(a, b, -1)
+    c = _staged(a, b, variant)
+    assert bool(torch.isfinite(c).all())
+    torch.testing.assert_close(c, c_ref, rtol=0, atol=0)
+    r = a.double() @ b.double().t()
+    assert ((c.double() - r).abs().max() / (a.abs().double() @ b.abs().double().t()).max()).item() < 1e-6
+    amax = [torch.zeros(1, device=dev) for _ in range(2)]
+    c1 = _staged(a, b, -1, bias=bias, relu=True, c_amax=amax[0])
+    c2 = _staged(a, b, variant, bias=bias, relu=True, c_amax=amax[1])
+    torch.testing.assert_close(c2, c1, rtol=0, atol=0)
+    assert amax[0].item() == amax[1].item() == c1.abs().max().item()
+    c0 = torch.randn(M, N, device=dev)
+    c1 = _staged(a, b, -1, out=c0.clone(), beta=1.0)
+    c2 = _staged(a, b, variant, out=c0.clone(), beta=1.0)
+    torch.testing.assert_close(c2, c1, rtol=0, atol=0)
+
+
+def test_gemm_staging_knob_range():
+    assert _lib.query("bgnn_get_tuning", STAGING) in (-1, 0, 1)
+    with pytest.raises(Exception):
+        _lib.call("bgnn_set_tuning", STAGING, 2)

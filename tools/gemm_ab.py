@@ -1,0 +1,69 @@
+#!/usr/bin/env python
+"""A/B of the f16x3 GEMM staging variants on the SAGE layer shapes, in one process: the
+register-staged kernel (staging -1) against the LDS-DMA variants, each timed over REPS launches
+with HIP events with operand maxima supplied (as inside the layer: no absmax passes), with a
+1 GiB cache flush between launches (cold L2 / Infinity Cache, as inside a training step).
+
+    python tools/gemm_ab.py [--reps 20] [--variants=-1,0,1,x5] [--shapes fwd,dgrad]
+
+A variant "xC" runs the register-staged kernel on tile config C (bgnn_gemm_set_cfg).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+import torch  # noqa: E402
+
+from bgnn import _lib, fused  # noqa: E402
+
+SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872, 512, 512),
+          "fwd_small": (10082, 1024, 512)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--variants", default="-1,0,1,2")
+    ap.add_argument("--shapes", default="fwd,dgrad")
+    ap.add_argument("--no-flush", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    flush = None if args.no_flush else torch.empty(1 << 28, device=dev)
+    for name in args.shapes.split(","):
+        M, N, K = SHAPES[name]
+        torch.manual_seed(0)
+        a = torch.randn(M, K, device=dev)
+        b = torch.randn(N, K, device=dev) * 0.05
+        am = torch.stack([a.abs().max(), b.abs().max()]).contiguous()
+        out = torch.empty(M, N, device=dev)
+        ref = None
+        for vs in args.variants.split(","):
+            v = -1 if vs.startswith("x") else int(vs)
+            _lib.call("bgnn_set_tuning", 8, v)
+            _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if vs.startswith("x") else -1)
+            ts = []
+            for i in range(args.reps + 3):
+                if flush is not None:
+                    flush.fill_(float(i))
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
+                e1.record()
+                ts.append((e0, e1))
+            torch.cuda.synchronize()
+            us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in ts[3:])
+            med = us[len(us) // 2]
+            same = "" if ref is None else ("bit-identical" if torch.equal(out, ref) else
+                                           f"DIFFERS max {(out - ref).abs().max().item():.3g}")
+            if ref is None:
+                ref = out.clone()
+            print(f"{name:9s} {M}x{N}x{K} staging {vs:>3s}: median {med:7.1f} us  min {us[0]:7.1f}  "
+                  f"{2 * M * N * K / med / 1e6:6.1f} TF  {same}", flush=True)
+        _lib.call("bgnn_set_tuning", 8, -1)
+        _lib.call("bgnn_gemm_set_cfg", -1)
+
+
+if __name__ == "__main__":
+    main()
