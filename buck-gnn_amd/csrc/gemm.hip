@@ -311,15 +311,7 @@ inline int pick_cfg(int64_t M, int64_t N, int64_t K, int ta, int tb) {
 inline int choose_split(int64_t M, int64_t N, int64_t K, const GemmCfg& c) {
     const int64_t tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
     const int64_t slots = 256 * c.blocks_per_cu;          // resident workgroups on the chip
-    if (tiles >= slots / 2) return 1;
-    if (K < 4 * 256) {
-        // a handful of tiles over a few hundred of K (the folded layer's weight-by-weight
-        // products: 8 tiles, K = 512): >= 64-deep slices, so dozens of workgroups share them
-        if (tiles > 16 || K < 128) return 1;
-        int64_t s = (slots + tiles - 1) / tiles;
-        if (s > K / 64) s = K / 64;
-        return s < 1 ? 1 : (int)s;
-    }
+    if (tiles >= slots / 2 || K < 4 * 256) return 1;
     int64_t s = (slots + tiles - 1) / tiles;
     const int64_t smax = K / 256;   // keep >= 256 of K per slice
     if (s > smax) s = smax;

@@ -388,7 +388,7 @@ using namespace bgnn;
 // (part[blk][0][c], the layout bgnn_reduce_partials reads) and max|g_out| folded into *amax.
 // C4 = C / 4 threads per row (a power of two dividing 256), 256 / C4 rows per block step; the
 // column sums are reduced over the block's threads in a fixed order.
-constexpr int kPrepBlocks = 1024;
+constexpr int kPrepBlocks = 512;
 
 __global__ __launch_bounds__(256) void k_linear_bwd_prep(const float4* __restrict__ g, const float4* __restrict__ y,
                                                          int64_t N, int C4, float4* __restrict__ gout,
@@ -417,9 +417,15 @@ __global__ __launch_bounds__(256) void k_linear_bwd_prep(const float4* __restric
                        max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
     }
     red[t] = acc;
+    // one atomic per block (same-address atomics serialise in L2)
+    __shared__ uint32_t wmax[4];
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
-    if ((t & 63) == 0 && m) atomicMax(amax, m);
+    if ((t & 63) == 0) wmax[t >> 6] = m;
     __syncthreads();
+    if (t == 0) {
+        m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m) atomicMax(amax, m);
+    }
     if (t < C4) {
         float4 s4 = red[t];
         for (int k = 1; k < rpi; ++k) {

@@ -39,3 +39,121 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def weight_products(name="GraphSage_addAggr_Shared"):
+    """The folded weight-by-weight products on the model's own parameters against fp64."""
+    import bgnn
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = bgnn.BuckGNN(16, 5, hidden_channels=512, num_layers=6, dropout_rate=0.0, model_name=name).to(dev)
+    blk = m.shared_graphsage_block if name.endswith("Shared") else m.sage_blocks[0]
+    wcat = torch.cat([blk.lin_l.weight, blk.lin_r.weight], 0).detach().contiguous()
+    w_in, b_in = m.node_encoder[4].weight.detach(), m.node_encoder[4].bias.detach()
+
+    def err(c, r, mag):
+        return ((c.double() - r).abs() / mag.clamp_min(1e-300)).max().item()
+    wf = fused.gemm(wcat, w_in.contiguous(), False, False)
+    print("wf", err(wf, wcat.double() @ w_in.double(), wcat.abs().double() @ w_in.abs().double()))
+    bf = fused.gemm(wcat, b_in.contiguous().view(-1, 1), False, False).view(-1)
+    print("bf", err(bf, wcat.double() @ b_in.double(), wcat.abs().double() @ b_in.abs().double()))
+
+
+if __name__ == "__main__" and os.environ.get("FOLD_WEIGHTS_CHECK"):
+    weight_products()
+
+
+def bisect(name="GraphSage_addAggr_Shared"):
+    """Which folded weight product moves the gradients: route one group of them at a time to
+    torch.mm (by shape) and report the mean relative error against fp64."""
+    dev = torch.device("cuda", 0)
+    orig = fused.gemm
+    groups = {"none": set(), "wf,bf": {(1024, 128, 512), (1024, 1, 512)}, "dw": {(1024, 512, 128)},
+              "dw_in,db_in": {(512, 128, 1024), (512, 1, 1024)}}
+
+    def make(route):
+        def g(a, b, trans_a, trans_b, **kw):
+            M = a.size(1) if trans_a else a.size(0)
+            K = a.size(0) if trans_a else a.size(1)
+            N = b.size(0) if trans_b else b.size(1)
+            if (M, N, K) in route and not kw:
+                return torch.mm(a.t() if trans_a else a, b.t() if trans_b else b)
+            return orig(a, b, trans_a, trans_b, **kw)
+        return g
+    fused.FOLD_WEIGHTS_TORCH = False
+    out = {}
+    for gname, route in groups.items():
+        fused.gemm = make(route)
+        b, sd, _, g = T.run(dev, name, 512, True)
+        out[gname] = g
+    fused.gemm = orig
+    exact = T.oracle_grads(b, sd, name)
+    for gname, g in out.items():
+        errs = [T.rel_err(g[k], exact[k]) for k in exact]
+        print(f"torch for {gname:12s}: mean rel err {sum(errs) / len(errs):.2e} max {max(errs):.2e}")
+
+
+if __name__ == "__main__" and os.environ.get("FOLD_BISECT"):
+    bisect()
+
+
+def inmodel(name="GraphSage_addAggr_Shared"):
+    """bgnn vs fp64 for the folded forward products as called inside the model."""
+    dev = torch.device("cuda", 0)
+    orig = fused.gemm
+
+    def g(a, b, trans_a, trans_b, **kw):
+        c = orig(a, b, trans_a, trans_b, **kw)
+        M = a.size(1) if trans_a else a.size(0)
+        N = b.size(0) if trans_b else b.size(1)
+        if M <= 1024 and N <= 1024 and not kw:
+            A = a.double().t() if trans_a else a.double()
+            B = b.double().t() if trans_b else b.double()
+            torch.cuda.synchronize()
+            e = ((c.double() - A @ B).abs() / (A.abs() @ B.abs()).clamp_min(1e-300)).max().item()
+            print(f"  gemm {tuple(a.shape)} x {tuple(b.shape)} ta={trans_a} tb={trans_b}: {e:.2e}"
+                  f" a contiguous {a.is_contiguous()} b contiguous {b.is_contiguous()} strides {a.stride()} {b.stride()}")
+        return c
+    fused.gemm = g
+    T.run(dev, name, 512, True)
+    fused.gemm = orig
+
+
+if __name__ == "__main__" and os.environ.get("FOLD_INMODEL"):
+    inmodel()
+
+
+def relu_flips(name="GraphSage_addAggr_Shared"):
+    """Layer outputs x_next of the folded path with Wf, bf on bgnn vs on torch.mm: how many
+    elements sit on different sides of ReLU's kink (x_next == 0 in one run, > 0 in the other)."""
+    from bgnn import buckgnn
+    dev = torch.device("cuda", 0)
+    orig_layer, orig_gemm = buckgnn.sage_layer, fused.gemm
+    outs = {}
+
+    def rec(tag):
+        def f(*a, **kw):
+            r = orig_layer(*a, **kw)
+            outs.setdefault(tag, []).append((r[0] if isinstance(r, tuple) else r).detach().clone())
+            return r
+        return f
+
+    def torch_small(a, b, trans_a, trans_b, **kw):
+        M = a.size(1) if trans_a else a.size(0)
+        N = b.size(0) if trans_b else b.size(1)
+        if M <= 1024 and N <= 128 and not kw:
+            return torch.mm(a.t() if trans_a else a, b.t() if trans_b else b)
+        return orig_gemm(a, b, trans_a, trans_b, **kw)
+    for tag in ("bgnn", "torch"):
+        buckgnn.sage_layer = rec(tag)
+        fused.gemm = torch_small if tag == "torch" else orig_gemm
+        T.run(dev, name, 512, True)
+    buckgnn.sage_layer, fused.gemm = orig_layer, orig_gemm
+    for i, (u, v) in enumerate(zip(outs["bgnn"], outs["torch"])):
+        flips = int(((u == 0) != (v == 0)).sum())
+        rel = ((u - v).norm() / v.norm()).item()
+        print(f"layer {i}: x_next rel diff {rel:.2e}, ReLU side flips {flips} of {u.numel()}")
+
+
+if __name__ == "__main__" and os.environ.get("FOLD_FLIPS"):
+    relu_flips()
