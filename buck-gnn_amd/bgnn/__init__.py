@@ -16,6 +16,9 @@ from .store import GraphStore
 from .checkpoint import load_checkpoint, load_reference_checkpoint, save_checkpoint
 from .inference import evaluate
 from .train import EigenvalueScaler, GradAllReduce, RelativeErrorLoss, mape_error, train_step
+from . import losses
+from .losses import (GraphMAELoss, GraphMaxComponentRelativeError, GraphMixedError, GraphMSELoss,
+                     GraphRelativeError, stress_errors)
 
 __all__ = [
     "BuckGNN", "GraphNetBlock", "MLPPooling", "Batch", "Data", "DataLoader", "Graph", "SegmentIndex",
@@ -23,7 +26,8 @@ __all__ = [
     "global_mean_pool", "scatter_add", "scatter_mean", "scatter_sum", "aggregate", "segment_reduce",
     "install_pyg_shim", "uninstall_pyg_shim", "EigenvalueScaler", "GradAllReduce", "RelativeErrorLoss",
     "mape_error", "train_step", "load_library", "GraphStore", "load_checkpoint", "load_reference_checkpoint",
-    "save_checkpoint", "evaluate",
+    "save_checkpoint", "evaluate", "losses", "GraphMAELoss", "GraphMaxComponentRelativeError", "GraphMixedError",
+    "GraphMSELoss", "GraphRelativeError", "stress_errors",
 ]
 
 
