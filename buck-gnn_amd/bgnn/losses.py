@@ -6,7 +6,8 @@ boolean mask per graph (`Utils/Losses.py:303-507`, `Dataset_Preparation/Metrics.
 one host sync plus O(B) small kernels per graph and call. Here every per-graph quantity is a
 segment reduction over the batch vector (`index_add_` / `scatter_reduce_` over graph ids, ragged
 per-graph quantiles as one `nanquantile` over a NaN-padded [B, max_len] view), so a call costs
-a fixed handful of device ops and no host syncs beyond the final `.item()`s the metrics return.
+a fixed handful of device ops, independent of B, and one host sync for the graph count (one
+more for the padded width where a quantile is taken).
 Results equal the reference's (tests/test_losses.py against the reference's own classes:
 tests/golden/heads/losses.npz, made by tests/golden/make_golden_losses.py).
 
