@@ -8,7 +8,7 @@ from . import _lib
 from .buckgnn import BuckGNN, GraphNetBlock, MLPPooling
 from .data import Batch, Data, DataLoader
 from .graph import Graph, SegmentIndex, clear_caches, graph_for, prepare, segments_for
-from .nn import (SAGEConv, global_add_pool, global_max_pool, global_mean_pool, scatter_add, scatter_mean,
+from .nn import (SAGEConv, SAGPooling, global_add_pool, global_max_pool, global_mean_pool, scatter_add, scatter_mean,
                  scatter_sum)
 from .ops import aggregate, segment_reduce
 from .pyg_shim import install_pyg_shim, uninstall_pyg_shim
@@ -22,7 +22,7 @@ from .losses import (GraphMAELoss, GraphMaxComponentRelativeError, GraphMixedErr
 
 __all__ = [
     "BuckGNN", "GraphNetBlock", "MLPPooling", "Batch", "Data", "DataLoader", "Graph", "SegmentIndex",
-    "clear_caches", "graph_for", "prepare", "segments_for", "SAGEConv", "global_add_pool", "global_max_pool",
+    "clear_caches", "graph_for", "prepare", "segments_for", "SAGEConv", "SAGPooling", "global_add_pool", "global_max_pool",
     "global_mean_pool", "scatter_add", "scatter_mean", "scatter_sum", "aggregate", "segment_reduce",
     "install_pyg_shim", "uninstall_pyg_shim", "EigenvalueScaler", "GradAllReduce", "RelativeErrorLoss",
     "mape_error", "train_step", "load_library", "GraphStore", "load_checkpoint", "load_reference_checkpoint",

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lock = threading.Lock()
 _lib = None
@@ -96,6 +96,12 @@ SIGNATURES = {
     "bgnn_absmax_f32": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p]),
     "bgnn_gemm_f32_ex": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p,
                                  c_i64, c_p, c_i32, c_p, c_sz, c_p]),
+    "bgnn_topk_rank": (c_i32, [c_p, c_p, c_p, c_i64, c_p, c_p]),
+    "bgnn_topk_select": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "bgnn_gather_scale": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_i64, c_p, c_i64, c_p]),
+    "bgnn_gather_scale_bwd": (c_i32, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p]),
+    "bgnn_filter_edges_ws_bytes": (c_sz, [c_i64]),
+    "bgnn_filter_edges": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,
                               c_p, c_sz, c_p]),
 }

@@ -7,9 +7,11 @@ Variants and where their loop is defined in the reference:
     GraphSage_addAggr_Shared (TRAIN_FINAL default)  :338-352 -> fused (no BN)
     GraphSage_maxAggr                               :459-471 -> per-op (bgnn SAGEConv max + torch BN)
     EA_GNN / EA_GNN_Shared                          :326-336,375-387 -> per-op (GraphNetBlock on bgnn scatter_mean)
-    GraphSage_MLP / *_woBatchNorm / GraphSAGE_SAG / EAGNN_SAG -> reproduce the reference's behaviour
-      (AttributeError for the first three: their ModuleLists are never built, :404-429,472-492;
-       SAG variants need SAGPooling, out of scope).
+    GraphSAGE_SAG                                   :190-217,493-511 -> fused SAGE layers (skip added
+                                                       after dropout), SAGPooling on bgnn kernels
+    EAGNN_SAG                                       :219-244,354-373 -> GraphNetBlocks + SAGPooling
+    GraphSage_MLP / *_woBatchNorm -> reproduce the reference's behaviour (AttributeError: their
+      ModuleLists are never built, :404-429,472-492).
 Pooling (get_pooling_layer, :246-307) is vectorised: the reference's per-node Python
 loop over `batch` (:256-271) is `last index of every run of equal batch ids`.
 """
@@ -156,8 +158,19 @@ class BuckGNN(nn.Module):
         self.relu = nn.ReLU()
         self.dropout = nn.Dropout(p=dropout_rate)
         self.pooling_mpl = MLPPooling(h, h, h)
-        if model_name in ("GraphSAGE_SAG", "EAGNN_SAG"):
-            self.pool = SAGPooling(h, ratio=0.5)  # raises: out of scope
+        if model_name in ("GraphSAGE_SAG", "EAGNN_SAG"):   # Models/BuckGNN.py:190-244
+            n_before = num_layers // 2
+            n_after = num_layers - n_before
+            sag = model_name == "GraphSAGE_SAG"
+            pre, bns = ("sage_layers_", True) if sag else ("gnn_layers_", False)
+
+            def block():
+                return SAGEConv(h, h, normalize=True, aggr="add") if sag else GraphNetBlock(h)
+            setattr(self, pre + "1", nn.ModuleList([block() for _ in range(n_before)]))
+            self.batch_norms_1 = nn.ModuleList([nn.BatchNorm1d(h) for _ in range(n_before)] if bns else [])
+            self.pool = SAGPooling(h, ratio=0.5, GNN=SAGEConv, aggr="add")
+            setattr(self, pre + "2", nn.ModuleList([block() for _ in range(n_after)]))
+            self.batch_norms_2 = nn.ModuleList([nn.BatchNorm1d(h) for _ in range(n_after)] if bns else [])
         # fused-path switch (tests compare both paths)
         self.use_fused = True
         # EA_GNN GEMM precision on the fused path: False = f32-accurate (f16x3), True = bf16
@@ -249,6 +262,36 @@ class BuckGNN(nn.Module):
             x = self.dropout(x)
         return x
 
+    def _sag_sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, first_skip: bool,
+                       x_amax: Optional[Tensor] = None, x_in: Optional[nn.Linear] = None) -> Tensor:
+        """GraphSAGE_SAG's layer loops (Models/BuckGNN.py:494-501 with first_skip=False,
+        :505-511 with first_skip=True): conv -> BN -> ReLU -> Dropout, then + identity. The
+        fused layer computes the first four (no skip inside: here the skip follows dropout)."""
+        p = self.dropout.p
+        if self._sage_fused(x, "add"):
+            graph = graph_for(edge_index, x.size(0))
+            bufs = torch.zeros(len(convs), 3, dtype=torch.float32, device=x.device)
+            for i, (conv, bn) in enumerate(zip(convs, bns)):
+                skip = first_skip or i > 0
+                fold = x_in if i == 0 else None
+                y, y_amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, 0,
+                                       False, p, self.training, self._seed(), x_amax=x_amax, return_amax=True,
+                                       amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
+                                       b_in=None if fold is None else fold.bias)
+                x, x_amax = (y + x, None) if skip else (y, y_amax)
+            return x
+        if x_in is not None:
+            x = x_in(x)
+        for i, (conv, bn) in enumerate(zip(convs, bns)):
+            identity = x
+            x = self.dropout(self.relu(bn(conv(x, edge_index))))
+            if first_skip or i > 0:
+                x = x + identity
+        return x
+
+    def _ea_block(self, blk, x, e, edge_index, fused: bool):
+        return graphnet_block(blk, x, e, edge_index, self.ea_bf16) if fused else blk(x, edge_index, e)
+
     def forward(self, x, edge_index, edge_attr, batch=None, mask=None):
         name = self.model_name
         if "super" in self.pooling_layer:
@@ -258,15 +301,15 @@ class BuckGNN(nn.Module):
         x_amax = None   # max|x| after the encoder (f16x3 operand scale of the first SAGE GEMM)
         x_in = None     # the encoder's last Linear when it is folded into the first SAGE layer
         sage = _SAGE_VARIANTS.get(name, (None, "add", None))[1] if name != "GraphSage_addAggr_Shared" else "add"
-        if (name in _SAGE_VARIANTS or name == "GraphSage_addAggr_Shared") and self._sage_fused(x, sage) \
-                and self._foldable_encoder(x):
+        if (name in _SAGE_VARIANTS or name in ("GraphSage_addAggr_Shared", "GraphSAGE_SAG")) \
+                and self._sage_fused(x, sage) and self._foldable_encoder(x):
             x_in = self.node_encoder[-1]
             x, x_amax = mlp(self.node_encoder[:-1], x, return_amax=True)
         elif self._fused_ok(x) and x.size(0) >= 1024 and FUSED_ENCODER:
             x, x_amax = mlp(self.node_encoder, x, return_amax=True)   # GEMMs with fused bias+ReLU epilogues
         else:
             x = self.node_encoder(x)
-        ea_fused = name in ("EA_GNN", "EA_GNN_Shared") and self._fused_ok(x)
+        ea_fused = name in ("EA_GNN", "EA_GNN_Shared", "EAGNN_SAG") and self._fused_ok(x)
         if ea_fused:
             e = (mlp(self.edge_encoder, edge_attr) if edge_attr.size(0) >= 1024 and FUSED_ENCODER
                  else self.edge_encoder(edge_attr))
@@ -304,8 +347,25 @@ class BuckGNN(nn.Module):
             getattr(self, "sage_blocks_add")  # AttributeError, as in the reference (:405,473)
         elif name == "GraphSage_sumAggr_woBatchNorm":
             getattr(self, "sage_blocks_sum")  # AttributeError, as in the reference (:418)
-        elif name in ("GraphSAGE_SAG", "EAGNN_SAG"):
-            raise NotImplementedError(f"{name}: SAGPooling variants are out of scope")
+        elif name == "GraphSAGE_SAG":   # Models/BuckGNN.py:493-511
+            x = self._sag_sage_loop(x, edge_index, self.sage_layers_1, self.batch_norms_1, False, x_amax, x_in)
+            x, edge_index, edge_attr, batch, _perm, _score = self.pool(x, edge_index, edge_attr, batch)
+            x = self._sag_sage_loop(x, edge_index, self.sage_layers_2, self.batch_norms_2, True)
+        elif name == "EAGNN_SAG":       # Models/BuckGNN.py:354-373
+            if not ea_fused:
+                e = self.edge_encoder(edge_attr)
+            for i, blk in enumerate(self.gnn_layers_1):
+                x_prev, e_prev = x, e
+                x, e = self._ea_block(blk, x, e, edge_index, ea_fused)
+                x, e = self.dropout(x), self.dropout(e)
+                if i > 0:
+                    x, e = x + x_prev, e + e_prev
+            x, edge_index, e, batch, _perm, _score = self.pool(x, edge_index, e, batch)
+            for blk in self.gnn_layers_2:
+                x_prev, e_prev = x, e
+                x, e = self._ea_block(blk, x, e, edge_index, ea_fused)
+                x, e = self.dropout(x), self.dropout(e)
+                x, e = x + x_prev, e + e_prev
 
         if self.prediction_type == "buckling":
             pooled = self.get_pooling_layer(x, edge_index, batch)

@@ -83,7 +83,14 @@ class SAGEConv(nn.Module):
         if self.project:
             x_src = F.relu(self.lin(x_src))
         graph = graph_for(edge_index, x_src.size(0))
-        out = self.lin_l(aggregate(x_src, graph, self.aggr))
+        if self.aggr in ("add", "sum", "mean") and 2 * self.out_channels <= self.in_channels[0]:
+            # narrow output (e.g. SAGPooling's 1-channel scorer): transform first, then aggregate
+            # the narrow rows -- lin_l(AGG x) = AGG(x W_l^T) + b_l, since sum / mean are linear
+            out = aggregate(F.linear(x_src, self.lin_l.weight), graph, self.aggr)
+            if self.lin_l.bias is not None:
+                out = out + self.lin_l.bias
+        else:
+            out = self.lin_l(aggregate(x_src, graph, self.aggr))
         if self.root_weight and x_dst is not None:
             out = out + self.lin_r(x_dst)
         if self.normalize:
@@ -154,10 +161,70 @@ def scatter_mean(src: Tensor, index: Tensor, dim: int = 0, out: Optional[Tensor]
     return _scatter(src, index, dim, out, dim_size, "mean")
 
 
-class SAGPooling(nn.Module):
-    """Placeholder for torch_geometric.nn.SAGPooling (GraphSAGE_SAG / EAGNN_SAG variants,
-    Models/BuckGNN.py:190-244). Not part of the hot path."""
+class _SelectTopK(nn.Module):
+    """The scoring projection of PyG's SelectTopK(in_channels=1) inside SAGPooling: weight
+    [1, 1], score = act((attn * w).sum(-1) / ||w||) = act(sign(w) * attn). PyG releases
+    before the select/connect refactor have no such weight (score = act(attn)); their
+    checkpoints load with w = 1, which is the same function."""
 
-    def __init__(self, *args, **kwargs):
+    def __init__(self):
         super().__init__()
-        raise NotImplementedError("bgnn: SAGPooling is not implemented (out of the hot-path scope)")
+        self.weight = nn.Parameter(torch.empty(1, 1))
+        with torch.no_grad():
+            self.weight.uniform_(-1.0, 1.0)   # PyG: uniform(in_channels=1, weight)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        if prefix + "weight" not in state_dict:
+            state_dict[prefix + "weight"] = torch.ones(1, 1)
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+
+class SAGPooling(nn.Module):
+    """torch_geometric.nn.SAGPooling in the form the reference builds it for GraphSAGE_SAG /
+    EAGNN_SAG (Models/BuckGNN.py:203-208,231-236: `SAGPooling(h, ratio=0.5, GNN=SAGEConv,
+    aggr='add')`, called at :364,502) [PyG-doc]:
+
+        attn  = GNN(x, edge_index)                     [N, 1] (bgnn SAGEConv, HIP aggregation)
+        score = tanh(sign(w) * attn)                   select.weight w
+        perm  = topk(score, ratio, batch)              bgnn_topk_rank / bgnn_topk_select
+        x'    = x[perm] * score[perm] (* multiplier)   bgnn_gather_scale (+ backward)
+        edge_index', edge_attr' = filter_adj(...)      bgnn_filter_edges
+
+    forward returns (x', edge_index', edge_attr', batch', perm, score[perm]). State-dict keys:
+    `gnn.*` (the GNN's own) and `select.weight`. Ties in the score go to the lower node index.
+    Not supported (the reference does not use them): the default GNN (GraphConv) and
+    min_score (softmax selection)."""
+
+    def __init__(self, in_channels: int, ratio: float = 0.5, GNN=None, min_score: Optional[float] = None,
+                 multiplier: float = 1.0, nonlinearity="tanh", **kwargs):
+        super().__init__()
+        if GNN is None:
+            raise NotImplementedError("SAGPooling: pass GNN= explicitly (GraphConv, PyG's default, is not provided)")
+        if min_score is not None:
+            raise NotImplementedError("SAGPooling: min_score (softmax selection) is not supported")
+        if not ratio > 0:
+            raise ValueError(f"SAGPooling: ratio must be > 0 (got {ratio})")
+        self.in_channels = in_channels
+        self.ratio = ratio
+        self.min_score = min_score
+        self.multiplier = multiplier
+        self.nonlinearity = torch.tanh if nonlinearity == "tanh" else nonlinearity
+        if not callable(self.nonlinearity):
+            raise ValueError(f"SAGPooling: unsupported nonlinearity {nonlinearity!r}")
+        self.gnn = GNN(in_channels, 1, **kwargs)
+        self.select = _SelectTopK()
+
+    def forward(self, x: Tensor, edge_index: Tensor, edge_attr: Optional[Tensor] = None,
+                batch: Optional[Tensor] = None, attn: Optional[Tensor] = None):
+        from .pool import sag_pool
+        if batch is None:
+            batch = edge_index.new_zeros(x.size(0))
+        attn = x if attn is None else attn
+        attn = attn.view(-1, 1) if attn.dim() == 1 else attn
+        attn = self.gnn(attn, edge_index)
+        w = self.select.weight
+        score = self.nonlinearity((attn * w).sum(dim=-1) / w.norm(p=2, dim=-1))
+        return sag_pool(x, score, self.ratio, edge_index, edge_attr, batch, self.multiplier)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.gnn.__class__.__name__}, {self.in_channels}, ratio={self.ratio})"

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 3
+#define BGNN_ABI_VERSION 4
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -363,6 +363,40 @@ int bgnn_store_gather_groups(const int64_t* gtable, int32_t B, int32_t group_row
  * row-major store array (row_bytes per row, a multiple of 4) into the batch array. */
 int bgnn_store_gather_rows(const int64_t* table, int32_t B, int32_t per_edge, int64_t max_rows,
                            const void* src, int64_t row_bytes, void* dst, void* stream);
+
+/* ------------------------------------------------------------------------
+ * SAGPooling (torch_geometric.nn.SAGPooling as the reference builds it for GraphSAGE_SAG /
+ * EAGNN_SAG, Models/BuckGNN.py:203-208,231-236, called at :364,502): PyG's
+ * topk(score, ratio, batch) -> x[perm] * score[perm] -> filter_adj(edge_index, perm).
+ * `batch` must be non-decreasing (every PyG Batch is); ptr [B+1] = its graph offsets.
+ *
+ * bgnn_topk_rank: rank[i] = position of node i in its graph's descending score order,
+ *   #{j in graph(i) : s_j > s_i or (s_j == s_i and j < i)} (a stable descending sort;
+ *   O(n_g^2) compares per graph, staged through LDS).
+ * bgnn_topk_select: node i is kept iff rank[i] < k[g] (k[g] = ceil(ratio * n_g), computed by
+ *   the caller in fp32 as PyG does); perm[new_ptr[g] + rank[i]] = i, new_id[i] = that position
+ *   or -1, batch_out[position] = g (optional). new_ptr [B+1] = running sums of k.
+ * bgnn_gather_scale: out[p] = x[perm[p]] * score[perm[p]] ([k, H] rows).
+ * bgnn_gather_scale_bwd: over all n input rows: dx[i] = g[new_id[i]] * score[i] and
+ *   dscore[i] = <g[new_id[i]], x[i]> (zeros for rows that were not kept; dscore optional).
+ * bgnn_filter_edges: the edges whose two ends are kept, in edge_index order, relabelled by
+ *   new_id: out_edges[0 .. 2*n_kept) = [src' | dst'] (capacity 2 * num_edges), kept[pos] =
+ *   original edge position (optional, for edge_attr), *n_kept (device int64).
+ *   Deterministic (no atomics); edges with an end outside [0, num_nodes) are dropped.
+ * ---------------------------------------------------------------------- */
+int bgnn_topk_rank(const float* score, const int64_t* batch, const int64_t* ptr, int64_t n,
+                   int32_t* rank, void* stream);
+int bgnn_topk_select(const int32_t* rank, const int64_t* batch, const int64_t* k, const int64_t* new_ptr,
+                     int64_t n, int64_t* perm, int32_t* new_id, int64_t* batch_out, void* stream);
+int bgnn_gather_scale(const float* x, int64_t ldx, int32_t H, const int64_t* perm, const float* score,
+                      int64_t k, float* out, int64_t ldo, void* stream);
+int bgnn_gather_scale_bwd(const float* g, int64_t ldg, const float* x, int64_t ldx, int32_t H,
+                          const int32_t* new_id, const float* score, int64_t n, float* dx, int64_t lddx,
+                          float* dscore, void* stream);
+size_t bgnn_filter_edges_ws_bytes(int64_t num_edges);
+int bgnn_filter_edges(const int64_t* edge_index, int64_t num_edges, const int32_t* new_id,
+                      int64_t num_nodes, int64_t* out_edges, int64_t* kept, int64_t* n_kept,
+                      void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

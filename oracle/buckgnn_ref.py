@@ -11,6 +11,8 @@ Follows, line for line in meaning:
   loss               Utils/Losses.py:755-761 on Normalizer.py:207-215 denormalised values
   step               TRAIN_FINAL.py:190 (Adam lr, wd), :253-298 (fwd, loss, zero_grad, bwd, step)
   EA_GNN loop        Models/BuckGNN.py:375-387 with GraphNetBlock :528-566 (edge encoder :76-82)
+  SAG variants       Models/BuckGNN.py:493-511 (GraphSAGE_SAG), :354-373 (EAGNN_SAG), with
+                     SAGPooling :203-208,231-236 restated in oracle.pyg_ref (topk, filter_adj)
 The SAGEConv arithmetic is oracle.pyg_ref (gather -> index_add -> lin_l + lin_r -> normalize).
 """
 from __future__ import annotations
@@ -21,7 +23,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor
 
-from .pyg_ref import global_mean_pool, sage_aggregate
+from .pyg_ref import filter_adj, global_mean_pool, sage_aggregate, topk
 
 SAGE = {  # model_name -> (ModuleList attribute, aggr, batchnorm)
     "GraphSage_sumAggr": ("sage_blocks_sum", "sum", True),
@@ -118,6 +120,64 @@ def ea_forward(sd: Dict[str, Tensor], x: Tensor, edge_index: Tensor, edge_attr: 
             x, e = x + x_prev, e + e_prev
         x, e = F.dropout(x, dropout, training), F.dropout(e, dropout, training)
     return _mlp(sd, "decoder", global_mean_pool(x, batch)).squeeze()
+
+
+def sag_pool(sd: Dict[str, Tensor], x: Tensor, edge_index: Tensor, edge_attr: Optional[Tensor],
+             batch: Tensor, ratio: float = 0.5):
+    """SAGPooling(h, ratio, GNN=SAGEConv, aggr='add') at key prefix `pool`: returns
+    (x', edge_index', edge_attr', batch', perm, score[perm])."""
+    agg = sage_aggregate(x, edge_index, "add")
+    attn = F.linear(agg, sd["pool.gnn.lin_l.weight"], sd["pool.gnn.lin_l.bias"]) + \
+        F.linear(x, sd["pool.gnn.lin_r.weight"])
+    w = sd["pool.select.weight"]
+    score = torch.tanh((attn * w).sum(-1) / w.norm(p=2, dim=-1))
+    perm = topk(score, ratio, batch)
+    s = score[perm]
+    ei, ea = filter_adj(edge_index, edge_attr, perm, x.size(0))
+    return x[perm] * s.view(-1, 1), ei, ea, batch[perm], perm, s
+
+
+def sag_forward(sd: Dict[str, Tensor], model_name: str, x: Tensor, edge_index: Tensor, edge_attr: Tensor,
+                batch: Optional[Tensor], training: bool, dropout: float = 0.0, num_layers: int = 6,
+                bn_momentum: float = 0.1, bn_eps: float = 1e-5):
+    """GraphSAGE_SAG / EAGNN_SAG forward with mean pooling: returns (pred, perm)."""
+    x = _mlp(sd, "node_encoder", x)
+    if batch is None:
+        batch = torch.zeros(x.size(0), dtype=torch.long)
+    n1 = num_layers // 2
+    n2 = num_layers - n1
+    if model_name == "GraphSAGE_SAG":
+        def run(x, ei, part, n, first_skip):
+            for i in range(n):
+                identity = x
+                x = sage_conv(sd, f"sage_layers_{part}.{i}", x, ei, "add")
+                b = f"batch_norms_{part}.{i}"
+                x = F.batch_norm(x, sd[b + ".running_mean"], sd[b + ".running_var"], sd[b + ".weight"],
+                                 sd[b + ".bias"], training, bn_momentum, bn_eps)
+                x = F.dropout(F.relu(x), dropout, training)
+                if first_skip or i > 0:
+                    x = x + identity
+            return x
+        x = run(x, edge_index, 1, n1, False)
+        x, edge_index, _, batch, perm, _ = sag_pool(sd, x, edge_index, edge_attr, batch)
+        x = run(x, edge_index, 2, n2, True)
+    elif model_name == "EAGNN_SAG":
+        e = _mlp(sd, "edge_encoder", edge_attr)
+
+        def run(x, e, ei, part, n, first_skip):
+            for i in range(n):
+                x_prev, e_prev = x, e
+                x, e = graphnet_block(sd, f"gnn_layers_{part}.{i}", x, ei, e)
+                x, e = F.dropout(x, dropout, training), F.dropout(e, dropout, training)
+                if first_skip or i > 0:
+                    x, e = x + x_prev, e + e_prev
+            return x, e
+        x, e = run(x, e, edge_index, 1, n1, False)
+        x, edge_index, e, batch, perm, _ = sag_pool(sd, x, edge_index, e, batch)
+        x, e = run(x, e, edge_index, 2, n2, True)
+    else:
+        raise ValueError(model_name)
+    return _mlp(sd, "decoder", global_mean_pool(x, batch)).squeeze(), perm
 
 
 def relative_error_loss(pred: Tensor, target: Tensor, eps: float = 1e-8) -> Tensor:

@@ -109,10 +109,78 @@ class SAGEConv(nn.Module):
         return out
 
 
-class SAGPooling(nn.Module):
-    def __init__(self, *a, **k):
+# ----------------------------------------------------------------------------- SAGPooling
+def topk(score: Tensor, ratio: float, batch: Tensor) -> Tensor:
+    """PyG's topk (torch_geometric.nn.pool.select.topk, ratio < 1 form) [PyG-doc]: per graph
+    the k_g = ceil(ratio * n_g) highest scores (k_g computed in the score dtype), graphs in
+    order, scores descending. PyG's first sort is unstable, so its tie order is unspecified;
+    here both sorts are stable (ties: lower node index first)."""
+    n_graphs = int(batch.max()) + 1 if batch.numel() else 0
+    num_nodes = torch.zeros(n_graphs, dtype=torch.long).index_add_(0, batch, torch.ones_like(batch))
+    k = (float(ratio) * num_nodes.to(score.dtype)).ceil().to(torch.long)
+    _, x_perm = torch.sort(score.view(-1), descending=True, stable=True)
+    b = batch[x_perm]
+    b, b_perm = torch.sort(b, descending=False, stable=True)
+    ptr = torch.cat([num_nodes.new_zeros(1), num_nodes.cumsum(0)[:-1]])
+    mask = (torch.arange(score.numel()) - ptr[b]) < k[b]
+    return x_perm[b_perm[mask]]
+
+
+def filter_adj(edge_index: Tensor, edge_attr: Optional[Tensor], perm: Tensor, num_nodes: int):
+    """PyG's filter_adj [PyG-doc]: keep the edges whose two ends are in perm, in edge_index
+    order, relabelled to positions in perm."""
+    mask = perm.new_full((num_nodes,), -1)
+    mask[perm] = torch.arange(perm.numel(), dtype=torch.long)
+    row, col = mask[edge_index[0]], mask[edge_index[1]]
+    keep = (row >= 0) & (col >= 0)
+    return torch.stack([row[keep], col[keep]], 0), (edge_attr[keep] if edge_attr is not None else None)
+
+
+class _SelectTopK(nn.Module):
+    """The scoring projection of PyG's SelectTopK(in_channels=1): weight [1, 1],
+    score = act((attn * w).sum(-1) / ||w||), i.e. act(sign(w) * attn)."""
+
+    def __init__(self):
         super().__init__()
-        raise NotImplementedError("SAGPooling is outside the oracle's scope")
+        self.weight = nn.Parameter(torch.empty(1, 1))
+        with torch.no_grad():
+            self.weight.uniform_(-1.0, 1.0)   # PyG: uniform(in_channels=1, weight)
+
+
+class SAGPooling(nn.Module):
+    """torch_geometric.nn.SAGPooling restated [PyG-doc] for the form the reference builds
+    (Models/BuckGNN.py:203-208,231-236: GNN=SAGEConv, aggr='add', ratio=0.5, min_score=None):
+    attn = GNN(x, edge_index) [N, 1]; score = tanh(sign(w) attn) (select.weight w);
+    perm = topk(score, ratio, batch); x' = x[perm] * score[perm] (* multiplier);
+    edge_index', edge_attr' = filter_adj(...); batch' = batch[perm].
+    Returns (x', edge_index', edge_attr', batch', perm, score[perm])."""
+
+    def __init__(self, in_channels, ratio=0.5, GNN=None, min_score=None, multiplier=1.0, nonlinearity="tanh",
+                 **kwargs):
+        super().__init__()
+        if GNN is None:
+            raise NotImplementedError("SAGPooling: only an explicit GNN (the reference passes SAGEConv)")
+        if min_score is not None:
+            raise NotImplementedError("SAGPooling: min_score (softmax selection) is not restated")
+        self.in_channels, self.ratio, self.multiplier = in_channels, ratio, multiplier
+        self.nonlinearity = torch.tanh if nonlinearity == "tanh" else nonlinearity
+        self.gnn = GNN(in_channels, 1, **kwargs)
+        self.select = _SelectTopK()
+
+    def forward(self, x, edge_index, edge_attr=None, batch=None, attn=None):
+        if batch is None:
+            batch = edge_index.new_zeros(x.size(0))
+        attn = x if attn is None else attn
+        attn = attn.view(-1, 1) if attn.dim() == 1 else attn
+        attn = self.gnn(attn, edge_index)
+        w = self.select.weight
+        score = self.nonlinearity((attn * w).sum(dim=-1) / w.norm(p=2, dim=-1))
+        perm = topk(score, self.ratio, batch)
+        s = score[perm]
+        x = x[perm] * s.view(-1, 1)
+        x = self.multiplier * x if self.multiplier != 1 else x
+        edge_index, edge_attr = filter_adj(edge_index, edge_attr, perm, score.numel())
+        return x, edge_index, edge_attr, batch[perm], perm, s
 
 
 # ----------------------------------------------------------------------------- batching

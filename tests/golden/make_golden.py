@@ -48,6 +48,11 @@ CASES = [
     ("shared_h512", "GraphSage_addAggr_Shared", 512, "mean", [(6, False, 12)], False),
     ("add_h256", "GraphSage_addAggr", 256, "mean", [(5, False, 13), (5, True, 14)], False),
     ("ea_gnn_h64", "EA_GNN", 64, "mean", [(4, False, 15), (5, False, 16)], False),
+    # SAGPooling variants (Models/BuckGNN.py:190-244,354-373,493-511)
+    ("sag_h64", "GraphSAGE_SAG", 64, "mean", [(5, False, 17), (6, False, 18), (4, False, 19)], True),
+    ("sag_super_h64", "GraphSAGE_SAG", 64, "mean", [(5, True, 20), (4, True, 21)], True),
+    ("sag_single_h64", "GraphSAGE_SAG", 64, "mean", [(6, False, 22)], True),
+    ("eagnn_sag_h64", "EAGNN_SAG", 64, "mean", [(4, False, 23), (5, False, 24)], False),
 ]
 
 
@@ -78,6 +83,9 @@ def run_case(BuckGNN, case):
     batch = None if single else b["batch"]
     captured = {}
     model.decoder.register_forward_pre_hook(lambda m, inp: captured.__setitem__("pooled", inp[0].detach().clone()))
+    if hasattr(model, "pool"):   # SAGPooling outputs: perm, score[perm], pooled edge count
+        model.pool.register_forward_hook(lambda m, inp, o: captured.update(
+            perm=o[4].clone(), score=o[5].detach().clone(), n_edges=o[1].size(1)))
     model.train()
     pred, _ = model(b["x"], b["edge_index"], b["edge_attr"], batch)
     y = b["y"] if not single else b["y"][0]
@@ -93,6 +101,9 @@ def run_case(BuckGNN, case):
         "pred_train": pred.detach().numpy().reshape(-1), "loss_train": np.array(loss.item()),
         "pooled_train": captured["pooled"].numpy(),
     }
+    if "perm" in captured:
+        out.update(pool_perm=captured["perm"].numpy(), pool_score=captured["score"].numpy(),
+                   pool_edges=np.array(captured["n_edges"]))
     for k, p in model.named_parameters():
         if p.grad is None:
             continue
@@ -115,7 +126,9 @@ def run_case(BuckGNN, case):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default="", help="comma-separated case names (default: all)")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
     if not os.path.isdir(os.path.join(REF, "Models")):
         print("reference not present; nothing to do")
         return 0
@@ -128,6 +141,8 @@ def main():
         sys.path.remove(REF)
     total = 0
     for case in CASES:
+        if only and case[0] not in only:
+            continue
         name, out = run_case(BuckGNN, case)
         path = os.path.join(args.out, f"{name}.npz")
         np.savez_compressed(path, **out)

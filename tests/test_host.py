@@ -76,7 +76,7 @@ def test_no_cpu_fallback(fn):
 
 
 VARIANTS = ["GraphSage_addAggr", "GraphSage_sumAggr", "GraphSage_meanAggr", "GraphSage_maxAggr",
-            "GraphSage_addAggr_Shared", "EA_GNN", "EA_GNN_Shared", "GraphSAGE_MLP"]
+            "GraphSage_addAggr_Shared", "EA_GNN", "EA_GNN_Shared", "GraphSAGE_MLP", "GraphSAGE_SAG", "EAGNN_SAG"]
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference not present")

@@ -102,7 +102,12 @@ def reference_shapes(meta):
     return {k: tuple(v.shape) for k, v in m.state_dict().items()}
 
 
-@pytest.mark.parametrize("path", [p for p in golden_files() if "ea_gnn" not in p], ids=os.path.basename)
+def _is_sag(p):
+    return os.path.basename(p).startswith(("sag_", "eagnn_sag"))
+
+
+@pytest.mark.parametrize("path", [p for p in golden_files() if "ea_gnn" not in p and not _is_sag(p)],
+                         ids=os.path.basename)
 def test_oracle_matches_reference_golden(path):
     z, meta = load_case(path)
     sd = oracle_state(meta, reference_shapes(meta))
@@ -165,3 +170,56 @@ def test_ea_oracle_matches_reference_golden(path):
     with torch.no_grad():
         pe = R.ea_forward(step, x, ei, ea, batch, False, 0.0, meta["num_layers"])
     np.testing.assert_allclose(pe.numpy().reshape(-1), z["pred_eval"], rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("path", [p for p in golden_files() if _is_sag(p)], ids=os.path.basename)
+def test_sag_oracle_matches_reference_golden(path):
+    """oracle.buckgnn_ref.sag_forward (GraphSAGE_SAG / EAGNN_SAG with SAGPooling,
+    Models/BuckGNN.py:190-244,354-373,493-511) against the golden vectors of the reference's own
+    model: the pooled node selection (perm, scores), prediction, loss, gradients, BN state."""
+    z, meta = load_case(path)
+    sd = oracle_state(meta, reference_shapes(meta))
+    x = torch.from_numpy(z["x"])
+    ei = torch.from_numpy(z["edge_index"])
+    ea = torch.from_numpy(z["edge_attr"])
+    batch = None if meta["single_graph"] else torch.from_numpy(z["batch"])
+    y = torch.from_numpy(z["y"])
+    if meta["single_graph"]:
+        y = y[0]
+    step = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    pred, perm = R.sag_forward(step, meta["model_name"], x, ei, ea, batch, True, 0.0, meta["num_layers"])
+    np.testing.assert_array_equal(perm.numpy(), z["pool_perm"])
+    loss = R.relative_error_loss(pred, y)
+    loss.backward()
+    np.testing.assert_allclose(pred.detach().numpy().reshape(-1), z["pred_train"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(loss.item(), float(z["loss_train"]), rtol=2e-5, atol=2e-5)
+    n = 0
+    for k in z.files:
+        if k.startswith("grad/"):
+            np.testing.assert_allclose(step[k[5:]].grad.numpy(), z[k], rtol=1e-4, atol=1e-5, err_msg=k)
+            n += 1
+        elif k.startswith("gradsum/"):
+            np.testing.assert_allclose(grad_checksum(step[k[8:]].grad.numpy()), z[k], rtol=1e-3, atol=1e-4,
+                                       err_msg=k)
+            n += 1
+        elif k.startswith("state/"):
+            np.testing.assert_allclose(step[k[6:]].detach().numpy(), z[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    assert n > 0
+    with torch.no_grad():
+        pe, _ = R.sag_forward(step, meta["model_name"], x, ei, ea, batch, False, 0.0, meta["num_layers"])
+    np.testing.assert_allclose(pe.numpy().reshape(-1), z["pred_eval"], rtol=2e-5, atol=2e-5)
+
+
+def test_kat_topk_and_filter_adj():
+    """Hand-derived known answers for PyG's topk / filter_adj (ratio 0.5: ceil(n/2) per graph,
+    descending, ties to the lower index; kept edges in order, relabelled)."""
+    from oracle.pyg_ref import filter_adj, topk
+    score = torch.tensor([0.1, 0.9, 0.5, 0.5, -1.0, 0.3, 0.3, 0.3])
+    batch = torch.tensor([0, 0, 0, 0, 0, 1, 1, 1])
+    perm = topk(score, 0.5, batch)
+    assert perm.tolist() == [1, 2, 3, 5, 6]    # graph 0: k=3 of 5; graph 1: k=2 of 3 (ties)
+    ei = torch.tensor([[1, 2, 0, 3, 5, 6, 7], [2, 1, 1, 5, 6, 5, 5]])
+    ea = torch.arange(7.0).view(7, 1)
+    e2, a2 = filter_adj(ei, ea, perm, 8)
+    assert e2.tolist() == [[0, 1, 2, 3, 4], [1, 0, 3, 4, 3]]
+    assert a2.view(-1).tolist() == [0.0, 1.0, 3.0, 4.0, 5.0]
