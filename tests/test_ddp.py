@@ -66,4 +66,64 @@ def test_grad_allreduce_gloo_world2():
     assert res[0][5] == res[1][5] and res[0][6] != res[1][6]
 
 
+class Deep(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.layers = torch.nn.ModuleList([torch.nn.Linear(16, 16) for _ in range(5)])
+        self.unused = torch.nn.Linear(16, 16)
+
+    def forward(self, x):
+        for i, l in enumerate(self.layers):
+            x = torch.relu(l(x)) + (x if i else 0)
+        return x
+
+
+def _worker_overlap(rank, world, port, q):
+    """Three steps with bucketed all-reduces launched from the gradient hooks (several buckets)
+    against the flat blocking all-reduce: identical averaged gradients every step."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bgnn
+
+    out = []
+    for overlap in (True, False):
+        torch.manual_seed(0)
+        m = Deep()
+        ar = bgnn.GradAllReduce(m, bucket_mb=0.001, overlap=overlap)   # ~1 KB buckets: one per layer
+        grads = []
+        for step in range(3):
+            torch.manual_seed(100 * step + rank)
+            m.zero_grad(set_to_none=True)
+            m(torch.randn(8, 16)).pow(2).sum().backward()
+            ar()
+            grads.append([p.grad.numpy().copy() for p in m.layers.parameters()])
+            assert m.unused.weight.grad is None
+        out.append((grads, len(ar._buckets) if ar._buckets else 0))
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_overlapped_buckets_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlap, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ((g_ov, nb), (g_flat, _)) in res:
+        assert nb == 5
+        for a, b in zip(g_ov, g_flat):
+            for x, y in zip(a, b):
+                assert (x == y).all()
+    for x, y in zip(res[0][1][0][0][-1], res[1][1][0][0][-1]):
+        assert (x == y).all()   # every rank holds the same average
+
+
 PORT = _free_port()

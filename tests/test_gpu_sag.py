@@ -144,9 +144,15 @@ def test_sag_pooling_module_matches_oracle(dev, h, super_node):
     (o_ref[0] * gy).sum().backward()
     (o[0] * gy.to(dev)).sum().backward()
     np.testing.assert_allclose(xm.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    # the scorer's weight gradients are sums over all nodes (|g| up to ~2e3 at h = 512) and the
+    # GPU scorer is transform-first: elements that cancel are compared at 2e-6 of the tensor's max
     pr = dict(ref.named_parameters())
     for k, p in mine.named_parameters():
-        np.testing.assert_allclose(p.grad.cpu().numpy(), pr[k].grad.numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+        if k == "select.weight":   # d tanh(attn * w / |w|) / dw = 0 exactly: both sides hold rounding noise
+            continue
+        r = pr[k].grad.numpy()
+        np.testing.assert_allclose(p.grad.cpu().numpy(), r, rtol=1e-4, atol=max(1e-5, 2e-6 * np.abs(r).max()),
+                                   err_msg=k)
 
 
 def test_sag_pooling_loads_checkpoint_without_select_weight(dev):
