@@ -239,11 +239,8 @@ class GraphStore:
         graph = Graph(Nb, Eb, fwd, bwd, perm_t, ei_b, None)
         _graph_cache.put(ei_b, (Nb, self.chunk), graph)
         # pooling segments: graph b owns positions [ptr[b], ptr[b+1])
-        heavy_g = nn_ > self.chunk
         ptr32 = ptr.to(torch.int32)
-        seg_plan = self._plan(ptr32, B, Nb, int(heavy_g.sum()),
-                              int(((nn_ + self.chunk - 1) // self.chunk)[heavy_g].sum()))
-        seg_f = Csr(ptr32, self._arange(Nb), B, Nb, seg_plan)
+        seg_f = Csr(ptr32, self._arange(Nb), B, Nb, self._plan_host(dn))
         empty = Plan(torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
                      torch.zeros(1, dtype=torch.int32, device=dev), 0, 0, self.chunk)
         seg_b = Csr(self._arange(Nb + 1), batch.to(torch.int32), Nb, Nb, empty)
@@ -284,10 +281,37 @@ class GraphStore:
         return out
 
     def _plan(self, rowptr, n_rows, nnz, n_heavy, n_chunks) -> Plan:
+        if n_heavy == 0:   # no row above `chunk` (cfg2 meshes): nothing to plan, no launch
+            z = self._zeros_i32()
+            return Plan(z, z, z, 0, 0, self.chunk)
         counts = torch.empty(2, dtype=torch.int32, device=self.device)   # device copy unused: counts known
         p = enqueue_plan(rowptr, n_rows, nnz, counts, self.chunk)
         p.n_heavy, p.n_chunks = n_heavy, n_chunks
         return p
+
+    def _plan_host(self, rowptr_h: np.ndarray) -> Plan:
+        """Heavy-row plan of a CSR whose rowptr the host holds (the pooling segments: one row per
+        graph), computed in numpy and uploaded in one copy -- the same arrays bgnn_heavy_plan
+        writes: heavy rows ascending, heavy_chunk0 = running chunk counts, chunk -> heavy row."""
+        deg = np.diff(np.asarray(rowptr_h, dtype=np.int64))
+        heavy = np.nonzero(deg > self.chunk)[0]
+        if heavy.size == 0:
+            z = self._zeros_i32()
+            return Plan(z, z, z, 0, 0, self.chunk)
+        nch = (deg[heavy] + self.chunk - 1) // self.chunk
+        c0 = np.concatenate([[0], np.cumsum(nch)])
+        ch = np.repeat(np.arange(heavy.size), nch)
+        pack = torch.from_numpy(np.concatenate([heavy, c0, ch]).astype(np.int32)).pin_memory()
+        d = pack.to(self.device, non_blocking=True)
+        h = heavy.size
+        return Plan(d[:h], d[h:2 * h + 1], d[2 * h + 1:], int(h), int(c0[-1]), self.chunk)
+
+    def _zeros_i32(self) -> torch.Tensor:
+        z = self._ptr_cache.get("zeros")
+        if z is None:
+            z = torch.zeros(2, dtype=torch.int32, device=self.device)
+            self._ptr_cache["zeros"] = z
+        return z
 
     def _arange(self, n: int) -> torch.Tensor:
         t = self._ptr_cache.get(n)

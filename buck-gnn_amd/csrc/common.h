@@ -86,6 +86,9 @@ int gemm_mode();
 // variant v (gemm_h3g.hip) where the shape allows
 void set_gemm_staging(int v);
 int gemm_staging();
+// tail split of tall f16x3 GEMMs whose last 256x256 tile round is under-filled (gemm.hip)
+void set_gemm_tail(int on);
+int gemm_tail();
 // non-temporal output stores of the row-wise SAGE kernels (sage.hip)
 void set_rows_nt(int on);
 int rows_nt();

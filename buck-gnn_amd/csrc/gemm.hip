@@ -360,7 +360,48 @@ struct Plan {
     int cfg;           // index into kX6Cfgs / kCfgs
     int bm, bn, bk;    // tile
     int split;
+    // tail split (f16x3 tall products whose last round of 256x256 tiles would run under-filled):
+    // rows [0, rows_a) as whole rounds of 256x256 tiles, rows [rows_a, M) as 256x256 tiles with
+    // split-K tail_split (+ slab reduce). rows_a = M: off.
+    int64_t rows_a;
+    int tail_split;
 };
+
+constexpr int kNumCUs = 256;              // MI355X: one 256x256 f16x3 workgroup per CU (128 KB LDS)
+// tail split (A/B knob BGNN_TUNE_GEMM_TAIL), off by default: measured in the cfg2 train step
+// (tools/ab_step.py, MI355X) 9.96 ms/step with it against 9.89 ms with the 128x256 dgrad tiles
+static int g_gemm_tail = 0;
+namespace bgnn {
+void set_gemm_tail(int on) { g_gemm_tail = on; }
+int gemm_tail() { return g_gemm_tail; }
+}  // namespace bgnn
+
+// dgrad 80656x512x1024 runs 128x256 tiles (1,262 tiles = 4.93 rounds) because 256x256 tiles
+// leave the third round half empty (632 tiles = 2.47 rounds), yet a 256x256 tile does twice the
+// MFMA work per operand byte. Tail split: two full rounds of 256x256 tiles over the first
+// 65,536 rows, and the remaining 120 tiles as 240 half-K pieces (one round) + a slab reduce.
+// Measured slower than the 128x256 tiles in the train step (see g_gemm_tail): kept as a knob.
+static void plan_tail(Plan& p, int64_t M, int64_t N, int64_t K, int ta, int64_t a_blk, int64_t c_blk) {
+    p.rows_a = M;
+    p.tail_split = 1;
+    if (!g_gemm_tail || g_gemm_cfg >= 0 || !p.x6 || p.prec != 1 || p.cfg != 2 || p.split != 1 || ta != 0 ||
+        a_blk != 0 || c_blk != 0 || K < 512 || K % 64 != 0)
+        return;
+    const int64_t tcols = (N + 255) / 256;
+    const int64_t trows = (M + 255) / 256;
+    const int64_t tiles = trows * tcols;
+    const int64_t full = tiles / kNumCUs;                  // whole rounds
+    const int64_t rem = tiles - full * kNumCUs;
+    if (full < 1 || rem == 0 || 4 * rem > 3 * kNumCUs) return;   // last round >= 3/4 full: keep
+    const int64_t rows_a = (full * kNumCUs / tcols) * 256;
+    if (rows_a <= 0 || rows_a >= M) return;
+    const int64_t tail_tiles = ((M - rows_a + 255) / 256) * tcols;
+    if (2 * tail_tiles > kNumCUs) return;                  // the halved tail must fit one round
+    p.cfg = 4;
+    p.bm = 256; p.bn = 256;
+    p.rows_a = rows_a;
+    p.tail_split = 2;
+}
 
 static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk,
                       int precision = 0) {
@@ -372,6 +413,8 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         if (a_blk != 0 || c_blk != 0) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves, kX6Cfgs[p.cfg].blocks_per_cu});
+        p.rows_a = M;
+        p.tail_split = 1;
         return p;
     }
     auto planes_ok = [&](int bm, int bn, int bk) {
@@ -386,6 +429,8 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves,
                                                  kX6Cfgs[p.cfg].blocks_per_cu});
+        plan_tail(p, M, N, K, ta, a_blk, c_blk);
+        return p;
     } else {
         p.cfg = pick_cfg(M, N, K, ta, tb);
         // plane blocks must be whole multiples of the tile along the split dimension; fall back
@@ -395,6 +440,8 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.bm = c.bm; p.bn = c.bn; p.bk = c.bk;
         p.split = choose_split(M, N, K, c);
     }
+    p.rows_a = M;
+    p.tail_split = 1;
     return p;
 }
 
@@ -409,7 +456,35 @@ constexpr size_t kAmaxHead = 256;
 
 static size_t ws_need(const Plan& p, int64_t M, int64_t N) {
     const size_t head = (p.x6 && p.prec == 1) ? kAmaxHead : 0;
+    if (p.rows_a < M) return head + (size_t)p.tail_split * (size_t)(M - p.rows_a) * (size_t)N * sizeof(float);
     return head + (p.split > 1 ? (size_t)p.split * (size_t)M * (size_t)N * sizeof(float) : 0);
+}
+
+// slab reduce of a split-K GEMM: C = act(alpha * sum of slabs + beta C + bias)
+static int launch_splitk_reduce(float* slabs, int split, int64_t M, int64_t N, float alpha, float beta, float* C,
+                                int64_t ldc, const float* bias, int relu, int64_t c_blk, int64_t c_pstride,
+                                hipStream_t s) {
+    int64_t blocks = (M * N + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    // few outputs, many slabs: sum slab groups first so the reduction spreads over >= ~512
+    // workgroups instead of one serial sum per output element (encoder wgrads: 100 -> ~10 us)
+    int stride = 1;
+    const int64_t eb = (M * N + 255) / 256;
+    if (split >= 16 && eb < 512) {
+        int64_t groups = (512 + eb - 1) / eb;
+        if (groups > split / 4) groups = split / 4;
+        if (groups >= 2) {
+            stride = (int)((split + groups - 1) / groups);
+            groups = (split + stride - 1) / stride;
+            hipLaunchKernelGGL(k_splitk_stage1, dim3((unsigned)eb, (unsigned)groups), dim3(256), 0, s, slabs, split,
+                               M * N, stride);
+            BGNN_CHECK_LAUNCH();
+        }
+    }
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)slabs, split, stride,
+                       M, N, alpha, beta, C, ldc, bias, relu, c_blk, c_pstride);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
 }
 
 extern "C" size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t ta, int32_t tb) {
@@ -475,18 +550,24 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     }
     float* slabs = ws ? reinterpret_cast<float*>(static_cast<char*>(ws) + head) : nullptr;
     const size_t slab_bytes = ws_bytes > head ? ws_bytes - head : 0;
-    int split = pl.split;
+    const int64_t Mt = M - pl.rows_a;   // tail rows (tail split), 0 = none
+    if (Mt > 0 && (slabs == nullptr || slab_bytes < (size_t)pl.tail_split * Mt * N * sizeof(float))) {
+        return fail(BGNN_E_WS, "gemm: workspace too small for the tail split (need bgnn_gemm_ws_bytes_ex())");
+    }
+    int split = Mt > 0 ? 1 : pl.split;
     if (split > 1 && (slabs == nullptr || slab_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
-    GemmArgs g{A, B, C, slabs, M, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
+    const int64_t Ma = pl.rows_a;
+    GemmArgs g{A, B, C, slabs, Ma, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
                a_blk, a_pstride, c_blk, c_pstride, a_amax, b_amax, nullptr};
     // max |C| for the next GEMM's operand scale: in the split kernels' epilogue, else one pass
-    const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1;
+    const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1 && Mt == 0;
     if (c_amax_fused) g.c_amax = c_amax;
     int64_t kc = (K + split - 1) / split;
     kc = (kc + pl.bk - 1) / pl.bk * pl.bk;
     g.kchunk = kc > 0 ? kc : pl.bk;
-    dim3 grid((unsigned)tiles, split);
-    if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, M, N), s, g);
+    const int64_t tiles_a = ((Ma + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
+    dim3 grid((unsigned)tiles_a, split);
+    if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, Ma, N), s, g);
     else if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
     else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
     else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
@@ -494,26 +575,23 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     else launch_cfg<1, 1>(pl.cfg, grid, s, g);
     BGNN_CHECK_LAUNCH();
     if (split > 1) {
-        int64_t blocks = (M * N + 255) / 256;
-        if (blocks > 4096) blocks = 4096;
-        // few outputs, many slabs: sum slab groups first so the reduction spreads over >= ~512
-        // workgroups instead of one serial sum per output element (encoder wgrads: 100 -> ~10 us)
-        int stride = 1;
-        const int64_t eb = (M * N + 255) / 256;
-        if (split >= 16 && eb < 512) {
-            int64_t groups = (512 + eb - 1) / eb;
-            if (groups > split / 4) groups = split / 4;
-            if (groups >= 2) {
-                stride = (int)((split + groups - 1) / groups);
-                groups = (split + stride - 1) / stride;
-                hipLaunchKernelGGL(k_splitk_stage1, dim3((unsigned)eb, (unsigned)groups), dim3(256), 0, s, slabs, split,
-                                   M * N, stride);
-                BGNN_CHECK_LAUNCH();
-            }
-        }
-        hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)slabs, split, stride,
-                           M, N, alpha, beta, C, ldc, bias, relu, c_blk, c_pstride);
+        const int rc = launch_splitk_reduce(slabs, split, M, N, alpha, beta, C, ldc, bias, relu, c_blk, c_pstride, s);
+        if (rc != BGNN_OK) return rc;
+    }
+    if (Mt > 0) {   // tail rows: 256x256 tiles, split-K over tail_split slabs, then the slab reduce
+        GemmArgs t = g;
+        t.A = A + Ma * lda;
+        t.C = C + Ma * ldc;
+        t.M = Mt;
+        t.split = pl.tail_split;
+        t.c_amax = nullptr;
+        int64_t tk = (K + t.split - 1) / t.split;
+        t.kchunk = (tk + pl.bk - 1) / pl.bk * pl.bk;
+        const int64_t tiles_t = ((Mt + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
+        launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles_t, t.split), s, t);
         BGNN_CHECK_LAUNCH();
+        const int rc = launch_splitk_reduce(slabs, t.split, Mt, N, alpha, beta, t.C, ldc, bias, relu, 0, 0, s);
+        if (rc != BGNN_OK) return rc;
     }
     if (c_amax != nullptr && !c_amax_fused) {
         launch_absmax(C, M, N, ldc, c_blk, c_pstride, c_amax, s);
@@ -563,8 +641,11 @@ extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N
     BGNN_REQUIRE((tb == 0 && ldb >= N) || (tb == 1 && ldb >= K) || N == 0 || K == 0, "gemm_gather_add: bad ldb");
     BGNN_REQUIRE(ldc >= N || M == 0, "gemm_gather_add: bad ldc");
     if (M == 0 || N == 0) return BGNN_OK;
-    const Plan pl = make_plan(M, N, K, ta, tb, 0, 0, precision);
+    Plan pl = make_plan(M, N, K, ta, tb, 0, 0, precision);
     BGNN_REQUIRE(pl.x6, "gemm_gather_add: needs the split GEMM family (BGNN_TUNE_GEMM_MODE 1 or 2)");
+    if (pl.rows_a < M) {   // no split-K here (the gathered epilogue): the plain 128x256 tiles
+        pl.cfg = 2; pl.bm = 128; pl.bn = 256; pl.rows_a = M; pl.tail_split = 1;
+    }
     const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
     BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm_gather_add: too many tiles");
     hipStream_t s = as_stream(stream);

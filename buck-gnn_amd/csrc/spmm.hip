@@ -704,7 +704,9 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
 // per row and column: VALU, hidden under the loads). Groups are swept per XCD like rows in
 // k_seg_sweep. Per row, the entries are summed in plan order (deterministic; for the group's
 // first row it is CSR order), so results match the sweep kernel to rounding, not bitwise.
-template <int NV, int OP, int EPI, int R, int U>
+// ZE (SAGE epilogue): issue the group's z_r row loads before its gathers (they complete under
+// them) instead of after (one more round trip per group, fewer VGPRs held).
+template <int NV, int OP, int EPI, int R, int U, int ZE = 0>
 __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -767,6 +769,16 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                 sl_n = lane < c ? A.gsrc[b + lane] : 0;
                 ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
             }
+            constexpr bool kZE = EPI == EPI_SAGE && ZE != 0;
+            Vec<4> zre[kZE ? R : 1][NV];
+            if constexpr (kZE) {
+#pragma unroll
+                for (int t = 0; t < R; ++t) {
+                    const int64_t r = r0 + (t < rows ? t : 0);
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) zre[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
+                }
+            }
             float a[R][NV][4];
 #pragma unroll
             for (int t = 0; t < R; ++t)
@@ -825,7 +837,10 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                 for (int t = 0; t < R; ++t) {
                     const int64_t r = r0 + (t < rows ? t : 0);
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) zr[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
+                    for (int v = 0; v < NV; ++v) {
+                        if constexpr (kZE) zr[t][v] = zre[kZE ? t : 0][v];
+                        else zr[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
+                    }
                 }
 #pragma unroll
                 for (int t = 0; t < R; ++t) {
@@ -906,6 +921,8 @@ static int g_seg_kernel = 0;     // 0 = auto (row-group kernel where planned, el
 static int g_grp_blocks = 1024;  // row-group kernel grid (4 blocks of 4 waves per CU)
 static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
 static int g_seg_nt = 1;         // non-temporal hints on stream-once data (default on: +8 % fwd)
+static int g_grp_u = 8;          // source rows per gather batch in the row-group kernel (8 or 16)
+static int g_grp_ze = 0;         // row-group SAGE epilogue: z_r loads before the gathers (0/1)
 static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto = 12:
                                  // mesh rows have 8 neighbours + ~1 virtual edge, one batch)
 
@@ -994,10 +1011,19 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     if (A.n_rows > 0) {
         if constexpr (VEC == 4 && LPR == 64 && (OP == OP_SUM || OP == OP_MEAN || OP == OP_MEANT)) {
             if (group) {
+                const dim3 gr((unsigned)blocks);
+                constexpr int ZE = EPI == EPI_SAGE ? 1 : 0;   // (plain epilogue: no z_r variant)
+                const bool ze = ZE && g_grp_ze;
                 if (A.group_rows == 8)
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 8>), dim3((unsigned)blocks), dim3(256), 0, s, A);
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 8>), gr, dim3(256), 0, s, A);
+                else if (g_grp_u == 16 && ze)
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 16, ZE>), gr, dim3(256), 0, s, A);
+                else if (g_grp_u == 16)
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 16>), gr, dim3(256), 0, s, A);
+                else if (ze)
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8, ZE>), gr, dim3(256), 0, s, A);
                 else
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8>), dim3((unsigned)blocks), dim3(256), 0, s, A);
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8>), gr, dim3(256), 0, s, A);
                 BGNN_CHECK_LAUNCH();
             }
         }
@@ -1150,6 +1176,9 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
         case BGNN_TUNE_GEMM_STAGING: return gemm_staging();
+        case BGNN_TUNE_GEMM_TAIL: return gemm_tail();
+        case BGNN_TUNE_GROUP_U: return g_grp_u;
+        case BGNN_TUNE_GROUP_ZR_EARLY: return g_grp_ze;
         default: return -1;
     }
 }
@@ -1175,6 +1204,12 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             g_grp_blocks = value;
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
+        case BGNN_TUNE_GEMM_TAIL: set_gemm_tail(value ? 1 : 0); return BGNN_OK;
+        case BGNN_TUNE_GROUP_U:
+            BGNN_REQUIRE(value == 8 || value == 16, "set_tuning: group U must be 8 or 16");
+            g_grp_u = value;
+            return BGNN_OK;
+        case BGNN_TUNE_GROUP_ZR_EARLY: g_grp_ze = value ? 1 : 0; return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: gemm mode must be 0 (f32), 1 (bf16x6) or 2 (f16x3)");
             set_gemm_mode(value);

@@ -72,6 +72,13 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_GEMM_STAGING 8 /* f16x3 operand staging: -1 = registers (gemm_x6), 0..1 =
                                     LDS-DMA kernel variant (gemm_h3g) for tall K-contiguous
                                     products                                                 */
+#define BGNN_TUNE_GEMM_TAIL 9     /* tall f16x3 GEMMs whose last round of 256x256 tiles would be
+                                    under-filled (the SAGE dgrad): whole rounds of 256x256 tiles +
+                                    the remaining rows as split-K halves (1 = on; 0 = the 128x256
+                                    tiles, default: measured faster in the train step)       */
+#define BGNN_TUNE_GROUP_U 10      /* row-group kernel: source rows per gather batch, 8 or 16    */
+#define BGNN_TUNE_GROUP_ZR_EARLY 11 /* row-group SAGE epilogue: z_r loads issued before the gathers
+                                    (1) or after them (0)                                    */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);

@@ -273,3 +273,34 @@ def test_gemm_staging_knob_range():
     assert _lib.query("bgnn_get_tuning", STAGING) in (-1, 0, 1)
     with pytest.raises(Exception):
         _lib.call("bgnn_set_tuning", STAGING, 2)
+
+
+@pytest.mark.parametrize("mnk", [(80656, 512, 1024), (70000, 512, 512), (66000, 256, 768)])
+def test_gemm_tail_split_matches_fp64(dev, mnk):
+    """Tail split (BGNN_TUNE_GEMM_TAIL, the SAGE dgrad shape 80656x512x1024): whole rounds of
+    256x256 tiles + the remaining rows as split-K halves with a slab reduce. With beta = 1 and a
+    bias, against fp64: the same error class as the 128x256-tile path (tail off); deterministic."""
+    M, N, K = mnk
+    torch.manual_seed(M % 97)
+    a = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) * 0.03
+    c0 = torch.randn(M, N, device=dev)
+    bias = torch.randn(N, device=dev)
+    r = c0.double() + a.double() @ w.double().t() + bias.double()
+    outs = {}
+    for tail in (1, 0):
+        _lib.call("bgnn_set_tuning", 9, tail)
+        c = c0.clone()
+        fused.gemm(a, w, False, True, out=c, beta=1.0, bias=bias)
+        c2 = c0.clone()
+        fused.gemm(a, w, False, True, out=c2, beta=1.0, bias=bias)
+        assert torch.equal(c, c2)
+        outs[tail] = c
+    _lib.call("bgnn_set_tuning", 9, 0)
+    err = {t: (c.double() - r).abs().max().item() for t, c in outs.items()}
+    assert err[1] <= 1.5 * err[0] + 1e-6, err
+    assert err[0] <= 2e-6 * (a.abs().max() * w.abs().max()).item() * K, err
+
+
+def test_gemm_tail_knob():
+    assert _lib.query("bgnn_get_tuning", 9) == 0

@@ -230,3 +230,52 @@ def test_spmm_bwd_folds_max_abs(dev, kernel, reduce):
             assert amax.item() == gx.abs().max().item()
     finally:
         _lib.call("bgnn_set_tuning", 1, old)
+
+
+@pytest.mark.parametrize("knobs", [(16, 0), (8, 1), (16, 1)], ids=["u16", "zr_early", "u16_zr_early"])
+@pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
+def test_group_kernel_knobs_bit_identical(dev, knobs, graph):
+    """Row-group kernel variants (BGNN_TUNE_GROUP_U: 16 source rows per gather batch;
+    BGNN_TUNE_GROUP_ZR_EARLY: z_r loads before the gathers) change only load scheduling: the
+    fused SAGE forward (o, norms, BN partial sums) and the plain / transpose aggregations are
+    bit-identical to the defaults."""
+    from bgnn import _lib
+    ei, n = _variant_graph(dev, graph)
+    g = Graph.build(ei, n)
+    assert g.fwd.groups is not None
+    H = 512
+    torch.manual_seed(9)
+    z = torch.randn(n, 2 * H, device=dev)
+    bias = torch.randn(H, device=dev)
+    x = torch.randn(n, H, device=dev)
+    gy = torch.randn(n, H, device=dev)
+    slots = _lib.query("bgnn_sage_fwd_slots", g.fwd.ref())
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        o = torch.empty(n, H, device=dev)
+        nrm = torch.empty(n, device=dev)
+        bnp = torch.empty(slots, 2, H, device=dev)
+        part = torch.empty(max(g.fwd.plan.n_chunks, 1) * H, device=dev)
+        _lib.call("bgnn_sage_fwd", g.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H, bias.data_ptr(), H,
+                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
+        red = {}
+        for r in ("sum", "mean"):
+            xx = x.clone().requires_grad_(True)
+            y = bgnn.aggregate(xx, g, r)
+            y.backward(gy)
+            red[r] = (y.detach(), xx.grad)
+        return o, nrm, bnp, red
+
+    ref = run()
+    try:
+        _lib.call("bgnn_set_tuning", 10, knobs[0])
+        _lib.call("bgnn_set_tuning", 11, knobs[1])
+        got = run()
+    finally:
+        _lib.call("bgnn_set_tuning", 10, 8)
+        _lib.call("bgnn_set_tuning", 11, 0)
+    for a, b in zip(ref[:3], got[:3]):
+        assert torch.equal(a, b)
+    for r in ("sum", "mean"):
+        assert torch.equal(ref[3][r][0], got[3][r][0]) and torch.equal(ref[3][r][1], got[3][r][1]), r

@@ -16,7 +16,7 @@ import torch  # noqa: E402
 from bgnn import _lib, synthetic  # noqa: E402
 from bgnn.graph import Graph  # noqa: E402
 
-KNOB = {"kernel": 1, "blocks": 2, "u": 3, "nt": 4, "gblocks": 7}
+KNOB = {"kernel": 1, "blocks": 2, "u": 3, "nt": 4, "gblocks": 7, "gu": 10, "gze": 11}
 
 
 def main():
@@ -52,13 +52,13 @@ def main():
     def set_variant(v):
         # "blocked" | "sweep[U][_b<blocks>][_nt][_planes]" | "group<R>[_b<blocks>][_nt][_planes]"
         # (U = 0 auto, 8, 12, 16; R = 4 or 8 rows per group; planes = z as two [N, H] planes)
-        kern, u, blocks, nt, rows = 2, 0, 1024, 1, 0
+        kern, u, blocks, nt, rows, gu, gze = 2, 0, 1024, 1, 0, 8, 0
         layout["il"] = not v.endswith("_planes")
         parts = v.split("_")
         if v == "blocked":
             kern = 1
         elif parts[0].startswith("group"):
-            kern, rows, blocks = 0, int(parts[0][5:] or 8), 512
+            kern, rows, blocks = 0, int(parts[0][5:] or 8), 1024
         else:
             u = int(parts[0][5:] or 0)
         for p in parts[1:]:
@@ -66,11 +66,17 @@ def main():
                 blocks = int(p[1:])
             elif p == "nt0":
                 nt = 0
+            elif p == "u16":     # row-group kernel: 16 source rows per gather batch
+                gu = 16
+            elif p == "ze":      # row-group SAGE epilogue: z_r loads before the gathers
+                gze = 1
         cur["g"] = graphs[rows]
         _lib.call("bgnn_set_tuning", KNOB["kernel"], kern)
         _lib.call("bgnn_set_tuning", KNOB["u"], u)
         _lib.call("bgnn_set_tuning", KNOB["blocks" if kern else "gblocks"], blocks)
         _lib.call("bgnn_set_tuning", KNOB["nt"], nt)
+        _lib.call("bgnn_set_tuning", KNOB["gu"], gu)
+        _lib.call("bgnn_set_tuning", KNOB["gze"], gze)
 
     def run_fwd():
         g = cur["g"]
