@@ -28,7 +28,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .fused import gemm, linear, mlp
+from .fused import gemm, linear, mlp, relu_bias_grad
 from .graph import SegmentIndex, _index_cache, _stream
 from .ops import segment_reduce
 
@@ -103,11 +103,14 @@ class _LinearGatherReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         e, W, out = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(g.contiguous(), out, 0.0)   # ReLU mask in one pass
+        # ReLU mask, bias gradient and max|g'| (the f16x3 operand scale of both GEMMs) in one pass
+        g, db, g_amax = relu_bias_grad(g, out, ctx.has_bias)
         bf16 = ctx.bf16
-        de = gemm(g, W.t().contiguous(), trans_a=False, trans_b=True, bf16=bf16) if ctx.needs_input_grad[0] else None
-        dW = gemm(g, e, trans_a=True, trans_b=False, bf16=bf16)
-        db = g.sum(0) if ctx.has_bias else None
+        if bf16:
+            g_amax = None
+        de = (gemm(g, W.t().contiguous(), trans_a=False, trans_b=True, a_amax=g_amax, bf16=bf16)
+              if ctx.needs_input_grad[0] else None)
+        dW = gemm(g, e, trans_a=True, trans_b=False, a_amax=g_amax, bf16=bf16)
         d1 = segment_reduce(g, ctx.seg1, "sum")
         d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
         return de, dW, db, d1, None, d2, None, None

@@ -159,6 +159,31 @@ def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float
     return out
 
 
+def relu_bias_grad(g: torch.Tensor, y=None, bias: bool = True):
+    """(g', db, max|g'|) for the backward of act(x W^T + b): g' = g masked by y > 0 (y = the ReLU
+    output; None = no ReLU), db = column sums of g' (None when bias is False). One pass over g
+    (bgnn_linear_bwd_prep: mask, bias-gradient partials and max|g'|) where the width allows,
+    else torch threshold_backward + sum + a max pass."""
+    g = g.contiguous()
+    C = g.size(1)
+    if C % 4 == 0 and 4 <= C <= 1024 and 256 % (C // 4) == 0:
+        gm = torch.empty_like(g) if y is not None else g
+        slots = _lib.query("bgnn_linear_bwd_prep_slots")
+        part = torch.empty(slots, 2, C, dtype=torch.float32, device=g.device)
+        g_amax = torch.zeros(1, dtype=torch.float32, device=g.device)
+        s = _stream()
+        _lib.call("bgnn_linear_bwd_prep", g.data_ptr(), None if y is None else y.data_ptr(), g.size(0), C,
+                  gm.data_ptr() if y is not None else None, part.data_ptr(), g_amax.data_ptr(), s)
+        db = None
+        if bias:
+            db = torch.empty(C, dtype=torch.float32, device=g.device)
+            _lib.call("bgnn_reduce_partials", part.data_ptr(), slots, C, db.data_ptr(), None, 0, s)
+        return gm, db, g_amax
+    if y is not None:
+        g = torch.ops.aten.threshold_backward(g, y, 0.0)   # ReLU mask in one pass
+    return g, (g.sum(0) if bias else None), absmax(g)
+
+
 class LinearFn(torch.autograd.Function):
     """(y, max|y|) with y = act(x W^T + b) on the bgnn GEMM (bias + ReLU fused in the epilogue,
     max|y| folded in there too: the next Linear's operand scale); backward: dgrad and wgrad
@@ -188,30 +213,10 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _g_amax):
         x, weight, y, x_amax, w_amax = ctx.saved_tensors
-        g = g.contiguous()
         bf16 = ctx.bf16
-        C = g.size(1)
-        db = None
-        if C % 4 == 0 and 4 <= C <= 1024 and 256 % (C // 4) == 0:
-            # ReLU mask, bias-gradient partials and max|g| in one pass (bgnn_linear_bwd_prep)
-            gm = torch.empty_like(g) if ctx.relu else g
-            slots = _lib.query("bgnn_linear_bwd_prep_slots")
-            part = torch.empty(slots, 2, C, dtype=torch.float32, device=g.device)
-            g_amax = torch.zeros(1, dtype=torch.float32, device=g.device)
-            s = _stream()
-            _lib.call("bgnn_linear_bwd_prep", g.data_ptr(), y.data_ptr() if ctx.relu else None, g.size(0), C,
-                      gm.data_ptr() if ctx.relu else None, part.data_ptr(), g_amax.data_ptr(), s)
-            if ctx.has_bias:
-                db = torch.empty(C, dtype=torch.float32, device=g.device)
-                _lib.call("bgnn_reduce_partials", part.data_ptr(), slots, C, db.data_ptr(), None, 0, s)
-            g = gm
-            if bf16:
-                g_amax = None
-        else:
-            if ctx.relu:
-                g = torch.ops.aten.threshold_backward(g, y, 0.0)   # ReLU mask in one pass
-            g_amax = None if bf16 else absmax(g)
-            db = g.sum(0) if ctx.has_bias else None
+        g, db, g_amax = relu_bias_grad(g, y if ctx.relu else None, ctx.has_bias)
+        if bf16:
+            g_amax = None
         w_amax = None if bf16 else w_amax
         x_amax = None if bf16 else x_amax
         dx = None
