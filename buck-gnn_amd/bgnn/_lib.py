@@ -102,6 +102,11 @@ SIGNATURES = {
     "bgnn_gather_scale_bwd": (c_i32, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p]),
     "bgnn_filter_edges_ws_bytes": (c_sz, [c_i64]),
     "bgnn_filter_edges": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "bgnn_mlp2_supported": (c_i32, [c_i32, c_i32, c_i32]),
+    "bgnn_mlp2_fwd": (c_i32, [c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "bgnn_mlp2_bwd_ws_bytes": (c_sz, [c_i64]),
+    "bgnn_mlp2_bwd": (c_i32, [c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                              c_sz, c_p]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,
                               c_p, c_sz, c_p]),
 }

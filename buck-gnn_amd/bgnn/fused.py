@@ -238,13 +238,71 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, rel
     return (y, y_amax) if return_amax else y
 
 
+# the node encoder's leading Linear(16,64).ReLU.Linear(64,128).ReLU as one VALU kernel
+# (bgnn_mlp2_fwd / _bwd) instead of two GEMM launches with their operand-max passes
+FUSED_MLP2 = True
+
+
+class _Mlp2Fn(torch.autograd.Function):
+    """(h, max|h|) with h = ReLU(ReLU(x W1^T + b1) W2^T + b2) on bgnn_mlp2_fwd; backward: the
+    four weight / bias gradients from bgnn_mlp2_bwd (x gets none: node features are data)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        N, F = x.shape
+        D1, D2 = W1.size(0), W2.size(0)
+        h = torch.empty(N, D2, dtype=torch.float32, device=x.device)
+        amax = torch.zeros(1, dtype=torch.float32, device=x.device)
+        _lib.call("bgnn_mlp2_fwd", x.data_ptr(), N, F, D1, D2, W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                  b2.data_ptr(), h.data_ptr(), amax.data_ptr(), _stream())
+        ctx.save_for_backward(x, W1, b1, W2, h)
+        ctx.mark_non_differentiable(amax)
+        return h, amax
+
+    @staticmethod
+    def backward(ctx, dh, _g_amax):
+        x, W1, b1, W2, h = ctx.saved_tensors
+        dh = dh.contiguous()
+        N, F = x.shape
+        D1, D2 = W1.size(0), W2.size(0)
+        dW1, db1 = torch.empty_like(W1), torch.empty_like(b1)
+        dW2 = torch.empty_like(W2)
+        db2 = torch.empty(D2, dtype=torch.float32, device=x.device)
+        ws_bytes = _lib.query("bgnn_mlp2_bwd_ws_bytes", N)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=x.device)
+        _lib.call("bgnn_mlp2_bwd", x.data_ptr(), N, F, D1, D2, W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                  h.data_ptr(), dh.data_ptr(), dW1.data_ptr(), db1.data_ptr(), dW2.data_ptr(), db2.data_ptr(),
+                  ws.data_ptr(), ws_bytes, _stream())
+        return None, dW1, db1, dW2, db2
+
+
+def _mlp2_prefix(mods, x: torch.Tensor) -> bool:
+    """Whether mods starts with Linear . ReLU . Linear . ReLU that bgnn_mlp2 covers for x."""
+    if not FUSED_MLP2 or len(mods) < 4 or x.requires_grad or x.dtype != torch.float32 or x.dim() != 2:
+        return False
+    l1, r1, l2, r2 = mods[:4]
+    if not (isinstance(l1, torch.nn.Linear) and isinstance(l2, torch.nn.Linear) and isinstance(r1, torch.nn.ReLU)
+            and isinstance(r2, torch.nn.ReLU) and l1.bias is not None and l2.bias is not None):
+        return False
+    if l2.in_features != l1.out_features or x.size(1) != l1.in_features:
+        return False
+    return bool(_lib.query("bgnn_mlp2_supported", l1.in_features, l1.out_features, l2.out_features))
+
+
 def mlp(seq: torch.nn.Sequential, x: torch.Tensor, return_amax: bool = False, bf16: bool = False):
     """Run an nn.Sequential of Linear/ReLU through bgnn GEMMs, fusing each ReLU into the
-    preceding Linear's epilogue (same parameters, same result as seq(x)). With return_amax,
-    also returns max|output| (device scalar) when the last module is a Linear, else None."""
+    preceding Linear's epilogue (same parameters, same result as seq(x)); a leading
+    Linear(16,64).ReLU.Linear(64,128).ReLU runs as one bgnn_mlp2 kernel. With return_amax,
+    also returns max|output| (device scalar) when the last module is a Linear or that kernel's
+    ReLU, else None."""
     mods = list(seq)
     i = 0
     amax = None
+    if not bf16 and _mlp2_prefix(mods, x):
+        x, amax = _Mlp2Fn.apply(x.contiguous(), mods[0].weight, mods[0].bias, mods[2].weight, mods[2].bias)
+        if len(mods) == 4:
+            return (x, amax) if return_amax else x
+        mods = mods[4:]
     n_lin = sum(isinstance(m, torch.nn.Linear) for m in mods)
     bufs = torch.zeros(n_lin, 2, dtype=torch.float32, device=x.device)   # one fill for the whole MLP
     k = 0
@@ -310,7 +368,7 @@ class SageLayerFn(torch.autograd.Function):
                 bf = torch.mv(wcat, b_in)
             else:
                 wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False)
-                bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False).view(-1)
+                bf = torch.mv(wcat, b_in)   # a GEMV (f32 accumulation): no GEMM tile launch for one column
             absmax(wf, w_amax, accumulate=True)
             wmat = wf
         else:
@@ -439,7 +497,7 @@ class SageLayerFn(torch.autograd.Function):
                 dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)             # [2H, H]
                 dw.add_(torch.outer(dbf, b_in))
                 dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                       # [H, K_in]
-                db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)  # [H]
+                db_in = torch.mv(wcat.t(), dbf)                                            # [H] (GEMV)
             return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
                     None, None, None, None, None, dw_in, db_in)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev

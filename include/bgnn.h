@@ -405,6 +405,23 @@ int bgnn_filter_edges(const int64_t* edge_index, int64_t num_edges, const int32_
                       int64_t num_nodes, int64_t* out_edges, int64_t* kept, int64_t* n_kept,
                       void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Node-encoder head (Models/BuckGNN.py:67-74, h >= 256): h = ReLU(ReLU(x W1^T + b1) W2^T + b2)
+ * for x [N, F] (F = 16), W1 [D1, F] (D1 = 64), W2 [D2, D1] (D2 = 128), row-major fp32, on the
+ * VALU with both weights in LDS (the encoder's last Linear is folded into the first SAGE layer).
+ * bgnn_mlp2_fwd folds max|h| into *h_amax (f32 bits, atomic max; NULL = off).
+ * bgnn_mlp2_bwd: given dh = dL/dh, the weight / bias gradients of both layers (written, not
+ * accumulated), deterministic (per-workgroup partials summed in order); x gets no gradient.
+ * bgnn_mlp2_supported: whether (F, D1, D2) is built (only 16 x 64 x 128).
+ * ---------------------------------------------------------------------- */
+int bgnn_mlp2_supported(int32_t F, int32_t D1, int32_t D2);
+int bgnn_mlp2_fwd(const float* x, int64_t N, int32_t F, int32_t D1, int32_t D2, const float* W1,
+                  const float* b1, const float* W2, const float* b2, float* h, float* h_amax, void* stream);
+size_t bgnn_mlp2_bwd_ws_bytes(int64_t N);
+int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, int32_t D2, const float* W1,
+                  const float* b1, const float* W2, const float* h, const float* dh, float* dW1,
+                  float* db1, float* dW2, float* db2, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

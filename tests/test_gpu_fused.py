@@ -1,6 +1,7 @@
 """GPU: the fused SAGE layer (bgnn.fused.SageLayerFn) against the CPU oracle
 composition SAGEConv(normalize) -> BatchNorm1d -> ReLU -> skip -> Dropout
 (Models/BuckGNN.py:430-444), forward and every gradient."""
+import copy
 import numpy as np
 import pytest
 import torch
@@ -119,3 +120,34 @@ def test_dropout_mask_fraction_and_backward_consistency(dev):
     ro.backward(up.cpu().double())
     torch.testing.assert_close(xd.grad.cpu(), xc.grad.float(), **TOL)
     torch.testing.assert_close(d["w_l"].grad.cpu(), t["w_l"].grad.float(), **TOL)
+
+
+@pytest.mark.parametrize("N", [1, 63, 65, 1000, 80656])
+def test_encoder_head_mlp2_matches_fp64(dev, N):
+    """bgnn_mlp2 (the encoder's Linear(16,64).ReLU.Linear(64,128).ReLU on the VALU, weights in
+    LDS) against an fp64 torch run: output, max|h|, and the four parameter gradients; the
+    backward is deterministic (bit-identical on a second run)."""
+    from bgnn import fused
+    torch.manual_seed(N)
+    seq = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 128), torch.nn.ReLU())
+    seq = seq.to(dev)
+    x = torch.randn(N, 16, device=dev)
+    gy = torch.randn(N, 128, device=dev)
+    assert fused._mlp2_prefix(list(seq), x)
+    h, amax = fused.mlp(seq, x, return_amax=True)
+    (h * gy).sum().backward()
+    grads = [p.grad.clone() for p in seq.parameters()]
+    for p in seq.parameters():
+        p.grad = None
+    h2, _ = fused.mlp(seq, x, return_amax=True)
+    (h2 * gy).sum().backward()
+    for g, p in zip(grads, seq.parameters()):
+        assert torch.equal(g, p.grad)
+    ref = copy.deepcopy(seq).double().cpu()
+    hr = ref(x.double().cpu())
+    (hr * gy.double().cpu()).sum().backward()
+    torch.testing.assert_close(h.double().cpu(), hr, rtol=1e-5, atol=1e-5)
+    assert float(amax) == float(h.abs().max())
+    for g, p in zip(grads, ref.parameters()):
+        scale = p.grad.abs().max().item() + 1e-30
+        assert (g.double().cpu() - p.grad).abs().max().item() <= 1e-5 * scale + 1e-6
