@@ -239,8 +239,10 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, rel
 
 
 # the node encoder's leading Linear(16,64).ReLU.Linear(64,128).ReLU as one VALU kernel
-# (bgnn_mlp2_fwd / _bwd) instead of two GEMM launches with their operand-max passes
-FUSED_MLP2 = True
+# (bgnn_mlp2_fwd / _bwd) instead of two GEMM launches with their operand-max passes. Off:
+# measured slower in the cfg2 step (tools/ab_step.py: 10.09 vs 9.88 ms/step; fwd 188 us,
+# bwd 325 us + 64 us slot sums at one 4-wave workgroup per CU, latency-bound LDS chains)
+FUSED_MLP2 = False
 
 
 class _Mlp2Fn(torch.autograd.Function):
@@ -368,7 +370,9 @@ class SageLayerFn(torch.autograd.Function):
                 bf = torch.mv(wcat, b_in)
             else:
                 wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False)
-                bf = torch.mv(wcat, b_in)   # a GEMV (f32 accumulation): no GEMM tile launch for one column
+                # (bgnn GEMM, not torch.mv: rocBLAS's GEMV moved the BN-amplified gradients of the
+                # Shared variant 50x further from fp64, tests/test_gpu_fold.py)
+                bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False).view(-1)
             absmax(wf, w_amax, accumulate=True)
             wmat = wf
         else:
@@ -497,7 +501,7 @@ class SageLayerFn(torch.autograd.Function):
                 dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)             # [2H, H]
                 dw.add_(torch.outer(dbf, b_in))
                 dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                       # [H, K_in]
-                db_in = torch.mv(wcat.t(), dbf)                                            # [H] (GEMV)
+                db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)  # [H]
             return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
                     None, None, None, None, None, dw_in, db_in)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev

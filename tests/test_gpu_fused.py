@@ -128,6 +128,16 @@ def test_encoder_head_mlp2_matches_fp64(dev, N):
     LDS) against an fp64 torch run: output, max|h|, and the four parameter gradients; the
     backward is deterministic (bit-identical on a second run)."""
     from bgnn import fused
+    old = fused.FUSED_MLP2
+    fused.FUSED_MLP2 = True
+    try:
+        _check_mlp2(dev, N)
+    finally:
+        fused.FUSED_MLP2 = old
+
+
+def _check_mlp2(dev, N):
+    from bgnn import fused
     torch.manual_seed(N)
     seq = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 128), torch.nn.ReLU())
     seq = seq.to(dev)
