@@ -107,6 +107,8 @@ SIGNATURES = {
     "bgnn_mlp2_bwd_ws_bytes": (c_sz, [c_i64]),
     "bgnn_mlp2_bwd": (c_i32, [c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                               c_sz, c_p]),
+    "bgnn_gemm_f32_dropadd": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,
+                                      c_p, c_p, c_i64, c_f32, c_u64, c_p, c_sz, c_p]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,
                               c_p, c_sz, c_p]),
 }

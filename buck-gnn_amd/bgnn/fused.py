@@ -43,6 +43,9 @@ DGRAD_WT = True
 # both are f32-class, torch.mm saved ~1 % of the step but shifts the BN-amplified gradient
 # rounding noise, tools/fold_ab.py)
 FOLD_WEIGHTS_TORCH = False
+# skip layers' dgrad adds the dropout-masked incoming gradient in its epilogue
+# (bgnn_gemm_f32_dropadd) instead of reading a skip gradient bgnn_sage_bwd_rows wrote
+DGRAD_DROPADD = True
 
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
@@ -462,14 +465,18 @@ class SageLayerFn(torch.autograd.Function):
         else:
             dz = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)
             dzl, dh, lddz = dz, dz[:, H:], 2 * H
-        gskip = torch.empty(N, H, dtype=torch.float32, device=dev) if cfg.skip else None
+        # skip layers: the dgrad's epilogue adds drop(g) itself (bgnn_gemm_f32_dropadd), so
+        # bgnn_sage_bwd_rows does not write the [N, H] skip gradient
+        dropadd = (cfg.skip and DGRAD_DROPADD and GEMM_BACKEND == "hip" and DGRAD_WT and not planes
+                   and H % 4 == 0 and _lib.query("bgnn_get_tuning", 5) == 2)
+        gskip = torch.empty(N, H, dtype=torch.float32, device=dev) if (cfg.skip and not dropadd) else None
         rs = _lib.query("bgnn_rows_slots", N)
         part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
         _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), o.data_ptr(), nrm.data_ptr(),
                   _ptr(scale) if bn else None, _ptr(shift) if bn else None,
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
-                  float(cfg.p), cfg.seed, int(cfg.skip), N, H, dh.data_ptr(), lddz, _ptr(gskip),
+                  float(cfg.p), cfg.seed, int(cfg.skip and not dropadd), N, H, dh.data_ptr(), lddz, _ptr(gskip),
                   part_db.data_ptr(), dz_amax.data_ptr(), graph.fwd.rowptr.data_ptr() if ctx.folded else None,
                   (2 if cfg.reduce == 1 else 1) if ctx.folded else 0, s)
         db = torch.empty(2 if ctx.folded else 1, H, dtype=torch.float32, device=dev)
@@ -507,7 +514,15 @@ class SageLayerFn(torch.autograd.Function):
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
         wcat_t = wcat.t().contiguous() if DGRAD_WT else wcat
-        if gskip is not None:
+        if dropadd:
+            dx = torch.empty(N, H, dtype=torch.float32, device=dev)
+            M_, K_ = N, 2 * H
+            ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M_, H, K_, 0, 1, 0)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
+            _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M_, H, K_, dz.data_ptr(), lddz, wcat_t.data_ptr(),
+                      wcat_t.stride(0), dx.data_ptr(), H, dz_amax.data_ptr(), w_amax.data_ptr(), g.data_ptr(), H,
+                      float(cfg.p), cfg.seed, _ptr(ws), ws_bytes, s)
+        elif gskip is not None:
             dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, out=gskip, beta=1.0, a_amax=dz_amax,
                       b_amax=w_amax)
         else:

@@ -508,12 +508,50 @@ extern "C" int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64
     return BGNN_OK;
 }
 
+// beta operand from a dropout-masked source (bgnn_gemm_f32_dropadd); NULL src = from C
+struct BetaSrc {
+    const float* src;
+    int64_t ld;
+    uint64_t seed;
+    float p;
+};
+
+static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
+                            const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
+                            int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
+                            int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
+                            const float* b_amax, float* c_amax, int32_t precision, void* ws,
+                            size_t ws_bytes, void* stream, const BetaSrc& bs);
+
 extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
                                     const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
                                     int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
                                     int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
                                     const float* b_amax, float* c_amax, int32_t precision, void* ws,
                                     size_t ws_bytes, void* stream) {
+    return gemm_scaled_impl(ta, tb, M, N, K, alpha, A, lda, a_blk, a_pstride, B, ldb, beta, C, ldc, c_blk,
+                            c_pstride, bias, relu, a_amax, b_amax, c_amax, precision, ws, ws_bytes, stream,
+                            BetaSrc{nullptr, 0, 0, 0.f});
+}
+
+extern "C" int bgnn_gemm_f32_dropadd(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
+                                     int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                                     const float* a_amax, const float* b_amax, const float* src, int64_t ld_src,
+                                     float p, uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+    BGNN_REQUIRE(src != nullptr && ld_src >= N && ld_src % 4 == 0 && N % 4 == 0 && ((uintptr_t)src & 15) == 0,
+                 "gemm_dropadd: src must be 16-byte aligned with N and ld_src multiples of 4");
+    BGNN_REQUIRE(gemm_mode() == 2 && ta == 0 && tb == 1,
+                 "gemm_dropadd: built for the f16x3 family (BGNN_TUNE_GEMM_MODE 2) and C = A B^T only");
+    return gemm_scaled_impl(ta, tb, M, N, K, 1.f, A, lda, 0, 0, B, ldb, 1.f, C, ldc, 0, 0, nullptr, 0, a_amax,
+                            b_amax, nullptr, 0, ws, ws_bytes, stream, BetaSrc{src, ld_src, seed, p});
+}
+
+static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
+                            const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
+                            int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
+                            int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
+                            const float* b_amax, float* c_amax, int32_t precision, void* ws,
+                            size_t ws_bytes, void* stream, const BetaSrc& bs) {
     BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
     BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
     const int64_t a_inner = a_blk > 0 ? a_blk : (ta ? M : K);
@@ -556,9 +594,20 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     }
     int split = Mt > 0 ? 1 : pl.split;
     if (split > 1 && (slabs == nullptr || slab_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
+    if (bs.src) {   // the masked beta source lives in the split kernels' epilogue: no split-K, no tail
+        BGNN_REQUIRE(pl.x6 && pl.prec == 1 && Mt == 0, "gemm_dropadd: needs the f16x3 kernels without a tail split");
+        split = 1;
+    }
     const int64_t Ma = pl.rows_a;
     GemmArgs g{A, B, C, slabs, Ma, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
                a_blk, a_pstride, c_blk, c_pstride, a_amax, b_amax, nullptr};
+    if (bs.src) {
+        g.bsrc = bs.src;
+        g.ld_bsrc = bs.ld;
+        g.dseed = bs.seed;
+        g.dthr = dropout_threshold(bs.p);
+        g.dkeep = g.dthr ? 1.f / (1.f - bs.p) : 1.f;
+    }
     // max |C| for the next GEMM's operand scale: in the split kernels' epilogue, else one pass
     const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1 && Mt == 0;
     if (c_amax_fused) g.c_amax = c_amax;
@@ -567,8 +616,8 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
     g.kchunk = kc > 0 ? kc : pl.bk;
     const int64_t tiles_a = ((Ma + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
     dim3 grid((unsigned)tiles_a, split);
-    if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, Ma, N), s, g);
-    else if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, g_gemm_abl, grid, s, g);
+    if (!bs.src && use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, Ma, N), s, g);
+    else if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, bs.src ? 8 : g_gemm_abl, grid, s, g);
     else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
     else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
     else if (ta == 1 && tb == 0) launch_cfg<1, 0>(pl.cfg, grid, s, g);

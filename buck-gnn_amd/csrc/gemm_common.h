@@ -27,7 +27,24 @@ struct GemmArgs {
     // (EA_GNN's node-level blocks of the edge Linears, bgnn/ea.py); NULL = off
     const float* ga0; const int64_t* gi0; int64_t ldg0;
     const float* ga1; const int64_t* gi1; int64_t ldg1;
+    // split kernels, no split-K: the beta operand read from bsrc [M, ld_bsrc] through a dropout
+    // mask instead of from C -- the dgrad of a SAGE skip layer adds drop(g) recomputed from the
+    // layer's counter-based mask (keep_bits4(dseed, (row * ld_bsrc + col) / 4, dthr), kept
+    // values scaled by dkeep; dthr = 0: no mask), so bgnn_sage_bwd_rows need not write it
+    const float* bsrc; int64_t ld_bsrc; uint64_t dseed; uint32_t dthr; float dkeep;
 };
+
+// the beta operand of 4 consecutive columns (col % 4 == 0) of row `row`: masked bsrc
+__device__ __forceinline__ void beta_src4(const GemmArgs& g, int64_t row, int64_t col, float (&pv)[4]) {
+    const int64_t i = row * g.ld_bsrc + col;
+    const float4 t = *reinterpret_cast<const float4*>(g.bsrc + i);
+    const uint32_t m = g.dthr ? keep_bits4(g.dseed, (uint64_t)(i >> 2), g.dthr) : 0xFu;
+    const float kf = g.dthr ? g.dkeep : 1.f;
+    pv[0] = (m & 1u) ? t.x * kf : 0.f;
+    pv[1] = (m & 2u) ? t.y * kf : 0.f;
+    pv[2] = (m & 4u) ? t.z * kf : 0.f;
+    pv[3] = (m & 8u) ? t.w * kf : 0.f;
+}
 
 // Base pointer that makes plane-split storage addressable with global coordinates:
 // element with split-dim index x lives at P + (x / blk) * pstride + (x % blk); for all x of

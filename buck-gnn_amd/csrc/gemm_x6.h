@@ -122,9 +122,15 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                     if (g.ga1) a1 = *reinterpret_cast<const float4*>(g.ga1 + g.gi1[row] * g.ldg1 + col);
                 }
                 const float x0[4] = {a0.x, a0.y, a0.z, a0.w}, x1[4] = {a1.x, a1.y, a1.z, a1.w};
-                float4 c4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (g.beta != 0.f) c4 = *reinterpret_cast<const float4*>(p);
-                const float pv[4] = {c4.x, c4.y, c4.z, c4.w};
+                float pv[4] = {0.f, 0.f, 0.f, 0.f};
+                if (g.beta != 0.f) {
+                    if constexpr (ABL == 8) {   // beta operand = masked bsrc (bgnn_gemm_f32_dropadd)
+                        beta_src4(g, r0 + q * 8 + rq, col, pv);
+                    } else {
+                        const float4 c4 = *reinterpret_cast<const float4*>(p);
+                        pv[0] = c4.x; pv[1] = c4.y; pv[2] = c4.z; pv[3] = c4.w;
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     float v = one_mul ? e[k] * iab : (e[k] * ia) * ib;
@@ -161,7 +167,9 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
             if (!split) {
                 float prev[4] = {0.f, 0.f, 0.f, 0.f}, bv[4] = {0.f, 0.f, 0.f, 0.f};
                 if (g.beta != 0.f) {
-                    if (full) {
+                    if constexpr (ABL == 8) {   // (the host requires N % 4 == 0: every float4 is whole)
+                        beta_src4(g, row, col, prev);
+                    } else if (full) {
                         const float4 t = *reinterpret_cast<const float4*>(p);
                         prev[0] = t.x; prev[1] = t.y; prev[2] = t.z; prev[3] = t.w;
                     } else {

@@ -396,6 +396,10 @@ static void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 template <int PREC, int TA, int TB>
 static void launch_x6_t(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if (abl == 0) { launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g); return; }
+    // 8 = the dgrad epilogue with the masked beta source (bgnn_gemm_f32_dropadd; f16x3, C = A B^T)
+    if constexpr (PREC == 1 && TA == 0 && TB == 1) {
+        if (abl == 8) { launch_x6_a<PREC, TA, TB, 8>(cfg, grid, s, g); return; }
+    }
     // ablations are built for the forward shape only (TA = 0, TB = 1)
     if constexpr (TA == 0 && TB == 1) {
         switch (abl) {

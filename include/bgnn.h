@@ -311,6 +311,16 @@ int bgnn_gemm_f32_scaled(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
 /* Workspace of bgnn_gemm_f32_scaled for a given precision (0 = f32-accurate, the family of
  * BGNN_TUNE_GEMM_MODE; 1 = bf16 operands rounded to nearest, one MFMA product, f32
  * accumulation and output: the bf16 EA_GNN path of BASELINE configs[4]). */
+/* C = A' B' + drop(src): the dgrad of a SAGE skip layer (Models/BuckGNN.py:441-444) with the
+ * skip gradient drop(g) recomputed from the layer's counter-based dropout mask (seed, p; the
+ * mask bgnn_sage_apply / bgnn_sage_bwd_rows use, element (r, c) of src [M, ld_src]) in the
+ * GEMM epilogue, instead of being written by bgnn_sage_bwd_rows and read back as C. f16x3 mode
+ * (BGNN_TUNE_GEMM_MODE 2) and trans_a = 0, trans_b = 1 only; N and ld_src multiples of 4, src
+ * 16-byte aligned. */
+int bgnn_gemm_f32_dropadd(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
+                          const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                          const float* a_amax, const float* b_amax, const float* src, int64_t ld_src,
+                          float p, uint64_t seed, void* ws, size_t ws_bytes, void* stream);
 size_t bgnn_gemm_ws_bytes_ex(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b,
                              int32_t precision);
 /* C = act(op(A) op(B) + bias + add0[idx0[r], :] (+ add1[idx1[r], :])) -- gathered row adds
