@@ -242,10 +242,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, rel
 
 
 # the node encoder's leading Linear(16,64).ReLU.Linear(64,128).ReLU as one VALU kernel
-# (bgnn_mlp2_fwd / _bwd) instead of two GEMM launches with their operand-max passes. Off:
-# measured slower in the cfg2 step (tools/ab_step.py: 10.09 vs 9.88 ms/step; fwd 188 us,
-# bwd 325 us + 64 us slot sums at one 4-wave workgroup per CU, latency-bound LDS chains)
-FUSED_MLP2 = False
+# (bgnn_mlp2_fwd / _bwd) instead of two GEMM launches with their operand-max passes:
+# fwd 57 us, bwd 108 us + 11 us slot sums on cfg2; the step 9.94 -> 9.82 ms (tools/ab_step.py)
+FUSED_MLP2 = True
 
 
 class _Mlp2Fn(torch.autograd.Function):

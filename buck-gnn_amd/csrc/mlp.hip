@@ -24,8 +24,8 @@ struct MlpSmem {
     float b1[D1];
     float w2t[D1][D2];         // W2^T (forward) -- the backward keeps W2 as [D2][D1] in the same space
     float b2[D2];
-    float xs[kT][F + 1];
-    float h1[kT][D1 + 1];
+    float xs[kT][F + 4];       // row strides multiples of 4: float4 reads
+    float h1[kT][D1 + 4];
 };
 
 template <int F, int D1, int D2>
@@ -45,41 +45,55 @@ __device__ __forceinline__ void load_weights(MlpSmem<F, D1, D2>& S, const float*
     for (int i = threadIdx.x; i < D2; i += 256) S.b2[i] = b2 ? b2[i] : 0.f;
 }
 
-// h1[n][:] = ReLU(x[n] W1^T + b1) for the tile's nodes (xs loaded): 4 threads per node,
-// D1 / 4 outputs each
+__device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+
+// h1 = ReLU(x W1^T + b1) for the tile's 64 nodes (xs loaded): thread = 4 nodes x 4 hidden units
 template <int F, int D1, int D2>
 __device__ __forceinline__ void hidden(MlpSmem<F, D1, D2>& S) {
-    constexpr int P = D1 / 4;
-    const int n = threadIdx.x >> 2, jb = (threadIdx.x & 3) * P;
-    float acc[P];
+    static_assert(D1 == 64 && kT == 64, "hidden: 16 x 16 threads of 4 nodes x 4 units");
+    const int tn = threadIdx.x >> 4, tk = threadIdx.x & 15;
+    float acc[4][4];
 #pragma unroll
-    for (int q = 0; q < P; ++q) acc[q] = S.b1[jb + q];
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[i][c] = S.b1[tk * 4 + c];
 #pragma unroll
     for (int f = 0; f < F; ++f) {
-        const float xv = S.xs[n][f];
+        float w[4];
+        ld4(&S.w1t[f][tk * 4], w);
 #pragma unroll
-        for (int q = 0; q < P; ++q) acc[q] = fmaf(xv, S.w1t[f][jb + q], acc[q]);
+        for (int i = 0; i < 4; ++i) {
+            const float xv = S.xs[tn * 4 + i][f];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[i][c] = fmaf(xv, w[c], acc[i][c]);
+        }
     }
 #pragma unroll
-    for (int q = 0; q < P; ++q) S.h1[n][jb + q] = fmaxf(acc[q], 0.f);
+    for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<float4*>(&S.h1[tn * 4 + i][tk * 4]) =
+            make_float4(fmaxf(acc[i][0], 0.f), fmaxf(acc[i][1], 0.f), fmaxf(acc[i][2], 0.f), fmaxf(acc[i][3], 0.f));
 }
 
 template <int F>
-__device__ __forceinline__ void load_x(float (*xs)[F + 1], const float* x, int64_t n0, int64_t N) {
+__device__ __forceinline__ void load_x(float (*xs)[F + 4], const float* x, int64_t n0, int64_t N) {
     for (int i = threadIdx.x; i < kT * F; i += 256) {
         const int n = i / F, f = i % F;
         xs[n][f] = (n0 + n < N) ? x[(n0 + n) * F + f] : 0.f;
     }
 }
 
+// forward: thread = 4 nodes x 8 outputs of layer 2 (W2^T row segments as float4 pairs)
 template <int F, int D1, int D2>
 __global__ __launch_bounds__(256) void k_mlp2_fwd(const float* __restrict__ x, int64_t N, const float* W1,
                                                   const float* b1, const float* W2, const float* b2,
                                                   float* __restrict__ h, uint32_t* __restrict__ amax) {
+    static_assert(D2 == 128, "k_mlp2_fwd: 16 column groups of 8");
     __shared__ MlpSmem<F, D1, D2> S;
     load_weights(S, W1, b1, W2, b2, true);
-    constexpr int P = D2 / 4;   // outputs per thread
-    const int n = threadIdx.x >> 2, jb = (threadIdx.x & 3) * P;
+    const int tn = threadIdx.x >> 4, tj = threadIdx.x & 15;
     uint32_t m = 0;
     const int64_t tiles = (N + kT - 1) / kT;
     for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
@@ -89,29 +103,37 @@ __global__ __launch_bounds__(256) void k_mlp2_fwd(const float* __restrict__ x, i
         __syncthreads();
         hidden(S);
         __syncthreads();
-        float acc[P];
+        float acc[4][8];
 #pragma unroll
-        for (int q = 0; q < P; ++q) acc[q] = S.b2[jb + q];
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc[i][c] = S.b2[tj * 8 + c];
         for (int k = 0; k < D1; ++k) {
-            const float hv = S.h1[n][k];
+            float wa[4], wb[4];
+            ld4(&S.w2t[k][tj * 8], wa);
+            ld4(&S.w2t[k][tj * 8 + 4], wb);
 #pragma unroll
-            for (int q = 0; q < P; q += 4) {
-                const float4 w = *reinterpret_cast<const float4*>(&S.w2t[k][jb + q]);
-                acc[q] = fmaf(hv, w.x, acc[q]);
-                acc[q + 1] = fmaf(hv, w.y, acc[q + 1]);
-                acc[q + 2] = fmaf(hv, w.z, acc[q + 2]);
-                acc[q + 3] = fmaf(hv, w.w, acc[q + 3]);
+            for (int i = 0; i < 4; ++i) {
+                const float hv = S.h1[tn * 4 + i][k];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    acc[i][c] = fmaf(hv, wa[c], acc[i][c]);
+                    acc[i][c + 4] = fmaf(hv, wb[c], acc[i][c + 4]);
+                }
             }
         }
-        if (n0 + n < N) {
-            float* out = h + (n0 + n) * D2 + jb;
 #pragma unroll
-            for (int q = 0; q < P; q += 4) {
-                const float4 v = make_float4(fmaxf(acc[q], 0.f), fmaxf(acc[q + 1], 0.f), fmaxf(acc[q + 2], 0.f),
-                                             fmaxf(acc[q + 3], 0.f));
+        for (int i = 0; i < 4; ++i) {
+            const int64_t node = n0 + tn * 4 + i;
+            if (node >= N) continue;
+            float* out = h + node * D2 + tj * 8;
+#pragma unroll
+            for (int c = 0; c < 8; c += 4) {
+                const float4 v = make_float4(fmaxf(acc[i][c], 0.f), fmaxf(acc[i][c + 1], 0.f),
+                                             fmaxf(acc[i][c + 2], 0.f), fmaxf(acc[i][c + 3], 0.f));
                 m = max(m, max(max(__float_as_uint(v.x), __float_as_uint(v.y)),
                                max(__float_as_uint(v.z), __float_as_uint(v.w))));   // (>= 0)
-                *reinterpret_cast<float4*>(out + q) = v;
+                *reinterpret_cast<float4*>(out + c) = v;
             }
         }
     }
@@ -127,91 +149,137 @@ template <int F, int D1, int D2>
 __global__ __launch_bounds__(256) void k_mlp2_bwd(const float* __restrict__ x, int64_t N, const float* W1,
                                                   const float* b1, const float* W2, const float* __restrict__ h,
                                                   const float* __restrict__ dh, float* __restrict__ part) {
-    extern __shared__ float dyn[];   // g2 [kT][D2 + 1], g1 [kT][D1 + 1]
+    static_assert(D2 == 128 && D1 == 64 && F == 16, "k_mlp2_bwd: built for 16 x 64 x 128");
+    constexpr int G2 = D2 + 4, G1 = D1 + 4;
+    extern __shared__ float dyn[];   // g2 [kT][G2], g1 [kT][G1]
     __shared__ MlpSmem<F, D1, D2> S;
-    float (*g2)[D2 + 1] = reinterpret_cast<float (*)[D2 + 1]>(dyn);
-    float (*g1)[D1 + 1] = reinterpret_cast<float (*)[D1 + 1]>(dyn + kT * (D2 + 1));
+    float (*g2)[G2] = reinterpret_cast<float (*)[G2]>(dyn);
+    float (*g1)[G1] = reinterpret_cast<float (*)[G1]>(dyn + kT * G2);
     load_weights(S, W1, b1, W2, nullptr, false);   // W2 kept as [D2][D1] in S.w2t's space
     const float* w2 = &S.w2t[0][0];
-    // dW2: thread owns row j = tid / 2, columns kb..kb+D1/2 (D2 = 128 rows x 2 halves = 256 threads)
-    static_assert(D2 * 2 == 256, "k_mlp2_bwd: D2 must be 128");
-    constexpr int HK = D1 / 2;
-    const int j2 = threadIdx.x >> 1, kb2 = (threadIdx.x & 1) * HK;
-    float dw2[HK];
+    const int hi = threadIdx.x >> 4, lo = threadIdx.x & 15;
+    // dW2: rows hi*8..+8, columns lo*4..+4 (32 accumulators); db2 by the lo == 0 threads
+    float dw2[8][4], db2[8];
 #pragma unroll
-    for (int q = 0; q < HK; ++q) dw2[q] = 0.f;
-    float db2 = 0.f;
-    // g1: 4 threads per node, D1 / 4 columns each; dW1: thread owns (k = tid / 4, F / 4 columns)
-    constexpr int P1 = D1 / 4, PF = F / 4;
-    static_assert(D1 * 4 == 256, "k_mlp2_bwd: D1 must be 64");
-    const int n1 = threadIdx.x >> 2, kb1 = (threadIdx.x & 3) * P1;
-    const int k1 = threadIdx.x >> 2, fb1 = (threadIdx.x & 3) * PF;
-    float dw1[PF];
+    for (int c = 0; c < 8; ++c) {
+        db2[c] = 0.f;
 #pragma unroll
-    for (int q = 0; q < PF; ++q) dw1[q] = 0.f;
+        for (int q = 0; q < 4; ++q) dw2[c][q] = 0.f;
+    }
+    // dW1: row k1 = tid / 4, columns fb1..fb1+4; db1 by the fb1 == 0 threads
+    const int k1 = threadIdx.x >> 2, fb1 = (threadIdx.x & 3) * 4;
+    float dw1[4] = {0.f, 0.f, 0.f, 0.f};
     float db1 = 0.f;
     const int64_t tiles = (N + kT - 1) / kT;
     for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
         const int64_t n0 = t * kT;
         __syncthreads();
         load_x<F>(S.xs, x, n0, N);
-        for (int i = threadIdx.x; i < kT * D2; i += 256) {
-            const int n = i / D2, j = i % D2;
-            float v = 0.f;
+        for (int i = threadIdx.x; i < kT * (D2 / 4); i += 256) {
+            const int n = i / (D2 / 4), j4 = (i % (D2 / 4)) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (n0 + n < N) {
-                const int64_t o = (n0 + n) * D2 + j;
-                v = h[o] > 0.f ? dh[o] : 0.f;
+                const int64_t o = (n0 + n) * D2 + j4;
+                const float4 hv = *reinterpret_cast<const float4*>(h + o);
+                const float4 gv = *reinterpret_cast<const float4*>(dh + o);
+                v = make_float4(hv.x > 0.f ? gv.x : 0.f, hv.y > 0.f ? gv.y : 0.f, hv.z > 0.f ? gv.z : 0.f,
+                                hv.w > 0.f ? gv.w : 0.f);
             }
-            g2[n][j] = v;
+            *reinterpret_cast<float4*>(&g2[n][j4]) = v;
         }
         __syncthreads();
         hidden(S);
         __syncthreads();
-        // weight / bias gradients of layer 2 (rows of padded tail nodes are zero in g2)
+        // layer-2 weight / bias gradients (rows of padded tail nodes are zero in g2)
         for (int n = 0; n < kT; ++n) {
-            const float gv = g2[n][j2];
-            db2 += (kb2 == 0) ? gv : 0.f;
+            float ga[4], gb[4], hv[4];
+            ld4(&g2[n][hi * 8], ga);
+            ld4(&g2[n][hi * 8 + 4], gb);
+            ld4(&S.h1[n][lo * 4], hv);
 #pragma unroll
-            for (int q = 0; q < HK; ++q) dw2[q] = fmaf(gv, S.h1[n][kb2 + q], dw2[q]);
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    dw2[c][q] = fmaf(ga[c], hv[q], dw2[c][q]);
+                    dw2[c + 4][q] = fmaf(gb[c], hv[q], dw2[c + 4][q]);
+                }
+            }
+            if (lo == 0) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    db2[c] += ga[c];
+                    db2[c + 4] += gb[c];
+                }
+            }
         }
-        // g1 = (g2 W2) masked by h1 > 0
+        // g1 = (g2 W2) masked by h1 > 0: thread = 4 nodes (hi) x 4 hidden units (lo)
         {
-            float acc[P1];
+            float acc[4][4];
 #pragma unroll
-            for (int q = 0; q < P1; ++q) acc[q] = 0.f;
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[i][q] = 0.f;
             for (int j = 0; j < D2; ++j) {
-                const float gv = g2[n1][j];
+                float w[4];
+                ld4(&w2[j * D1 + lo * 4], w);
 #pragma unroll
-                for (int q = 0; q < P1; ++q) acc[q] = fmaf(gv, w2[j * D1 + kb1 + q], acc[q]);
+                for (int i = 0; i < 4; ++i) {
+                    const float gv = g2[hi * 4 + i][j];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(gv, w[q], acc[i][q]);
+                }
             }
 #pragma unroll
-            for (int q = 0; q < P1; ++q) g1[n1][kb1 + q] = S.h1[n1][kb1 + q] > 0.f ? acc[q] : 0.f;
+            for (int i = 0; i < 4; ++i) {
+                float hv[4];
+                ld4(&S.h1[hi * 4 + i][lo * 4], hv);
+                *reinterpret_cast<float4*>(&g1[hi * 4 + i][lo * 4]) =
+                    make_float4(hv[0] > 0.f ? acc[i][0] : 0.f, hv[1] > 0.f ? acc[i][1] : 0.f,
+                                hv[2] > 0.f ? acc[i][2] : 0.f, hv[3] > 0.f ? acc[i][3] : 0.f);
+            }
         }
         __syncthreads();
         for (int n = 0; n < kT; ++n) {
             const float gv = g1[n][k1];
+            float xv[4];
+            ld4(&S.xs[n][fb1], xv);
             db1 += (fb1 == 0) ? gv : 0.f;
 #pragma unroll
-            for (int q = 0; q < PF; ++q) dw1[q] = fmaf(gv, S.xs[n][fb1 + q], dw1[q]);
+            for (int q = 0; q < 4; ++q) dw1[q] = fmaf(gv, xv[q], dw1[q]);
         }
     }
     float* p = part + (int64_t)blockIdx.x * (D2 * D1 + D2 + D1 * F + D1);
 #pragma unroll
-    for (int q = 0; q < HK; ++q) p[j2 * D1 + kb2 + q] = dw2[q];
-    if (kb2 == 0) p[D2 * D1 + j2] = db2;
-#pragma unroll
-    for (int q = 0; q < PF; ++q) p[D2 * D1 + D2 + k1 * F + fb1 + q] = dw1[q];
+    for (int c = 0; c < 8; ++c) {
+        *reinterpret_cast<float4*>(p + (hi * 8 + c) * D1 + lo * 4) = make_float4(dw2[c][0], dw2[c][1], dw2[c][2], dw2[c][3]);
+        if (lo == 0) p[D2 * D1 + hi * 8 + c] = db2[c];
+    }
+    *reinterpret_cast<float4*>(p + D2 * D1 + D2 + k1 * F + fb1) = make_float4(dw1[0], dw1[1], dw1[2], dw1[3]);
     if (fb1 == 0) p[D2 * D1 + D2 + D1 * F + k1] = db1;
 }
 
-// sum over the slots s (in order) of part[s][i], scattered into [dW2 | db2 | dW1 | db1]
-__global__ __launch_bounds__(256) void k_sum_slots(const float* __restrict__ part, int slots, int L, int L0,
-                                                   int L1, int L2, float* __restrict__ o0, float* __restrict__ o1,
+// two-stage, fixed-order slot sums: stage 1 sums slot group y (slots [y*per, (y+1)*per)) of
+// column i into tmp[y][i]; stage 2 sums the groups in order into [dW2 | db2 | dW1 | db1]
+constexpr int kSumGroups = 16;
+
+__global__ __launch_bounds__(256) void k_sum_slots1(const float* __restrict__ part, int slots, int L,
+                                                    float* __restrict__ tmp) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= L) return;
+    const int per = (slots + kSumGroups - 1) / kSumGroups;
+    const int s0 = blockIdx.y * per, s1 = min(slots, s0 + per);
+    float s = 0.f;
+    for (int k = s0; k < s1; ++k) s += part[(int64_t)k * L + i];
+    tmp[(int64_t)blockIdx.y * L + i] = s;
+}
+
+__global__ __launch_bounds__(256) void k_sum_slots(const float* __restrict__ tmp, int L, int L0, int L1, int L2,
+                                                   float* __restrict__ o0, float* __restrict__ o1,
                                                    float* __restrict__ o2, float* __restrict__ o3) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= L) return;
     float s = 0.f;
-    for (int k = 0; k < slots; ++k) s += part[(int64_t)k * L + i];
+    for (int k = 0; k < kSumGroups; ++k) s += tmp[(int64_t)k * L + i];
     if (i < L0) o0[i] = s;
     else if (i < L0 + L1) o1[i - L0] = s;
     else if (i < L0 + L1 + L2) o2[i - L0 - L1] = s;
@@ -221,9 +289,9 @@ __global__ __launch_bounds__(256) void k_sum_slots(const float* __restrict__ par
 constexpr int kF = 16, kD1 = 64, kD2 = 128;
 constexpr int kPartLen = kD2 * kD1 + kD2 + kD1 * kF + kD1;
 
-inline int mlp_blocks(int64_t N) {
+inline int mlp_blocks(int64_t N, int cap = kMlpBlocks) {
     const int64_t tiles = (N + kT - 1) / kT;
-    return (int)(tiles < kMlpBlocks ? (tiles > 0 ? tiles : 1) : kMlpBlocks);
+    return (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
 }
 
 }  // namespace
@@ -244,14 +312,15 @@ extern "C" int bgnn_mlp2_fwd(const float* x, int64_t N, int32_t F, int32_t D1, i
     if (N == 0) return BGNN_OK;
     BGNN_REQUIRE(x && W1 && W2 && h, "mlp2: null pointer");
     BGNN_REQUIRE(aligned16(h), "mlp2: h must be 16-byte aligned");
-    hipLaunchKernelGGL((k_mlp2_fwd<kF, kD1, kD2>), dim3(mlp_blocks(N)), dim3(256), 0, as_stream(stream), x, N, W1,
+    // 2 workgroups per CU (58 KB of LDS each)
+    hipLaunchKernelGGL((k_mlp2_fwd<kF, kD1, kD2>), dim3(mlp_blocks(N, 2 * kMlpBlocks)), dim3(256), 0, as_stream(stream), x, N, W1,
                        b1, W2, b2, h, reinterpret_cast<uint32_t*>(h_amax));
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
 
 extern "C" size_t bgnn_mlp2_bwd_ws_bytes(int64_t N) {
-    return (size_t)mlp_blocks(N) * kPartLen * sizeof(float);
+    return (size_t)(mlp_blocks(N) + kSumGroups) * kPartLen * sizeof(float);
 }
 
 extern "C" int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, int32_t D2, const float* W1,
@@ -272,12 +341,16 @@ extern "C" int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, i
     BGNN_REQUIRE(ws && ws_bytes >= bgnn_mlp2_bwd_ws_bytes(N), "mlp2_bwd: workspace too small");
     const int blocks = mlp_blocks(N);
     float* part = static_cast<float*>(ws);
-    const size_t dyn = sizeof(float) * kT * ((kD2 + 1) + (kD1 + 1));
+    const size_t dyn = sizeof(float) * kT * ((kD2 + 4) + (kD1 + 4));
     hipLaunchKernelGGL((k_mlp2_bwd<kF, kD1, kD2>), dim3(blocks), dim3(256), dyn, s, x, N, W1, b1, W2, h, dh, part);
     BGNN_CHECK_LAUNCH();
     // slot sums straight into the four gradient tensors (partial layout [dW2 | db2 | dW1 | db1])
-    hipLaunchKernelGGL(k_sum_slots, dim3((kPartLen + 255) / 256), dim3(256), 0, s, part, blocks, kPartLen,
-                       kD2 * kD1, kD2, kD1 * kF, dW2, db2, dW1, db1);
+    float* tmp = part + (int64_t)blocks * kPartLen;
+    hipLaunchKernelGGL(k_sum_slots1, dim3((kPartLen + 255) / 256, kSumGroups), dim3(256), 0, s, part, blocks,
+                       kPartLen, tmp);
+    BGNN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_sum_slots, dim3((kPartLen + 255) / 256), dim3(256), 0, s, tmp, kPartLen, kD2 * kD1, kD2,
+                       kD1 * kF, dW2, db2, dW1, db1);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
