@@ -23,7 +23,7 @@ import torch
 from torch import Tensor, nn
 
 from .ea import graphnet_block
-from .fused import mlp, sage_layer
+from .fused import mlp, prepare_weights, sage_layer
 from .graph import Graph, SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
@@ -238,15 +238,19 @@ class BuckGNN(nn.Module):
             red = 1 if aggr == "mean" else 0
             amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
             bufs = torch.zeros(L, 3, dtype=torch.float32, device=x.device)   # per-layer operand maxima, one fill
+            layers = [convs[i] if convs is not None else self.shared_graphsage_block for i in range(L)]
+            wprep = prepare_weights([(c.lin_l.weight, c.lin_r.weight) for c in layers], bufs,
+                                    [not (i == 0 and x_in is not None) for i in range(L)])
+            self._count_bn_batches(bns)
             for i in range(L):
-                conv = convs[i] if convs is not None else self.shared_graphsage_block
+                conv = layers[i]
                 bn = bns[i] if bns is not None else None
                 skip = 0 < i < L - 1
                 fold = x_in if i == 0 else None
                 x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
                                      skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
                                      amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
-                                     b_in=None if fold is None else fold.bias)
+                                     b_in=None if fold is None else fold.bias, wprep=wprep[i], count_batch=False)
             return x
         if x_in is not None:   # (only reached when the caller folded the encoder's last Linear)
             x = x_in(x)
@@ -261,6 +265,15 @@ class BuckGNN(nn.Module):
                 x = x + x_prev
             x = self.dropout(x)
         return x
+
+    def _count_bn_batches(self, bns) -> None:
+        """BatchNorm1d's num_batches_tracked += 1 for every module of a fused loop in one launch
+        (the fused layers are then called with count_batch=False)."""
+        if bns is None or not self.training:
+            return
+        ts = [bn.num_batches_tracked for bn in bns if bn.track_running_stats]
+        if ts:
+            torch._foreach_add_(ts, 1)
 
     def _sag_sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, first_skip: bool,
                        x_amax: Optional[Tensor] = None, x_in: Optional[nn.Linear] = None) -> Tensor:

@@ -349,12 +349,14 @@ class SageLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_prev, x_amax, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
-                cfg: LayerConfig, amax=None, w_in=None, b_in=None):
+                cfg: LayerConfig, amax=None, w_in=None, b_in=None, wprep=None):
         dev = x_prev.device
         x_prev = x_prev.contiguous()
         H = w_l.size(0)
         N = x_prev.size(0)
-        wcat = torch.cat([w_l, w_r], 0).contiguous()             # [2H, H]
+        # [W_l;W_r] [2H, H] and its transpose (dgrad operand): from prepare_weights (all layers in
+        # a few launches; the amax slot then already holds max|W|) or built here
+        wcat, wcat_t_pre = wprep if wprep is not None else (torch.cat([w_l, w_r], 0).contiguous(), None)
         # operand maxima: [0] = max|W|, [1] = max|x_next| (this layer's output), [2] = max|dz|
         # (zeroed; the layer loop passes one slice of a single per-step fill)
         if amax is None:
@@ -378,7 +380,8 @@ class SageLayerFn(torch.autograd.Function):
             absmax(wf, w_amax, accumulate=True)
             wmat = wf
         else:
-            absmax(wcat, w_amax, accumulate=True)
+            if wprep is None:
+                absmax(wcat, w_amax, accumulate=True)
             wmat, bf = wcat, None
         if x_amax is None:
             x_amax = absmax(x_prev)
@@ -423,6 +426,7 @@ class SageLayerFn(torch.autograd.Function):
         ctx.graph = graph
         ctx.cfg = cfg
         ctx.folded = folded
+        ctx.wcat_t = wcat_t_pre
         ctx.fold = (w_in, b_in, wf) if folded else None
         ctx.save_for_backward(x_prev, o, nrm, wcat, gamma if gamma is not None else torch.empty(0, device=dev),
                               scale if scale is not None else torch.empty(0, device=dev),
@@ -509,10 +513,10 @@ class SageLayerFn(torch.autograd.Function):
                 dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                       # [H, K_in]
                 db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)  # [H]
             return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
-                    None, None, None, None, None, dw_in, db_in)
+                    None, None, None, None, None, dw_in, db_in, None)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
-        wcat_t = wcat.t().contiguous() if DGRAD_WT else wcat
+        wcat_t = (ctx.wcat_t if ctx.wcat_t is not None else wcat.t().contiguous()) if DGRAD_WT else wcat
         if dropadd:
             dx = torch.empty(N, H, dtype=torch.float32, device=dev)
             M_, K_ = N, 2 * H
@@ -529,13 +533,35 @@ class SageLayerFn(torch.autograd.Function):
         dw = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)      # [2H, H]
         dw_l, dw_r = dw[:H], dw[H:]
         return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
+
+
+def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
+    """[W_l;W_r] and its transpose for every layer of a loop in a few launches (one concatenation,
+    one transpose, one max|W| reduction, one copy) instead of three per layer. pairs: [(w_l, w_r)]
+    per layer; amax_bufs: the loop's zeroed [L, 3] operand-max slots, whose slot 0 receives
+    max|[W_l;W_r]| for the layers where fill_amax[i] (a folded layer scales by max|Wf| instead).
+    Returns [(wcat, wcat_t)] per layer (views of two [L, ...] buffers)."""
+    L = len(pairs)
+    H = pairs[0][0].size(0)
+    with torch.no_grad():   # operands only: the layers return the weight gradients themselves
+        W = torch.cat([t for pr in pairs for t in pr], 0).view(L, 2 * H, H)
+        Wt = W.transpose(1, 2).contiguous() if DGRAD_WT else None
+        m = torch.linalg.vector_norm(W, ord=float("inf"), dim=(1, 2))
+        if all(fill_amax):
+            amax_bufs[:, 0].copy_(m)
+        else:
+            idx = [i for i, f in enumerate(fill_amax) if f]
+            if idx:
+                sel = torch.tensor(idx, device=W.device)
+                amax_bufs[:, 0].index_copy_(0, sel, m.index_select(0, sel))
+    return [(W[i], Wt[i] if Wt is not None else None) for i in range(L)]
 
 
 def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
                seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None,
-               w_in: torch.Tensor = None, b_in: torch.Tensor = None):
+               w_in: torch.Tensor = None, b_in: torch.Tensor = None, wprep=None, count_batch: bool = True):
     """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
     x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
     spares the GEMM a pass over x_prev; return_amax: also return max|x_next|.
@@ -553,7 +579,7 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
     if bn_module is not None:
         use_batch_stats = training or not bn_module.track_running_stats
         momentum = bn_module.momentum
-        if training and bn_module.track_running_stats:
+        if training and bn_module.track_running_stats and count_batch:
             bn_module.num_batches_tracked.add_(1)
             if momentum is None:
                 momentum = 1.0 / float(bn_module.num_batches_tracked.item())
@@ -561,9 +587,10 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
-                                bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in)
+                                bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in,
+                                wprep)
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
-                                w_in, b_in)
+                                w_in, b_in, wprep)
     return out if return_amax else out[0]
