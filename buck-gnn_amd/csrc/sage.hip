@@ -10,7 +10,7 @@
 
 namespace bgnn {
 
-constexpr int kRowsBlocks = 1024;   // max partial slots for row-blocked reductions
+constexpr int kRowsBlocks = 1024;   // max partial slots for row-blocked reductions (2048: rows 112 -> 121 us, stats 58 -> 61 us)
 
 inline int64_t rows_grid(int64_t n_rows, int rows_per_block_min, int64_t* rpb) {
     int64_t blocks = (n_rows + rows_per_block_min - 1) / rows_per_block_min;
