@@ -537,8 +537,8 @@ class SageLayerFn(torch.autograd.Function):
 
 
 def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
-    """[W_l;W_r] and its transpose for every layer of a loop in a few launches (one concatenation,
-    one transpose, one max|W| reduction, one copy) instead of three per layer. pairs: [(w_l, w_r)]
+    """[W_l;W_r] and its transpose for every layer of a loop in one concatenation, one transpose
+    and one max|W| pass per layer, instead of three launches per layer. pairs: [(w_l, w_r)]
     per layer; amax_bufs: the loop's zeroed [L, 3] operand-max slots, whose slot 0 receives
     max|[W_l;W_r]| for the layers where fill_amax[i] (a folded layer scales by max|Wf| instead).
     Returns [(wcat, wcat_t)] per layer (views of two [L, ...] buffers)."""
@@ -547,14 +547,10 @@ def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
     with torch.no_grad():   # operands only: the layers return the weight gradients themselves
         W = torch.cat([t for pr in pairs for t in pr], 0).view(L, 2 * H, H)
         Wt = W.transpose(1, 2).contiguous() if DGRAD_WT else None
-        m = torch.linalg.vector_norm(W, ord=float("inf"), dim=(1, 2))
-        if all(fill_amax):
-            amax_bufs[:, 0].copy_(m)
-        else:
-            idx = [i for i, f in enumerate(fill_amax) if f]
-            if idx:
-                sel = torch.tensor(idx, device=W.device)
-                amax_bufs[:, 0].index_copy_(0, sel, m.index_select(0, sel))
+        # max|W| per layer with bgnn_absmax (torch's dim=(1, 2) max-reduction took 128 us here)
+        for i, f in enumerate(fill_amax):
+            if f:
+                absmax(W[i], amax_bufs[i, 0:1], accumulate=True)
     return [(W[i], Wt[i] if Wt is not None else None) for i in range(L)]
 
 
