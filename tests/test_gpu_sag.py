@@ -211,3 +211,44 @@ def test_sag_model_cfg2_sized_matches_oracle(dev, monkeypatch):
     np.testing.assert_array_equal(got["perm"].cpu().numpy(), pyg_ref.topk(scores["s"], 0.5, b.batch).numpy())
     same = np.mean(np.isin(got["perm"].cpu().numpy(), ref_perm.numpy()))
     assert same > 0.999
+
+
+@pytest.mark.parametrize("name,h,n", [("GraphSAGE_SAG", 512, 71), ("EAGNN_SAG", 64, 30)])
+def test_sag_adam_steps_follow_oracle(dev, name, h, n):
+    """Three Adam steps (lr 1e-3, dropout 0, BN in train mode) of the whole pooled model on the GPU
+    (fused SAGE / GraphNet layers, the folded encoder for GraphSAGE_SAG on 20k nodes, SAGPooling
+    forward + backward) follow the oracle's CPU trajectory: same losses to 1e-3 relative, finite
+    gradients for every trained parameter, the scorer included."""
+    b = Batch.from_data_list([S.make_mesh_graph(n, s) for s in range(4)])
+    torch.manual_seed(0)
+    m = bgnn.BuckGNN(16, 5, hidden_channels=h, num_layers=6, pooling_layer="mean", dropout_rate=0.0,
+                     model_name=name)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev).train()
+    bd = b.to(dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    crit = bgnn.RelativeErrorLoss()
+    ref_p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    used = [k for k, v in ref_p.items() if v.requires_grad]
+    ref_opt = torch.optim.Adam([ref_p[k] for k in used], lr=1e-3)
+    got, ref = [], []
+    for _ in range(3):
+        pred, _ = m(bd.x, bd.edge_index, bd.edge_attr, bd.batch)
+        loss = crit(pred, bd.y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        for k in ("pool.gnn.lin_l.weight", "pool.gnn.lin_r.weight"):
+            gk = dict(m.named_parameters())[k].grad
+            assert gk is not None and bool(torch.isfinite(gk).all()), k
+        for k, p in m.named_parameters():
+            if p.grad is not None:
+                assert bool(torch.isfinite(p.grad).all()), k
+        opt.step()
+        got.append(float(loss))
+        rp, _ = R.sag_forward(ref_p, name, b.x, b.edge_index, b.edge_attr, b.batch, True, 0.0)
+        rl = R.relative_error_loss(rp, b.y)
+        ref_opt.zero_grad(set_to_none=True)
+        rl.backward()
+        ref_opt.step()
+        ref.append(float(rl))
+    np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-5)
