@@ -22,7 +22,7 @@ from typing import Optional
 import torch
 from torch import Tensor, nn
 
-from .ea import graphnet_block
+from .ea import graphnet_block, skip_dropout
 from .fused import mlp, prepare_weights, sage_layer
 from .graph import Graph, SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
@@ -302,6 +302,17 @@ class BuckGNN(nn.Module):
                 x = x + identity
         return x
 
+    def _skip_dropout(self, x, e, x_prev, e_prev, skip: bool, fused: bool):
+        """EA_GNN's `if 0 < i < L-1: x, e = x + x_prev, e + e_prev` then Dropout on both
+        (Models/BuckGNN.py:382-387); one bgnn_add_dropout pass each on the fused path."""
+        if not fused:
+            if skip:
+                x, e = x + x_prev, e + e_prev
+            return self.dropout(x), self.dropout(e)
+        p = self.dropout.p
+        return (skip_dropout(x, x_prev if skip else None, p, self.training, self._seed()),
+                skip_dropout(e, e_prev if skip else None, p, self.training, self._seed()))
+
     def _ea_block(self, blk, x, e, edge_index, fused: bool):
         return graphnet_block(blk, x, e, edge_index, self.ea_bf16) if fused else blk(x, edge_index, e)
 
@@ -335,9 +346,7 @@ class BuckGNN(nn.Module):
                     x, e = graphnet_block(self.shared_gn_block, x, e, edge_index, self.ea_bf16)
                 else:
                     x, e = self.shared_gn_block(x, edge_index, e)
-                if 0 < i < self.num_layers - 1:
-                    x, e = x + x_prev, e + e_prev
-                x, e = self.dropout(x), self.dropout(e)
+                x, e = self._skip_dropout(x, e, x_prev, e_prev, 0 < i < self.num_layers - 1, ea_fused)
         if name == "GraphSage_addAggr_Shared":
             x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax, x_in)
         elif name == "EA_GNN":
@@ -350,9 +359,7 @@ class BuckGNN(nn.Module):
                     x, e = graphnet_block(blk, x, e, edge_index, self.ea_bf16)
                 else:
                     x, e = blk(x, edge_index, e)
-                if 0 < i < L - 1:
-                    x, e = x + x_prev, e + e_prev
-                x, e = self.dropout(x), self.dropout(e)
+                x, e = self._skip_dropout(x, e, x_prev, e_prev, 0 < i < L - 1, ea_fused)
         elif name in _SAGE_VARIANTS:
             attr, aggr, _ = _SAGE_VARIANTS[name]
             x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax, x_in)

@@ -151,6 +151,41 @@ class _ColumnBlocks(torch.autograd.Function):
 
 # the two-step form (linear, then _GatherAdd) is kept for A/B measurement
 FUSED_GATHER = True
+# EA_GNN's skip add + dropout over [E, H] / [N, H] as one pass (bgnn_add_dropout)
+FUSED_SKIP_DROPOUT = True
+
+
+def _add_dropout(a: torch.Tensor, b, p: float, seed: int) -> torch.Tensor:
+    out = torch.empty_like(a)
+    _lib.call("bgnn_add_dropout", a.data_ptr(), None if b is None else b.data_ptr(), a.numel(), float(p), seed,
+              out.data_ptr(), _stream())
+    return out
+
+
+class _SkipDropout(torch.autograd.Function):
+    """drop(a + b) with the counter-based mask (nothing stored); backward drop(g) to both."""
+
+    @staticmethod
+    def forward(ctx, a, b, p: float, seed: int):
+        ctx.p, ctx.seed, ctx.has_b = p, seed, b is not None
+        return _add_dropout(a, b, p, seed)
+
+    @staticmethod
+    def backward(ctx, g):
+        gd = _add_dropout(g.contiguous(), None, ctx.p, ctx.seed)
+        return gd, (gd if ctx.has_b else None), None, None
+
+
+def skip_dropout(a: torch.Tensor, b, p: float, training: bool, seed: int) -> torch.Tensor:
+    """Dropout_p(a + b) (b may be None) as one pass: Models/BuckGNN.py:382-387."""
+    if not training or p == 0.0:
+        return a + b if b is not None else a
+    ok = (FUSED_SKIP_DROPOUT and a.is_cuda and a.dtype == torch.float32 and a.is_contiguous()
+          and a.numel() % 4 == 0 and a.data_ptr() % 16 == 0
+          and (b is None or (b.is_contiguous() and b.shape == a.shape and b.data_ptr() % 16 == 0)))
+    if not ok:
+        return torch.nn.functional.dropout(a + b if b is not None else a, p, True)
+    return _SkipDropout.apply(a, b, p, seed)
 
 
 def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tensor, bf16: bool = False):

@@ -432,6 +432,15 @@ int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, int32_t D2, 
                   const float* b1, const float* W2, const float* h, const float* dh, float* dW1,
                   float* db1, float* dW2, float* db2, void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Skip + dropout of the EA_GNN layer loop (Models/BuckGNN.py:382-387): out = drop(a + b) over
+ * n floats (b optional: plain dropout; also the backward, drop(g)), with the counter-based
+ * mask of the fused SAGE layers (keep_bits4(seed, i / 4), kept values scaled by 1 / (1 - p)).
+ * n a multiple of 4, pointers 16-byte aligned; out may alias a.
+ * ---------------------------------------------------------------------- */
+int bgnn_add_dropout(const float* a, const float* b, int64_t n, float p, uint64_t seed, float* out,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

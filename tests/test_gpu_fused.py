@@ -214,3 +214,29 @@ def _check_mlp2(dev, N):
     for g, p in zip(grads, ref.parameters()):
         scale = p.grad.abs().max().item() + 1e-30
         assert (g.double().cpu() - p.grad).abs().max().item() <= 1e-5 * scale + 1e-6
+
+
+@pytest.mark.parametrize("p,with_b", [(0.1, True), (0.25, False), (0.0, True)])
+def test_ea_skip_dropout(dev, p, with_b):
+    """EA_GNN's skip + dropout in one pass (bgnn_add_dropout): kept elements are exactly
+    (a + b) / (1 - p), the keep fraction is 1 - p, and the backward sends the same mask of the
+    incoming gradient to both inputs; p = 0 is the plain add."""
+    from bgnn.ea import skip_dropout
+    torch.manual_seed(3)
+    a = torch.randn(20000, 512, device=dev, requires_grad=True)
+    b = torch.randn(20000, 512, device=dev, requires_grad=True) if with_b else None
+    out = skip_dropout(a, b, p, True, 123456789)
+    s = (a + b if with_b else a).detach()
+    keep = out.detach() != 0
+    if p == 0.0:
+        assert torch.equal(out.detach(), s)
+    else:
+        frac = 1 - keep.float().mean().item()
+        assert abs(frac - p) < 0.005, frac
+        torch.testing.assert_close(out.detach()[keep], s[keep] * (1.0 / (1.0 - p)), rtol=0, atol=0)
+    g = torch.randn_like(out)
+    out.backward(g)
+    want = torch.where(keep, g * (1.0 / (1.0 - p)) if p else g, torch.zeros_like(g))
+    torch.testing.assert_close(a.grad, want, rtol=0, atol=0)
+    if with_b:
+        assert torch.equal(b.grad, a.grad)
