@@ -227,13 +227,15 @@ def test_ea_skip_dropout(dev, p, with_b):
     b = torch.randn(20000, 512, device=dev, requires_grad=True) if with_b else None
     out = skip_dropout(a, b, p, True, 123456789)
     s = (a + b if with_b else a).detach()
-    keep = out.detach() != 0
+    # the mask itself, from the same seed on a tensor of ones (value-independent)
+    keep = skip_dropout(torch.ones_like(s), None, p, True, 123456789) != 0
     if p == 0.0:
         assert torch.equal(out.detach(), s)
     else:
         frac = 1 - keep.float().mean().item()
         assert abs(frac - p) < 0.005, frac
-        torch.testing.assert_close(out.detach()[keep], s[keep] * (1.0 / (1.0 - p)), rtol=0, atol=0)
+        torch.testing.assert_close(out.detach(), torch.where(keep, s * (1.0 / (1.0 - p)), torch.zeros_like(s)),
+                                   rtol=0, atol=0)
     g = torch.randn_like(out)
     out.backward(g)
     want = torch.where(keep, g * (1.0 / (1.0 - p)) if p else g, torch.zeros_like(g))

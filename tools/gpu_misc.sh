@@ -1,7 +1,6 @@
 #!/bin/bash
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_model.py tests/test_gpu_fold.py -q --timeout 120 --timeout-method thread > gpurun_out/rows_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_ea_train.py tests/test_gpu_model.py -q --timeout 120 --timeout-method thread > gpurun_out/ea_tests.log 2>&1
 rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-ROOT=$(pwd)
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_rows" -o run -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$ROOT/gpurun_out/prof_rows_bench.json" 2>&1
+timeout -k 10 300 python bench.py --model EA_GNN --bf16 --config cfg5 --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/bench_ea_cfg5_bf16_c.json 2> gpurun_out/bench_ea_c.err || exit $?
+timeout -k 10 300 python -c "import sys, runpy; sys.argv=['bench.py','--model','EA_GNN','--bf16','--config','cfg5','--steps','6','--warmup','2','--no-cpu-baseline']; sys.path.insert(0,'buck-gnn_amd'); import bgnn.ea as E; E.FUSED_SKIP_DROPOUT=False; runpy.run_path('bench.py', run_name='__main__')" > gpurun_out/bench_ea_cfg5_bf16_noskipdrop.json 2>> gpurun_out/bench_ea_c.err
