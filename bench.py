@@ -26,7 +26,7 @@ MFMA peak 157.3 TF is reported beside it).
 bias + L2 normalize + BN statistics), 499.1 MB per launch against 8 TB/s. Both use HIP
 events recorded on the launching stream around each launch inside the timed region;
 `traffic` is the per-launch fabric traffic from rocprofv3 PMC passes
-(profiles/traffic_r02j.json, tools/traffic.py).
+(profiles/traffic_r02l.json, tools/traffic.py).
 """
 from __future__ import annotations
 
@@ -45,7 +45,7 @@ FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.m
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md)
 X6_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6   # f32-equivalent ceiling of the 6-product bf16 split GEMM
 H3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 3   # f32-equivalent ceiling of the 3-product f16 split GEMM (f16 = bf16 rate)
-TRAFFIC_FILE = "traffic_r02j.json"   # rocprofv3 PMC passes of this bench (tools/gpu_round.sh)
+TRAFFIC_FILE = "traffic_r02l.json"   # rocprofv3 PMC passes of this bench (tools/gpu_round.sh)
 METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"   # BASELINE.json
 
 
