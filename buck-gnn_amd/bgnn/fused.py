@@ -211,10 +211,13 @@ class LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device),
                               x_amax if x_amax is not None else torch.empty(0, device=x.device), w_amax)
         ctx.mark_non_differentiable(y_amax)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for y_amax
         return y, y_amax
 
     @staticmethod
     def backward(ctx, g, _g_amax):
+        if g is None:
+            return None, None, None, None, None, None, None
         x, weight, y, x_amax, w_amax = ctx.saved_tensors
         bf16 = ctx.bf16
         g, db, g_amax = relu_bias_grad(g, y if ctx.relu else None, ctx.has_bias)
@@ -261,10 +264,13 @@ class _Mlp2Fn(torch.autograd.Function):
                   b2.data_ptr(), h.data_ptr(), amax.data_ptr(), _stream())
         ctx.save_for_backward(x, W1, b1, W2, h)
         ctx.mark_non_differentiable(amax)
+        ctx.set_materialize_grads(False)
         return h, amax
 
     @staticmethod
     def backward(ctx, dh, _g_amax):
+        if dh is None:
+            return None, None, None, None, None
         x, W1, b1, W2, h = ctx.saved_tensors
         dh = dh.contiguous()
         N, F = x.shape
@@ -427,6 +433,7 @@ class SageLayerFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.folded = folded
         ctx.wcat_t = wcat_t_pre
+        ctx.set_materialize_grads(False)   # the amax output never gets a gradient: no zero fill for it
         ctx.fold = (w_in, b_in, wf) if folded else None
         ctx.save_for_backward(x_prev, o, nrm, wcat, gamma if gamma is not None else torch.empty(0, device=dev),
                               scale if scale is not None else torch.empty(0, device=dev),
@@ -439,6 +446,8 @@ class SageLayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _g_amax):
+        if g is None:   # (materialize_grads off: the layer output did not reach the loss)
+            return (None,) * 15
         x_prev, o, nrm, wcat, gamma, scale, shift, mean, invstd, x_amax, w_amax, dz_amax = ctx.saved_tensors
         cfg: LayerConfig = ctx.cfg
         graph: Graph = ctx.graph
