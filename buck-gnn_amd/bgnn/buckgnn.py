@@ -24,7 +24,7 @@ from torch import Tensor, nn
 
 from .ea import graphnet_block, skip_dropout
 from .fused import mlp, prepare_weights, sage_layer
-from .graph import Graph, SegmentIndex, graph_for, _index_cache
+from .graph import SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
 
