@@ -17,16 +17,19 @@ instead; --data host collates on the host (PCIe-inclusive).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
-Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel, the forward GEMM
-z = x [W_l;W_r]^T (18 GEMMs of this size make up about half of the step), MFMA-bound: 84.6 GFLOP
-per launch; its peak is the ceiling of the algorithm that runs (default f16x3: f16 dense MFMA
-2.5 PF / 3 piece products = 833.3 TF f32-equivalent; bf16x6: 2.5 PF / 6 = 416.7 TF; the f32
-MFMA peak 157.3 TF is reported beside it).
+Rank 0 prints ONE JSON line. `roofline` is the dominant kernel: the SAGE-layer GEMM family
+(forward z = x [W_l;W_r]^T, dgrad or wgrad; 18 GEMMs of 84.6 GFLOP each per step) with the
+largest time per step, MFMA-bound. Each family is timed under its own key (bgnn/fused.py) so
+every averaged launch has the same flops; the folded first layer's K = 128 launches are timed
+separately. `roofline_gemm` lists all six shapes and the step total. The GEMM peak is the
+ceiling of the algorithm that runs (default f16x3: f16 dense MFMA 2.5 PF / 3 piece products =
+833.3 TF f32-equivalent; bf16x6: 2.5 PF / 6 = 416.7 TF; the f32 MFMA peak 157.3 TF is reported
+beside it); tools/gemm_launches.py recomputes the same figures from a rocprofv3 kernel trace.
 `roofline_hbm` is the fused aggregation kernel (bgnn_sage_fwd: neighbour sum + lin_r term +
-bias + L2 normalize + BN statistics), 499.1 MB per launch against 8 TB/s. Both use HIP
-events recorded on the launching stream around each launch inside the timed region;
-`traffic` is the per-launch fabric traffic from rocprofv3 PMC passes
-(profiles/traffic_r02l.json, tools/traffic.py).
+bias + L2 normalize + BN statistics), 499.1 MB per launch against 8 TB/s; `roofline_agg_bwd`
+the transpose aggregation (333.6 MB). All use HIP events recorded on the launching
+stream around each launch inside the timed region; `traffic` is the per-launch fabric traffic
+from rocprofv3 PMC passes (profiles/TRAFFIC_FILE, tools/traffic.py).
 """
 from __future__ import annotations
 
@@ -67,6 +70,11 @@ def parse():
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg5"])
     ap.add_argument("--model", default="GraphSage_addAggr")
     ap.add_argument("--gemm", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--path", default="fused", choices=["fused", "per_op"],
+                    help="fused (default): bgnn.BuckGNN's fused SAGE layer loop; per_op: the same model with "
+                         "use_fused=False, i.e. the module graph the PyG shim gives the reference's unchanged "
+                         "Models/BuckGNN.py (bgnn.nn.SAGEConv modules on the hand-written GEMM + fused "
+                         "aggregation/normalize, torch BatchNorm/ReLU/Dropout and encoder)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
@@ -142,6 +150,7 @@ def main():
                          model_name=args.model)
     state0 = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
+    model.use_fused = args.path == "fused"
     model.ea_bf16 = bool(args.bf16)
     is_ea = args.model.startswith("EA_GNN")
     lr = args.lr if args.lr is not None else (1e-3 if is_ea else 1e-2)
@@ -198,6 +207,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timers, fused.TIMERS = fused.TIMERS, None
+    if args.path == "per_op":   # the per-module SAGEConv launches (bgnn.fused.SageConvFn) under the same keys
+        timers = {k[5:]: v for k, v in timers.items() if k.startswith("conv_")}
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -227,16 +238,51 @@ def main():
             traffic = {k: v["bytes_per_launch"] for k, v in json.load(open(tpath))["kernels"].items()}
         except (ValueError, OSError, KeyError):
             traffic = {}
-    gemm_ms = avg_ms("gemm_fwd")
-    gemm_flop = 2.0 * N * (2 * H) * H
     gmode = _lib.query("bgnn_get_tuning", 5) if args.gemm == "hip" else -1
     gemm_peak = {1: X6_PEAK_TFS, 2: H3_PEAK_TFS}.get(gmode, FP32_MFMA_PEAK_TFS)
-    gemm_kernel = {2: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<1,0,1,256,256,4,2> (f32-accurate f16x3)",
-                   1: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_x6<0,0,1,256,128,4,2> (f32-accurate bf16x6)",
-                   0: "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T: k_gemm_f32 (f32 MFMA)"}.get(gmode, "torch.mm")
     gemm_basis = {2: "f16 dense MFMA 2500 TF / 3 f16 products per f32 product",
                   1: "bf16 dense MFMA 2500 TF / 6 bf16 products per f32 product"}.get(gmode, "f32 dense MFMA")
-    gemm_tfs = gemm_flop / (gemm_ms * 1e-3) / 1e12
+    # The SAGE layer GEMMs, one timer per shape (bgnn/fused.py): every launch averaged under a key
+    # has the same flops. K=512 layers: fwd z = x [W_l;W_r]^T, dgrad dx = [dz_l|dh] [W_l;W_r],
+    # wgrad d[W_l;W_r] = [dz_l|dh]^T x (each 2*N*2H*H flops); the folded first layer runs the
+    # same three products with the encoder width K_in = 128 in place of one H.
+    K_in = 128
+    fams = {
+        "gemm_fwd": (2.0 * N * (2 * H) * H, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", "gemm_fwd_h3",
+                     "fwd z = x [W_l;W_r]^T, K = 512 layers (5 per step)"),
+        "gemm_dgrad": (2.0 * N * H * (2 * H), "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8> (skip layers, drop-add "
+                       "epilogue) + k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0> (last layer)", "gemm_dgrad",
+                       "dgrad dx = [dz_l|dh] [W_l;W_r], K = 512 layers (5 per step)"),
+        "gemm_wgrad": (2.0 * (2 * H) * H * N, "k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0> + split-K slab reduce",
+                       "gemm_wgrad", "wgrad [dz_l|dh]^T x, K = 512 layers (5 per step)"),
+        "gemm_fwd_fold": (2.0 * N * (2 * H) * K_in, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", None,
+                          "folded layer 0 fwd z = h Wf^T, K = 128"),
+        "gemm_dgrad_fold": (2.0 * N * K_in * (2 * H), "k_gemm_x6<1, 0, 1, 256, 128, 4, 2, 0>", None,
+                            "folded layer 0 dgrad dh = dz Wf"),
+        "gemm_wgrad_fold": (2.0 * (2 * H) * K_in * N, "k_gemm_x6<1, 1, 0, 256, 128, 4, 2, 0>", None,
+                            "folded layer 0 wgrad dWf = dz^T h"),
+    }
+
+    def gemm_block(key):
+        flop, kname, tkey, what = fams[key]
+        ms = avg_ms(key)
+        n = len(timers.get(key, []))
+        tfs = flop / (ms * 1e-3) / 1e12 if n else float("nan")
+        return {"kernel": f"bgnn_gemm_f32 {what}: {kname}" + (" (f32-accurate f16x3)" if gmode == 2 else ""),
+                "bound": "mfma", "achieved": round(tfs, 2), "peak": gemm_peak, "unit": "TFLOP/s",
+                "frac": round(tfs / gemm_peak, 4), "traffic": traffic.get(tkey) if tkey else None,
+                "peak_basis": gemm_basis, "f32_mfma_peak": FP32_MFMA_PEAK_TFS, "algorithmic_flop": flop,
+                "avg_launch_ms": round(ms, 5), "launches": n,
+                "ms_per_step": round(ms * n / args.steps, 4) if n else float("nan")}
+
+    gemm_blocks = {k: gemm_block(k) for k in fams}
+    # all SAGE-layer GEMM launches of the step together: summed flops / summed event time
+    tot_flop = sum(fams[k][0] * gemm_blocks[k]["launches"] for k in fams)
+    tot_ms = sum(avg_ms(k) * gemm_blocks[k]["launches"] for k in fams if gemm_blocks[k]["launches"])
+    gemm_all_tfs = tot_flop / (tot_ms * 1e-3) / 1e12 if tot_ms else float("nan")
+    # `roofline` = the dominant kernel: the GEMM family with the largest time per step
+    main_key = max(("gemm_fwd", "gemm_dgrad", "gemm_wgrad"),
+                   key=lambda k: (gemm_blocks[k]["launches"] * avg_ms(k)) if gemm_blocks[k]["launches"] else -1)
     graphs = bsz * world * args.steps
     out = {
         "metric": metric_name(args.model, bsz),
@@ -255,6 +301,8 @@ def main():
             "workload": f"{args.config}: {bsz} synthetic 71x71 quad+diagonal FE meshes per GPU"
                         + (" + super node" if args.config == "cfg3" else " + 13.33% random virtual edges")
                         + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam"
+                        + ("; per-op modules (PyG-surface SAGEConv on the bgnn GEMM + fused aggregation/normalize, "
+                           "torch BatchNorm/ReLU/Dropout/encoder)" if args.path == "per_op" else "")
                         + (", bf16 GEMM operands" if args.bf16 and args.model.startswith("EA_GNN") else "") + "; "
                         + {"static": "CSR rebuilt every step" if not args.cache_graph else "CSR cached across steps",
                            "store": f"new shuffled batch every step gathered on the GPU from a resident "
@@ -269,20 +317,15 @@ def main():
             "layers": 6,
             "parallelism": f"dp{world}",
             "gemm": args.gemm,
+            "path": args.path,
         },
-        "roofline": {
-            "kernel": gemm_kernel,
-            "bound": "mfma",
-            "achieved": round(gemm_tfs, 2),
-            "peak": gemm_peak,
-            "unit": "TFLOP/s",
-            "frac": round(gemm_tfs / gemm_peak, 4),
-            "traffic": traffic.get({2: "gemm_fwd_h3", 1: "gemm_fwd"}.get(gmode, ""), None),
-            "peak_basis": gemm_basis,
-            "f32_mfma_peak": FP32_MFMA_PEAK_TFS,
-            "algorithmic_flop": gemm_flop,
-            "avg_launch_ms": round(gemm_ms, 5),
-            "launches": len(timers.get("gemm_fwd", [])),
+        "roofline": dict(gemm_blocks[main_key], family=main_key),
+        "roofline_gemm": {
+            **{k: {kk: gemm_blocks[k][kk] for kk in ("achieved", "frac", "avg_launch_ms", "launches", "ms_per_step",
+                                                     "algorithmic_flop", "kernel")} for k in fams},
+            "all_sage_gemms": {"achieved": round(gemm_all_tfs, 2), "frac": round(gemm_all_tfs / gemm_peak, 4),
+                               "ms_per_step": round(tot_ms / args.steps, 4),
+                               "tflop_per_step": round(tot_flop / args.steps / 1e12, 4)},
         },
         "roofline_hbm": {
             "kernel": "bgnn_sage_fwd: " + agg_name.format(e=1)
@@ -315,7 +358,7 @@ def main():
     if is_ea:
         # the SAGE kernels above never run for EA_GNN: no roofline blocks for them
         out["roofline"] = None
-        for k in ("roofline_hbm", "roofline_agg_bwd"):
+        for k in ("roofline_hbm", "roofline_agg_bwd", "roofline_gemm"):
             out.pop(k)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(batch_cpu, state0, args.model, args.cpu_steps)

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lock = threading.Lock()
 _lib = None
@@ -83,6 +83,7 @@ SIGNATURES = {
     "bgnn_linear_bwd_prep": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
                                    c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p]),
+    "bgnn_l2norm_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
     "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
     "bgnn_gemm_f32_planes": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,

@@ -325,7 +325,9 @@ class BuckGNN(nn.Module):
         x_amax = None   # max|x| after the encoder (f16x3 operand scale of the first SAGE GEMM)
         x_in = None     # the encoder's last Linear when it is folded into the first SAGE layer
         sage = _SAGE_VARIANTS.get(name, (None, "add", None))[1] if name != "GraphSage_addAggr_Shared" else "add"
-        if (name in _SAGE_VARIANTS or name in ("GraphSage_addAggr_Shared", "GraphSAGE_SAG")) \
+        # (GraphSAGE_SAG folds into sage_layers_1[0]: not when that list is empty, num_layers == 1)
+        if (name in _SAGE_VARIANTS or name == "GraphSage_addAggr_Shared"
+                or (name == "GraphSAGE_SAG" and len(self.sage_layers_1) >= 1)) \
                 and self._sage_fused(x, sage) and self._foldable_encoder(x):
             x_in = self.node_encoder[-1]
             x, x_amax = mlp(self.node_encoder[:-1], x, return_amax=True)

@@ -392,7 +392,9 @@ class SageLayerFn(torch.autograd.Function):
         if x_amax is None:
             x_amax = absmax(x_prev)
         planes = Z_PLANES and H % PLANE_TILE == 0 and not folded
-        with _timed("gemm_fwd"):
+        # (the folded layer's transform has K = K_in, not H: timed under its own name so the
+        # bench's flops per launch are right for every launch it averages)
+        with _timed("gemm_fwd_fold" if folded else "gemm_fwd"):
             if planes:   # z = [z_l ; z_r] as two dense [N, H] planes
                 z = torch.empty(2, N, H, dtype=torch.float32, device=dev)
                 gemm(x_prev, wmat, trans_a=False, trans_b=True, out=Planes(z), a_amax=x_amax, b_amax=w_amax)
@@ -509,8 +511,10 @@ class SageLayerFn(torch.autograd.Function):
             # then dWcat = dWf W_in^T + dbf b_in^T (= dz^T x), dW_in = Wcat^T dWf, db_in = Wcat^T dbf
             w_in, b_in, wf = ctx.fold
             wf_t = wf.t().contiguous() if DGRAD_WT else wf
-            dx = gemm(dz, wf_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
-            dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, K_in]
+            with _timed("gemm_dgrad_fold"):
+                dx = gemm(dz, wf_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
+            with _timed("gemm_wgrad_fold"):
+                dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, K_in]
             dbf = torch.cat([db_zl, db])                                                    # Σ dz_l ; Σ dh
             if FOLD_WEIGHTS_TORCH:
                 dw = torch.addmm(torch.outer(dbf, b_in), dwf, w_in.t())                    # [2H, H]
@@ -531,15 +535,19 @@ class SageLayerFn(torch.autograd.Function):
             M_, K_ = N, 2 * H
             ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M_, H, K_, 0, 1, 0)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
-            _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M_, H, K_, dz.data_ptr(), lddz, wcat_t.data_ptr(),
-                      wcat_t.stride(0), dx.data_ptr(), H, dz_amax.data_ptr(), w_amax.data_ptr(), g.data_ptr(), H,
-                      float(cfg.p), cfg.seed, _ptr(ws), ws_bytes, s)
+            with _timed("gemm_dgrad"):
+                _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M_, H, K_, dz.data_ptr(), lddz, wcat_t.data_ptr(),
+                          wcat_t.stride(0), dx.data_ptr(), H, dz_amax.data_ptr(), w_amax.data_ptr(), g.data_ptr(),
+                          H, float(cfg.p), cfg.seed, _ptr(ws), ws_bytes, s)
         elif gskip is not None:
-            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, out=gskip, beta=1.0, a_amax=dz_amax,
-                      b_amax=w_amax)
+            with _timed("gemm_dgrad"):
+                dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, out=gskip, beta=1.0, a_amax=dz_amax,
+                          b_amax=w_amax)
         else:
-            dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
-        dw = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)      # [2H, H]
+            with _timed("gemm_dgrad"):
+                dx = gemm(dz, wcat_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
+        with _timed("gemm_wgrad"):
+            dw = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)  # [2H, H]
         dw_l, dw_r = dw[:H], dw[H:]
         return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
                 None, None, None, None, None, None, None, None)
@@ -584,9 +592,11 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
     if bn_module is not None:
         use_batch_stats = training or not bn_module.track_running_stats
         momentum = bn_module.momentum
-        if training and bn_module.track_running_stats and count_batch:
-            bn_module.num_batches_tracked.add_(1)
-            if momentum is None:
+        if training and bn_module.track_running_stats:
+            if count_batch:
+                bn_module.num_batches_tracked.add_(1)
+            if momentum is None:   # cumulative average (torch: 1 / num_batches_tracked after the increment;
+                # with count_batch=False the caller has already incremented the counter)
                 momentum = 1.0 / float(bn_module.num_batches_tracked.item())
         cfg = LayerConfig(reduce, True, use_batch_stats, float(momentum or 0.0) if bn_module.track_running_stats
                           else 0.0, float(bn_module.eps), skip, p, seed)
@@ -599,3 +609,88 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
                                 w_in, b_in, wprep)
     return out if return_amax else out[0]
+
+
+class SageConvFn(torch.autograd.Function):
+    """One SAGEConv(normalize=True, aggr in {add, sum, mean}) module on the hand-written path:
+    the per-module form of SageLayerFn without the layer glue, for the PyG call surface
+    (bgnn.nn.SAGEConv, i.e. the reference's unchanged Models/BuckGNN.py:434 under the shim,
+    whose BatchNorm / ReLU / skip / Dropout stay torch modules).
+
+        z = x [W_l;W_r]^T                 f16x3 MFMA GEMM (bgnn_gemm_f32_scaled)
+        o = normalize(AGG z_l + z_r + b)  bgnn_sage_fwd (aggregation + bias + L2 normalize)
+
+    backward: bgnn_l2norm_bwd (dh, bias-gradient partials, max|dh|), the transpose aggregation
+    dz_l = A^T dh (bgnn_spmm_bwd) and the dgrad / wgrad GEMMs on [dz_l | dh]."""
+
+    @staticmethod
+    def forward(ctx, x, w_l, b_l, w_r, graph: Graph, reduce: int):
+        dev = x.device
+        x = x.contiguous()
+        N = x.size(0)
+        H = w_l.size(0)
+        wcat = torch.cat([w_l, w_r], 0).contiguous()            # [2H, C_in]
+        amax = torch.zeros(3, dtype=torch.float32, device=dev)   # max|W|, max|x|, max|dz|
+        w_amax, x_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
+        absmax(wcat, w_amax, accumulate=True)
+        absmax(x, x_amax, accumulate=True)
+        with _timed("conv_gemm_fwd"):
+            z = gemm(x, wcat, trans_a=False, trans_b=True, a_amax=x_amax, b_amax=w_amax)   # [N, 2H]
+        bias = b_l if b_l is not None else torch.zeros(H, dtype=torch.float32, device=dev)
+        o = torch.empty(N, H, dtype=torch.float32, device=dev)
+        nrm = torch.empty(N, dtype=torch.float32, device=dev)
+        slots = _lib.query("bgnn_sage_fwd_slots", graph.fwd.ref())
+        bn_part = torch.empty(slots, 2, H, dtype=torch.float32, device=dev)   # (BN sums: unused here)
+        part = (torch.empty(graph.fwd.plan.n_chunks * H, dtype=torch.float32, device=dev)
+                if graph.fwd.plan.n_chunks else None)
+        with _timed("conv_sage_fwd"):
+            _lib.call("bgnn_sage_fwd", graph.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H,
+                      bias.data_ptr(), H, reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part),
+                      _stream())
+        ctx.graph = graph
+        ctx.reduce = reduce
+        ctx.has_bias = b_l is not None
+        ctx.save_for_backward(x, o, nrm, wcat, x_amax, w_amax, dz_amax)
+        return o
+
+    @staticmethod
+    def backward(ctx, g):
+        x, o, nrm, wcat, x_amax, w_amax, dz_amax = ctx.saved_tensors
+        graph: Graph = ctx.graph
+        g = g.contiguous()
+        N, H = o.shape
+        dev = o.device
+        s = _stream()
+        dz = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)   # [dz_l | dh]
+        dh = dz[:, H:]
+        rs = _lib.query("bgnn_rows_slots", N)
+        part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
+        dz_amax.zero_()
+        _lib.call("bgnn_l2norm_bwd", g.data_ptr(), o.data_ptr(), nrm.data_ptr(), N, H, dh.data_ptr(), 2 * H,
+                  part_db.data_ptr(), dz_amax.data_ptr(), s)
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = torch.empty(H, dtype=torch.float32, device=dev)
+            _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
+        bw = graph.bwd
+        part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
+        with _timed("conv_spmm_bwd"):
+            _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
+                      dh.data_ptr(), 2 * H, H, ctx.reduce, None, dz.data_ptr(), 2 * H, _ptr(part),
+                      dz_amax.data_ptr(), s)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            with _timed("conv_gemm_dgrad"):
+                dx = gemm(dz, wcat.t().contiguous(), trans_a=False, trans_b=True, a_amax=dz_amax, b_amax=w_amax)
+        dw = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+            with _timed("conv_gemm_wgrad"):
+                dw = gemm(dz, x, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, C_in]
+        return (dx, None if dw is None else dw[:H], db, None if dw is None else dw[H:], None, None)
+
+
+def sage_conv(x: torch.Tensor, w_l: torch.Tensor, b_l, w_r: torch.Tensor, graph: Graph, reduce: int):
+    """normalize(lin_l(AGG x) + lin_r(x)) of one SAGEConv module on the hand-written path
+    (SageConvFn); reduce 0 = sum/add, 1 = mean."""
+    require_cuda(x, w_l, w_r, what="sage_conv")
+    return SageConvFn.apply(x, w_l, b_l, w_r, graph, reduce)

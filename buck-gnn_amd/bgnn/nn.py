@@ -27,6 +27,11 @@ from torch import Tensor, nn
 from .graph import graph_for, segments_for
 from .ops import REDUCE, aggregate, segment_reduce
 
+# SAGEConv(normalize=True, aggr in {add, sum, mean}) modules run on the hand-written path
+# (bgnn.fused.SageConvFn: MFMA transform + fused aggregation/bias/normalize) when the input is
+# on the GPU; False = aggregate-first through torch Linear + F.normalize (A/B and tests)
+FAST_SAGECONV = True
+
 
 class Linear(nn.Linear):
     """torch.nn.Linear with PyG's initialisation (kaiming_uniform(a=sqrt(5)) weight,
@@ -83,6 +88,12 @@ class SAGEConv(nn.Module):
         if self.project:
             x_src = F.relu(self.lin(x_src))
         graph = graph_for(edge_index, x_src.size(0))
+        if self._fast(x_src, x_dst):
+            # the hand-written path: f16x3 MFMA transform [W_l;W_r] + fused aggregation, bias and
+            # L2 normalize, with its own backward (bgnn.fused.SageConvFn)
+            from .fused import sage_conv
+            return sage_conv(x_src, self.lin_l.weight, self.lin_l.bias, self.lin_r.weight, graph,
+                             1 if self.aggr == "mean" else 0)
         if self.aggr in ("add", "sum", "mean") and 2 * self.out_channels <= self.in_channels[0]:
             # narrow output (e.g. SAGPooling's 1-channel scorer): transform first, then aggregate
             # the narrow rows -- lin_l(AGG x) = AGG(x W_l^T) + b_l, since sum / mean are linear
@@ -96,6 +107,18 @@ class SAGEConv(nn.Module):
         if self.normalize:
             out = F.normalize(out, p=2.0, dim=-1)
         return out
+
+    def _fast(self, x_src: Tensor, x_dst: Tensor) -> bool:
+        """Whether this call runs on bgnn.fused.SageConvFn: normalize=True, sum/mean
+        aggregation, root weight, no projection, fp32 CUDA input, out_channels a multiple of
+        4 up to 512 and not narrower than half the input (the narrow scorer of SAGPooling
+        aggregates its 1-wide transform instead)."""
+        return (FAST_SAGECONV and self.normalize and self.root_weight and not self.project
+                and self.aggr in ("add", "sum", "mean") and x_src is x_dst and x_src.is_cuda
+                and x_src.dtype == torch.float32 and x_src.dim() == 2
+                and self.out_channels % 4 == 0 and 4 <= self.out_channels <= 512
+                and 2 * self.out_channels > self.in_channels[0] and self.in_channels[0] % 4 == 0
+                and self.lin_l.weight.dtype == torch.float32)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels[0]}, {self.out_channels}, aggr={self.aggr})"
@@ -218,7 +241,7 @@ class SAGPooling(nn.Module):
                 batch: Optional[Tensor] = None, attn: Optional[Tensor] = None):
         from .pool import sag_pool
         if batch is None:
-            batch = edge_index.new_zeros(x.size(0))
+            batch = torch.zeros(x.size(0), dtype=torch.long, device=x.device)
         attn = x if attn is None else attn
         attn = attn.view(-1, 1) if attn.dim() == 1 else attn
         attn = self.gnn(attn, edge_index)

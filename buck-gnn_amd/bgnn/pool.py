@@ -48,7 +48,8 @@ def topk_select(score: torch.Tensor, ratio: float, batch: torch.Tensor):
     score = score.detach().reshape(-1).contiguous()
     if score.dtype != torch.float32:
         raise TypeError("topk_select: score must be float32")
-    batch = batch.contiguous()
+    # the kernels read `batch` as int64 (an int32 edge_index gives an int32 batch upstream)
+    batch = batch.to(torch.long).contiguous()
     N = score.numel()
     dev = score.device
     if batch.numel() != N:
@@ -110,6 +111,10 @@ def gather_scale(x: torch.Tensor, score: torch.Tensor, perm: torch.Tensor, new_i
     score = score.reshape(-1).contiguous()
     if score.numel() != x.size(0) or new_id.numel() != x.size(0):
         raise ValueError("gather_scale: score / new_id must have one entry per row of x")
+    if new_id.dtype != torch.int32 or perm.dtype != torch.long:
+        raise TypeError("gather_scale: new_id must be int32 and perm int64 (topk_select's outputs)")
+    if score.dtype != torch.float32:
+        raise TypeError("gather_scale: score must be float32")
     return _GatherScale.apply(x, score, perm.contiguous(), new_id.contiguous())
 
 
@@ -119,6 +124,9 @@ def filter_edges(edge_index: torch.Tensor, new_id: torch.Tensor, num_nodes: int)
     require_cuda(edge_index, new_id, what="filter_edges")
     if edge_index.dim() != 2 or edge_index.size(0) != 2:
         raise ValueError(f"filter_edges: edge_index must be [2, E], got {tuple(edge_index.shape)}")
+    if new_id.dtype != torch.int32 or new_id.numel() != int(num_nodes):
+        raise TypeError("filter_edges: new_id must be an int32 vector with one entry per node")
+    new_id = new_id.contiguous()
     ei = edge_index.to(torch.long).contiguous()
     E = ei.size(1)
     dev = ei.device

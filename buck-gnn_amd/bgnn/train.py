@@ -86,6 +86,8 @@ class GradAllReduce:
         self._ready = []
         self._next = 0
         self._works = []
+        self._extra = []
+        self.layout = None         # bucket layout (parameter indices), identical on every rank
         self._hooks = []
         if self.overlap:
             for p in model.parameters():
@@ -98,8 +100,9 @@ class GradAllReduce:
             self._seen.append(p)
             return
         b = self._bucket_of.get(id(p))
-        if b is None:
-            raise RuntimeError("GradAllReduce: a parameter without a gradient in the first step got one")
+        if b is None:   # reported by __call__ once this step's collectives are issued
+            self._extra.append(p)
+            return
         self._ready[b] += 1
         while self._next < len(self._buckets) and self._ready[self._next] == len(self._buckets[self._next][0]):
             params, flat, views = self._buckets[self._next]
@@ -108,14 +111,37 @@ class GradAllReduce:
             self._next += 1
 
     def _build_buckets(self) -> None:
+        """Bucket layout from the recording step's gradient arrival order. The layout must be the
+        same on every rank (a hook-launched all-reduce of bucket b sums bucket b of every rank),
+        but arrival order is data-dependent (the fold / encoder paths switch on the batch size),
+        so rank 0's order is broadcast and used everywhere (DDP's rebuilt-buckets approach);
+        every rank checks that it has gradients for exactly the same parameters and all ranks
+        raise together if any differs."""
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        index = {id(p): i for i, p in enumerate(params)}
         order, seen = [], set()
         for p in self._seen:
             if id(p) not in seen and p.grad is not None:
                 seen.add(id(p))
-                order.append(p)
+                order.append(index[id(p)])
         self._seen = []
+        if self.world > 1:
+            dev = params[0].device if params else torch.device("cpu")
+            n = torch.tensor([len(order)], dtype=torch.long, device=dev)
+            dist.broadcast(n, 0, group=self.group)
+            ref = torch.tensor(order if dist.get_rank(self.group) == 0 else [0] * int(n.item()),
+                               dtype=torch.long, device=dev)
+            dist.broadcast(ref, 0, group=self.group)
+            ref = ref.tolist()
+            ok = torch.tensor([int(sorted(ref) == sorted(order))], dtype=torch.long, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
+            if not int(ok.item()):
+                raise RuntimeError("GradAllReduce: the ranks produced gradients for different parameter sets "
+                                   "in the recording step; the bucket layout cannot be shared")
+            order = ref
         buckets, cur, nbytes = [], [], 0
-        for p in order:
+        for i in order:
+            p = params[i]
             cur.append(p)
             nbytes += p.numel() * p.element_size()
             if nbytes >= self.bucket_bytes:
@@ -124,32 +150,56 @@ class GradAllReduce:
         if cur:
             buckets.append(cur)
         self._buckets = []
-        for b, params in enumerate(buckets):
-            flat = torch.empty(sum(p.numel() for p in params), dtype=params[0].dtype, device=params[0].device)
+        self.layout = [[index[id(p)] for p in b] for b in buckets]   # parameter indices per bucket
+        for b, bparams in enumerate(buckets):
+            flat = torch.empty(sum(p.numel() for p in bparams), dtype=bparams[0].dtype, device=bparams[0].device)
             views, off = [], 0
-            for p in params:
+            for p in bparams:
                 views.append(flat[off:off + p.numel()].view_as(p))
                 self._bucket_of[id(p)] = b
                 off += p.numel()
-            self._buckets.append((params, flat, views))
+            self._buckets.append((bparams, flat, views))
         self._ready = [0] * len(self._buckets)
+
+    def _launch_rest(self) -> None:
+        """Launch the buckets whose gradients did not all arrive this step, with zeros for the
+        missing ones (DDP's semantics for a parameter unused on one rank), so every rank still
+        issues the same collective sequence."""
+        while self._next < len(self._buckets):
+            params, flat, views = self._buckets[self._next]
+            for p, v in zip(params, views):
+                if p.grad is None:
+                    v.zero_()
+                else:
+                    v.copy_(p.grad)
+            self._works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self._next += 1
 
     # ---------------------------------------------------------------- per step
     def __call__(self) -> None:
         if self.world <= 1:
             return
         if self.overlap and self._buckets is not None:
-            if self._next != len(self._buckets):
-                raise RuntimeError("GradAllReduce: not every bucket received all its gradients this step")
+            self._launch_rest()
             for w in self._works:
                 w.wait()
             inv = 1.0 / self.world
             for params, flat, views in self._buckets:
                 flat.mul_(inv)
+                for p in params:
+                    if p.grad is None:   # (unused on this rank this step: takes the others' average)
+                        p.grad = torch.zeros_like(p)
                 torch._foreach_copy_([p.grad for p in params], views)
+            extra = self._extra
+            self._extra = []
             self._works, self._next = [], 0
             self._ready = [0] * len(self._buckets)
+            if extra:   # (after this step's collectives, so the other ranks are not left blocked)
+                raise RuntimeError(f"GradAllReduce: {len(extra)} parameter(s) without a gradient in the "
+                                   "recording step got one; they are in no bucket")
             return
+        if self.overlap:   # layout (and the parameter-set check) before the first gradient collective
+            self._build_buckets()
         grads = [p.grad for p in self.model.parameters() if p.grad is not None]
         if grads:
             total = sum(g.numel() for g in grads)
@@ -166,7 +216,6 @@ class GradAllReduce:
             self._flat.mul_(1.0 / self.world)
             torch._foreach_copy_(grads, views)
         if self.overlap:
-            self._build_buckets()
             self._flat = None
 
 

@@ -244,8 +244,10 @@ __global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict_
     }
 }
 
-// Backward pass 2: one wave per row (H <= 512, NV float4 per lane).
-template <int NV>
+// Backward pass 2: one wave per row (H <= 512, NV float4 per lane). RELU = false: the layer
+// is the bare SAGEConv(normalize=True) of the per-op path (g is dL/do; no ReLU mask, no BN,
+// no dropout), i.e. only the L2-normalize backward.
+template <int NV, bool RELU = true>
 __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ o, const float* __restrict__ nrm,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ gamma,
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
                 const float g1 = ((m >> k) & 1u) ? gg[k] * (thr ? inv_keep : 1.f) : 0.f;
                 g1v[v][k] = g1;
                 const float yp = ov[v][k] * scv[v][k] + shv[v][k];
-                const float g2 = yp > 0.f ? g1 : 0.f;
+                const float g2 = (!RELU || yp > 0.f) ? g1 : 0.f;
                 float d;
                 if (bn) {
                     const float xh = (ov[v][k] - muv[v][k]) * isv[v][k];
@@ -566,6 +568,33 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
         hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
                            lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+// The L2-normalize backward of SAGEConv(normalize=True) on its own (bgnn.nn.SAGEConv's fused
+// per-module path, Models/BuckGNN.py:434 under the PyG shim): dh = (g - o <o, g>) / ||h|| per
+// row (rows with ||h|| < 1e-12 get g * 1e12: F.normalize's clamped denominator), written at dh (row stride lddh), per-block column sums of dh into partial_db (the bias
+// gradient, bgnn_reduce_partials layout) and max |dh| folded into *amax.
+extern "C" int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm, int64_t n_rows, int32_t H,
+                               float* dh, int64_t lddh, float* partial_db, float* amax, void* stream) {
+    BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 512, "l2norm_bwd: H=%d unsupported", H);
+    BGNN_REQUIRE(g && o && nrm && dh && partial_db && amax, "l2norm_bwd: null pointer");
+    BGNN_REQUIRE(lddh >= H && lddh % 4 == 0, "l2norm_bwd: bad lddh");
+    BGNN_REQUIRE(al16(g) && al16(o) && al16(dh) && al16(partial_db), "l2norm_bwd: pointers must be 16-byte aligned");
+    hipStream_t s = as_stream(stream);
+    int64_t rpb = 0;
+    const int64_t blocks = rows_grid(n_rows, 4, &rpb);
+    if (H > 256)
+        hipLaunchKernelGGL((k_sage_bwd_rows<2, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
+                           rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
+                           0);
+    else
+        hipLaunchKernelGGL((k_sage_bwd_rows<1, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
+                           rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
+                           0);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 4
+#define BGNN_ABI_VERSION 5
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -260,6 +260,16 @@ int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
                        int64_t n_rows, int32_t H, float* dh, int64_t lddh,
                        float* gskip, float* partial_db, float* amax,
                        const int32_t* w_rowptr, int32_t w_mode, void* stream);
+
+/* The L2-normalize backward of SAGEConv(normalize=True) alone (ABI 5): the per-module
+ * SAGEConv of the PyG surface (bgnn.nn.SAGEConv, called by the reference's unchanged
+ * Models/BuckGNN.py:434 under the shim), whose output o = h / max(||h||, 1e-12) feeds torch's
+ * BatchNorm/ReLU/Dropout. dh = (g - o <o, g>) / ||h|| per row (g * 1e12 where ||h|| < 1e-12),
+ * dh row stride lddh; partial_db [bgnn_rows_slots(n_rows)][2][H]: [.][0] = column sums of dh
+ * (the lin_l bias gradient; reduce with bgnn_reduce_partials), [.][1] = 0; *amax = max(*amax,
+ * max |dh|). nrm is bgnn_sage_fwd's row-norm output. */
+int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm, int64_t n_rows, int32_t H,
+                    float* dh, int64_t lddh, float* partial_db, float* amax, void* stream);
 
 /* ------------------------------------------------------------------------
  * fp32 GEMM (f32 operands, f32 result, f32 accumulation):

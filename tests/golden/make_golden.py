@@ -53,6 +53,15 @@ CASES = [
     ("sag_super_h64", "GraphSAGE_SAG", 64, "mean", [(5, True, 20), (4, True, 21)], True),
     ("sag_single_h64", "GraphSAGE_SAG", 64, "mean", [(6, False, 22)], True),
     ("eagnn_sag_h64", "EAGNN_SAG", 64, "mean", [(4, False, 23), (5, False, 24)], False),
+    # the production path (round 3): >= 1,024 nodes, where the fused model folds the node
+    # encoder's last Linear into the first SAGE layer and runs the encoder head as bgnn_mlp2
+    # (Models/BuckGNN.py:67-74,323,430-444); 23x23 + 22x22 meshes with virtual edges and an
+    # 8x8 mesh with a super node: 1,078 nodes
+    ("add_h512_n1k", "GraphSage_addAggr", 512, "mean", [(23, False, 30), (22, False, 31), (8, True, 32)], False),
+    ("shared_h512_n1k", "GraphSage_addAggr_Shared", 512, "mean", [(23, False, 30), (22, False, 31), (8, True, 32)],
+     False),
+    ("mean_h512_n1k", "GraphSage_meanAggr", 512, "mean", [(23, False, 33), (23, True, 34)], False),
+    ("sag_h512_n1k", "GraphSAGE_SAG", 512, "mean", [(23, False, 35), (23, False, 36)], False),
 ]
 
 

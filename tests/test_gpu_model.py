@@ -145,3 +145,35 @@ def test_ea_fused_gather_epilogue_matches_two_step(dev, monkeypatch, bf16):
         res.append([xo.detach(), eo.detach(), x.grad, e.grad, blk.edge_mlp[0].weight.grad.clone()])
     for a, c in zip(*res):
         torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-5)
+
+
+N1K = sorted(glob.glob(os.path.join(GOLDEN, "*_n1k.npz")))
+
+
+@pytest.mark.parametrize("path", N1K, ids=os.path.basename)
+def test_production_path_taken_on_n1k_goldens(dev, monkeypatch, path):
+    """The >= 1,024-node goldens run the bench's exact code path: the encoder head on
+    bgnn_mlp2 (fused._Mlp2Fn) and the encoder's last Linear folded into the first SAGE
+    layer (BuckGNN._foldable_encoder, sage_layer(w_in=...)); the parity itself is
+    test_model_matches_reference_golden on the same files."""
+    from bgnn import buckgnn, fused
+    seen = {"mlp2": 0, "fold": 0}
+    real_mlp2 = fused._Mlp2Fn.apply
+    monkeypatch.setattr(fused._Mlp2Fn, "apply", lambda *a: seen.__setitem__("mlp2", seen["mlp2"] + 1) or real_mlp2(*a))
+    real_layer = buckgnn.sage_layer
+
+    def spy(*a, **k):
+        if k.get("w_in") is not None:
+            seen["fold"] += 1
+        return real_layer(*a, **k)
+    monkeypatch.setattr(buckgnn, "sage_layer", spy)
+    z = np.load(path)
+    meta = meta_from_array(z["meta"])
+    model = build(meta, dev, True)
+    x = torch.from_numpy(z["x"]).to(dev)
+    assert x.size(0) >= 1024
+    model.train()
+    pred, _ = model(x, torch.from_numpy(z["edge_index"]).to(dev), torch.from_numpy(z["edge_attr"]).to(dev),
+                    torch.from_numpy(z["batch"]).to(dev))
+    assert seen == {"mlp2": 1, "fold": 1}, seen
+    np.testing.assert_allclose(pred.detach().cpu().numpy().reshape(-1), z["pred_train"], rtol=1e-4, atol=1e-4)

@@ -252,3 +252,26 @@ def test_sag_adam_steps_follow_oracle(dev, name, h, n):
         ref_opt.step()
         ref.append(float(rl))
     np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-5)
+
+
+def test_sagpooling_int32_edge_index_and_no_batch(dev):
+    """An int32 edge_index with batch=None (one graph): the pooled output equals the int64 call
+    (advisor round 2: the top-k kernels read `batch` as int64), and int32 `batch` vectors are
+    accepted by topk_select."""
+    b = S.make_batch(9, 1)
+    torch.manual_seed(5)
+    pool = bgnn.nn.SAGPooling(32, ratio=0.5, GNN=bgnn.nn.SAGEConv, aggr="add").to(dev)
+    x = torch.randn(b.num_nodes, 32, device=dev)
+    ei64 = b.edge_index.to(dev)
+    out64 = pool(x, ei64)
+    out32 = pool(x, ei64.to(torch.int32))
+    for a, c in zip(out64, out32):
+        if a is not None:
+            torch.testing.assert_close(a.to(c.dtype) if a.dtype != c.dtype else a, c)
+    score = torch.rand(b.num_nodes, device=dev)
+    p64 = P.topk_select(score, 0.5, torch.zeros(b.num_nodes, dtype=torch.long, device=dev))
+    p32 = P.topk_select(score, 0.5, torch.zeros(b.num_nodes, dtype=torch.int32, device=dev))
+    for a, c in zip(p64, p32):
+        assert torch.equal(a, c)
+    with pytest.raises(TypeError):
+        P.filter_edges(ei64, p64[1].to(torch.long), b.num_nodes)
