@@ -14,6 +14,7 @@ from .ops import aggregate, segment_reduce
 from .pyg_shim import install_pyg_shim, uninstall_pyg_shim
 from .store import GraphStore
 from .checkpoint import load_checkpoint, load_reference_checkpoint, save_checkpoint
+from .dataset import load_dataset_cache
 from .inference import evaluate
 from .train import EigenvalueScaler, GradAllReduce, RelativeErrorLoss, mape_error, train_step
 from . import losses
@@ -26,7 +27,7 @@ __all__ = [
     "global_mean_pool", "scatter_add", "scatter_mean", "scatter_sum", "aggregate", "segment_reduce",
     "install_pyg_shim", "uninstall_pyg_shim", "EigenvalueScaler", "GradAllReduce", "RelativeErrorLoss",
     "mape_error", "train_step", "load_library", "GraphStore", "load_checkpoint", "load_reference_checkpoint",
-    "save_checkpoint", "evaluate", "losses", "GraphMAELoss", "GraphMaxComponentRelativeError", "GraphMixedError",
+    "save_checkpoint", "load_dataset_cache", "evaluate", "losses", "GraphMAELoss", "GraphMaxComponentRelativeError", "GraphMixedError",
     "GraphMSELoss", "GraphRelativeError", "stress_errors",
 ]
 

@@ -25,12 +25,19 @@ def install_pyg_shim(force: bool = False) -> None:
     if existing is not None and not getattr(existing, "__bgnn_shim__", False) and not force:
         raise RuntimeError("a real torch_geometric is already imported; pass force=True to replace it")
     from . import data as D
+    from . import dataset as DS
     from . import nn as N
 
     nn_mod = _module("torch_geometric.nn", SAGEConv=N.SAGEConv, SAGPooling=N.SAGPooling,
                      global_mean_pool=N.global_mean_pool, global_max_pool=N.global_max_pool,
                      global_add_pool=N.global_add_pool)
     data_mod = _module("torch_geometric.data", Data=D.Data, Batch=D.Batch)
+    # unpickling targets of PyG-written dataset caches (GraphCreate.py:566-568 pickle.load):
+    # PyG's Data comes back as a bgnn Data with the same attributes
+    data_data_mod = _module("torch_geometric.data.data", Data=DS.PygData, DataEdgeAttr=DS.PygClassMarker,
+                            DataTensorAttr=DS.PygClassMarker)
+    storage_mod = _module("torch_geometric.data.storage", GlobalStorage=DS.PygStorage, NodeStorage=DS.PygStorage,
+                          EdgeStorage=DS.PygStorage, BaseStorage=DS.PygStorage)
     loader_mod = _module("torch_geometric.loader", DataLoader=D.DataLoader)
     pyg = _module("torch_geometric", nn=nn_mod, data=data_mod, loader=loader_mod, __version__="bgnn-shim")
     scatter = _module("torch_scatter", scatter_add=N.scatter_add, scatter_sum=N.scatter_sum,
@@ -39,14 +46,16 @@ def install_pyg_shim(force: bool = False) -> None:
         "torch_geometric": pyg,
         "torch_geometric.nn": nn_mod,
         "torch_geometric.data": data_mod,
+        "torch_geometric.data.data": data_data_mod,
+        "torch_geometric.data.storage": storage_mod,
         "torch_geometric.loader": loader_mod,
         "torch_scatter": scatter,
     })
 
 
 def uninstall_pyg_shim() -> None:
-    for k in ("torch_geometric", "torch_geometric.nn", "torch_geometric.data", "torch_geometric.loader",
-              "torch_scatter"):
+    for k in ("torch_geometric", "torch_geometric.nn", "torch_geometric.data", "torch_geometric.data.data",
+              "torch_geometric.data.storage", "torch_geometric.loader", "torch_scatter"):
         m = sys.modules.get(k)
         if m is not None and getattr(m, "__bgnn_shim__", False):
             del sys.modules[k]
