@@ -85,6 +85,14 @@ def parse():
                          "step; host: the same batches as store collated on the host (PyG DataLoader path of "
                          "the reference) and copied to the GPU inside the step")
     ap.add_argument("--store-graphs", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=0,
+                    help="> 0: the training loop's epoch shape (TRAIN_FINAL.py:246-298 over the DataLoader of "
+                         ":1298; BASELINE configs[3]): a dataset of --dataset-graphs meshes sharded by rank "
+                         "(each rank builds and keeps only its shard resident in a GraphStore), every epoch a "
+                         "shuffled pass over the shard in batches of 16 (drop_last); --steps is then the whole "
+                         "timed run (epochs x shard/16)")
+    ap.add_argument("--dataset-graphs", type=int, default=0,
+                    help="global dataset size for --epochs (default: --store-graphs per rank)")
     ap.add_argument("--lr", type=float, default=None,
                     help="Adam learning rate (default 1e-2, TRAIN_FINAL.py:37; EA_GNN 1e-3: at 1e-2 the h=512 "
                          "EA_GNN diverges in the reference too, tests/test_gpu_ea_train.py)")
@@ -170,17 +178,30 @@ def main():
     else:
         # a pool of meshes per rank, a different shuffled 16-graph batch every step
         c = synthetic.CONFIGS[args.config]
-        pool = [synthetic.make_mesh_graph(c["n"], 1000 * rank + g, super_node=c["super_node"])
-                for g in range(args.store_graphs)]
+        if args.epochs > 0:
+            # this rank's shard of a global dataset (graph g seeded by its global id)
+            n_global = args.dataset_graphs or args.store_graphs * world
+            gids = list(range(rank, n_global, world))
+            if len(gids) < bsz:
+                raise SystemExit(f"--epochs: the shard of rank {rank} has {len(gids)} graphs, fewer than a batch")
+            pool = [synthetic.make_mesh_graph(c["n"], g, super_node=c["super_node"]) for g in gids]
+            per_epoch = len(gids) // bsz
+            args.steps = args.epochs * per_epoch
+        else:
+            pool = [synthetic.make_mesh_graph(c["n"], 1000 * rank + g, super_node=c["super_node"])
+                    for g in range(args.store_graphs)]
         store = bgnn.GraphStore(pool, dev) if args.data == "store" else None
         rng = np.random.default_rng(rank)
         order = iter(())
+        epoch = -1
 
         def next_ids():
-            nonlocal order
+            nonlocal order, epoch
             ids = list(itertools.islice(order, bsz))
-            if len(ids) < bsz:
-                order = iter(rng.permutation(args.store_graphs))
+            if len(ids) < bsz:   # (drop_last: a partial batch starts the next epoch)
+                epoch += 1
+                order = iter(rng.permutation(len(pool)) if args.epochs <= 0
+                             else np.random.default_rng(1234 + epoch).permutation(len(pool)))
                 ids = list(itertools.islice(order, bsz))
             return ids
 
@@ -194,6 +215,9 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if args.epochs > 0:   # timed epochs start at an epoch boundary
+        order = iter(())
+        epoch = -1
     torch.cuda.synchronize()
     fused.TIMERS = {}
     if world > 1:
@@ -310,6 +334,8 @@ def main():
                            "host": f"new shuffled batch every step collated on the host from {args.store_graphs} "
                                    f"meshes and copied to the GPU (reference DataLoader path)"}[args.data],
             "data_path": args.data,
+            **({"epochs": args.epochs, "dataset_graphs": args.dataset_graphs or args.store_graphs * world,
+                "steps_per_epoch": args.steps // args.epochs} if args.epochs > 0 else {}),
             "global_batch": bsz * world,
             "nodes_per_gpu": N,
             "edges_per_gpu": E,
@@ -356,10 +382,29 @@ def main():
         "final_loss": loss_v,
     }
     if is_ea:
-        # the SAGE kernels above never run for EA_GNN: no roofline blocks for them
-        out["roofline"] = None
+        # the SAGE kernels above never run for EA_GNN. Its dominant kernels are the four per-edge
+        # K = H products of every GraphNetBlock (Models/BuckGNN.py:552-566 after the transform-first
+        # split, bgnn/ea.py): 2*E*H^2 flops each, reading an [E, H] f32 operand and writing an
+        # [E, H] f32 result (8*E*H bytes), so at these sizes they are HBM-bound.
         for k in ("roofline_hbm", "roofline_agg_bwd", "roofline_gemm"):
             out.pop(k)
+        ea_ms = avg_ms("ea_edge_fwd")
+        n_ea = len(timers.get("ea_edge_fwd", []))
+        ea_bytes = 8.0 * E * H
+        ea_flop = 2.0 * E * H * H
+        ea_gbs = ea_bytes / (ea_ms * 1e-3) / 1e9
+        ea_tfs = ea_flop / (ea_ms * 1e-3) / 1e12
+        ea_peak = BF16_MFMA_PEAK_TFS if args.bf16 else (H3_PEAK_TFS if gmode == 2 else FP32_MFMA_PEAK_TFS)
+        out["roofline"] = {
+            "kernel": "per-edge GraphNetBlock GEMMs (edge_mlp / phi, K = H = 512; gather-add + ReLU epilogues): "
+                      + ("k_gemm_x6 bf16 operands" if args.bf16 else "k_gemm_x6 f16x3"),
+            "bound": "hbm", "achieved": round(ea_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ea_gbs / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": ea_bytes,
+            "avg_launch_ms": round(ea_ms, 5), "launches": n_ea,
+            "ms_per_step": round(ea_ms * n_ea / args.steps, 4) if n_ea else float("nan"),
+            "mfma": {"achieved": round(ea_tfs, 2), "peak": ea_peak, "unit": "TFLOP/s",
+                     "frac": round(ea_tfs / ea_peak, 4), "algorithmic_flop": ea_flop},
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(batch_cpu, state0, args.model, args.cpu_steps)
     if rank == 0:

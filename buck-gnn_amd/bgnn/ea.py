@@ -28,6 +28,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from . import fused
 from .fused import gemm, linear, mlp, relu_bias_grad
 from .graph import SegmentIndex, _index_cache, _stream
 from .ops import segment_reduce
@@ -201,17 +202,23 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
     # node-level blocks of the two concatenation Linears, one GEMM
     P = linear(x, torch.cat([W1[:, :H], W1[:, H:2 * H], Wp[:, :H]], 0), None, False, bf16=bf16)
     P_row, P_col, Q = _ColumnBlocks.apply(P, 3)
-    if FUSED_GATHER:
-        h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=bf16)
-    else:
-        h1 = gather_add(linear(e, W1[:, 2 * H:], b1, False, bf16=bf16), P_row, seg_row, P_col,
-                        seg_col, relu=True)
-    e_out = linear(h1, W2, b2, False, bf16=bf16)
-    if FUSED_GATHER:
-        m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=bf16)
-    else:
-        m1 = gather_add(linear(e_out, Wp[:, H:], bp, False, bf16=bf16), Q, seg_col, relu=True)
-    msg = linear(m1, Wp2, bp2, False, bf16=bf16)
+    # the four per-edge K = H forward products, timed for the bench's EA_GNN roofline (each reads
+    # an [E, H] f32 operand and writes an [E, H] f32 result)
+    with fused._timed("ea_edge_fwd"):
+        if FUSED_GATHER:
+            h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=bf16)
+        else:
+            h1 = gather_add(linear(e, W1[:, 2 * H:], b1, False, bf16=bf16), P_row, seg_row, P_col,
+                            seg_col, relu=True)
+    with fused._timed("ea_edge_fwd"):
+        e_out = linear(h1, W2, b2, False, bf16=bf16)
+    with fused._timed("ea_edge_fwd"):
+        if FUSED_GATHER:
+            m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=bf16)
+        else:
+            m1 = gather_add(linear(e_out, Wp[:, H:], bp, False, bf16=bf16), Q, seg_col, relu=True)
+    with fused._timed("ea_edge_fwd"):
+        msg = linear(m1, Wp2, bp2, False, bf16=bf16)
     agg = segment_reduce(msg, seg_row, "mean")
     out = mlp(blk.node_mlp_gamma, torch.cat([x, agg], 1), bf16=bf16)
     out = out + mlp(blk.node_mlp_beta, out, bf16=bf16)
