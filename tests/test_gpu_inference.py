@@ -63,7 +63,9 @@ def test_evaluate_matches_oracle(dev):
         preds.append(p)
         t = scaler.denormalize_eigenvalue(b.y.double())
         apes.append(torch.abs((t - scaler.denormalize_eigenvalue(p)) / t) * 100)
-    np.testing.assert_allclose(r["predictions"].cpu().numpy(), torch.cat(preds).numpy(), rtol=1e-4, atol=1e-4)
+    # (evaluate returns denormalised predictions, INFERENCE.py:137-138)
+    np.testing.assert_allclose(r["predictions"].cpu().numpy(),
+                               scaler.denormalize_eigenvalue(torch.cat(preds)).numpy(), rtol=1e-4, atol=1e-4)
     ape = torch.cat(apes)
     assert r["mape"] == pytest.approx(float(ape.mean()), rel=1e-4, abs=1e-4)
     assert r["max_mape"] == pytest.approx(float(ape.max()), rel=1e-4, abs=1e-4)

@@ -61,7 +61,11 @@ def test_model_matches_reference_golden(dev, path, fused_path):
         elif k.startswith("gradsum/"):
             g = params[k[8:]].grad
             assert g is not None, k
-            np.testing.assert_allclose(grad_checksum(g.cpu().numpy()), z[k], rtol=2e-3, atol=2e-4, err_msg=k)
+            # [sum, sum |g|, projection]: the signed sums cancel (|sum| can be 1e-3 of sum |g| on
+            # the >= 1,024-node fixtures), so their error is bounded relative to the L1 mass sum |g|
+            # as well: |d| <= 2e-3 |ref| + 2e-4 + 1e-4 sum |g|
+            np.testing.assert_allclose(grad_checksum(g.cpu().numpy()), z[k], rtol=2e-3,
+                                       atol=2e-4 + 1e-4 * float(z[k][1]), err_msg=k)
     sd = model.state_dict()
     for k in z.files:
         if k.startswith("state/"):
