@@ -84,9 +84,9 @@ SIGNATURES = {
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
                                    c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p]),
     "bgnn_l2norm_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p]),
-    "bgnn_split_f16x2": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_i64, c_p]),
-    "bgnn_gemm_p16": (c_i32, [c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_i64, c_i64, c_p, c_f32, c_f32, c_p,
-                              c_i64, c_p, c_i32, c_p, c_p, c_i64, c_f32, c_u64, c_i32, c_p]),
+    "bgnn_split_f16x2": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p]),
+    "bgnn_gemm_p16": (c_i32, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_p, c_i64, c_p,
+                              c_i32, c_p, c_p, c_i64, c_f32, c_u64, c_i32, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
     "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
     "bgnn_gemm_f32_planes": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,

@@ -215,7 +215,8 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
 // ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored in
 // every piece slot), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA +
 // barriers), 4 = MFMA + barriers only, 5 = everything but the C stores, 6 = cached C stores,
-// 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands.
+// 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands,
+// 9 / 10 = s_setprio(1) around the MFMA block forced on / off (scheduling only; results unchanged).
 template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int NT = 64 * WM * WN;
@@ -282,6 +283,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
     constexpr bool kStage = ABL != 3 && ABL != 4, kLoad = kStage && ABL != 2;
+    // ABL 9: the MFMA block at s_setprio 1 (guide T5). Measured and not adopted: in an
+    // interleaved A/B (tools/prio_ab.py, cold cache) it lost on every SAGE shape -- fwd 317 ->
+    // 341 us, dgrad 324 -> 359, wgrad 303 -> 406 (a one-off sequential run had suggested a fwd
+    // gain). ABL 10 = the default (no priority change), kept for the A/B.
+    constexpr bool kPrio = ABL == 9;
     // the main loop is instantiated twice (interior tiles without guards, edge tiles with
     // them) and selected once, so the hot loop carries no per-slice bounds branches
     auto mainloop = [&](auto full_tag) {
@@ -339,7 +345,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             if (kt + 1 + PF < nk && kLoad) load_ab(kb + (kt + 1 + PF) * X6_BK, r);
             // keep the staging (split VALU, LDS writes, global loads) out of the MFMA block
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);
             mma_slice(cur, kt);
+            if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
             __syncthreads();
         };
         if (nk > 0) {
@@ -409,10 +417,14 @@ static void launch_x6_t(int cfg, int abl, dim3 grid, hipStream_t s, const GemmAr
             case 4: launch_x6_a<PREC, TA, TB, 4>(cfg, grid, s, g); break;
             case 5: launch_x6_a<PREC, TA, TB, 5>(cfg, grid, s, g); break;
             case 6: launch_x6_a<PREC, TA, TB, 6>(cfg, grid, s, g); break;
+            case 9: launch_x6_a<PREC, TA, TB, 9>(cfg, grid, s, g); break;
+            case 10: launch_x6_a<PREC, TA, TB, 10>(cfg, grid, s, g); break;
             default: launch_x6_a<PREC, TA, TB, 7>(cfg, grid, s, g); break;
         }
-    } else if constexpr (TA == 1 && TB == 0) {   // wgrad: ablation 7 (dword k-major staging) only
+    } else if constexpr (TA == 1 && TB == 0) {   // wgrad: ablations 7 (dword k-major staging), 9, 10 (priority)
         if (abl == 7) launch_x6_a<PREC, TA, TB, 7>(cfg, grid, s, g);
+        else if (abl == 9) launch_x6_a<PREC, TA, TB, 9>(cfg, grid, s, g);
+        else if (abl == 10) launch_x6_a<PREC, TA, TB, 10>(cfg, grid, s, g);
         else launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);
     } else {
         launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);

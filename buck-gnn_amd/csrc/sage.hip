@@ -267,37 +267,55 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     const float invn = 1.f / (float)(n_rows > 0 ? n_rows : 1);
     int cpos[NV];
     bool cok[NV];
-    float scv[NV][4], shv[NV][4], kA[NV][4], kB[NV][4], kC[NV][4], muv[NV][4], isv[NV][4];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         cpos[v] = (lane + 64 * v) * 4;
         cok[v] = cpos[v] < H;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int c = cok[v] ? cpos[v] + k : 0;
-            scv[v][k] = scale ? scale[c] : 1.f;
-            shv[v][k] = shift ? shift[c] : 0.f;
-            if (bn) {
-                // do = gamma*invstd/N * (N*g2 - sum_g2 - xhat*sum_g2xhat)
-                const float gi = (gamma ? gamma[c] : 1.f) * invstd[c];
-                kA[v][k] = gi;
-                kB[v][k] = gi * sum_g2[c] * invn;
-                kC[v][k] = gi * sum_g2xhat[c] * invn;
-                muv[v][k] = mean[c];
-                isv[v][k] = invstd[c];
-            } else {
-                kA[v][k] = 1.f; kB[v][k] = 0.f; kC[v][k] = 0.f; muv[v][k] = 0.f; isv[v][k] = 0.f;
-            }
+    }
+    // per-channel constants in LDS (read back per row as float4), not VGPRs: 56 registers
+    // fewer keep 4 waves per SIMD with two rows in flight per wave.
+    // cst[0..6][c] = scale, shift, kA, kB, kC, mean, invstd with
+    // do = gamma*invstd/N * (N*g2 - sum_g2 - xhat*sum_g2xhat) = kA g2 - kB - xhat kC
+    __shared__ __attribute__((aligned(16))) float cst[7][512];
+    for (int c = threadIdx.x; c < H; c += 256) {
+        cst[0][c] = scale ? scale[c] : 1.f;
+        cst[1][c] = shift ? shift[c] : 0.f;
+        if (bn) {
+            const float gi = (gamma ? gamma[c] : 1.f) * invstd[c];
+            cst[2][c] = gi;
+            cst[3][c] = gi * sum_g2[c] * invn;
+            cst[4][c] = gi * sum_g2xhat[c] * invn;
+            cst[5][c] = mean[c];
+            cst[6][c] = invstd[c];
+        } else {
+            cst[2][c] = 1.f; cst[3][c] = 0.f; cst[4][c] = 0.f; cst[5][c] = 0.f; cst[6][c] = 0.f;
         }
     }
+    __syncthreads();
     float db[NV][4], dw[NV][4];   // sums of dh and of w_r * dh (w_mode: row weights from w_rowptr)
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
         for (int k = 0; k < 4; ++k) db[v][k] = dw[v][k] = 0.f;
 
+    // the next row's g and o rows are loaded one row ahead (two rows in flight per wave: the
+    // kernel is latency-bound on these loads, not bandwidth-bound); same rows, same order
+    float4 gn[NV], on[NV];
+    auto fetch = [&](int64_t rr) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t i4 = rr * H4 + (cok[v] ? (cpos[v] >> 2) : 0);
+            gn[v] = reinterpret_cast<const float4*>(g)[i4];
+            on[v] = reinterpret_cast<const float4*>(o)[i4];
+        }
+    };
+    if (r0 + wave < r1) fetch(r0 + wave);
     for (int64_t r = r0 + wave; r < r1; r += 4) {
         float ov[NV][4], dov[NV][4], g1v[NV][4];
+        float4 gc[NV], oc[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) { gc[v] = gn[v]; oc[v] = on[v]; }
+        if (r + 4 < r1) fetch(r + 4);
         float dot = 0.f;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -307,22 +325,28 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
                 continue;
             }
             const int64_t i4 = r * H4 + (cpos[v] >> 2);
-            const float4 gv = reinterpret_cast<const float4*>(g)[i4];
-            const float4 o4 = reinterpret_cast<const float4*>(o)[i4];
+            const float4 gv = gc[v];
+            const float4 o4 = oc[v];
             const float gg[4] = {gv.x, gv.y, gv.z, gv.w};
             ov[v][0] = o4.x; ov[v][1] = o4.y; ov[v][2] = o4.z; ov[v][3] = o4.w;
             uint32_t m = 0xF;
             if (thr) m = keep_bits4(seed, (uint64_t)i4, thr);
+            float cv[7][4];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+                const float4 t4 = *reinterpret_cast<const float4*>(&cst[q][cpos[v]]);
+                cv[q][0] = t4.x; cv[q][1] = t4.y; cv[q][2] = t4.z; cv[q][3] = t4.w;
+            }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float g1 = ((m >> k) & 1u) ? gg[k] * (thr ? inv_keep : 1.f) : 0.f;
                 g1v[v][k] = g1;
-                const float yp = ov[v][k] * scv[v][k] + shv[v][k];
+                const float yp = ov[v][k] * cv[0][k] + cv[1][k];
                 const float g2 = (!RELU || yp > 0.f) ? g1 : 0.f;
                 float d;
                 if (bn) {
-                    const float xh = (ov[v][k] - muv[v][k]) * isv[v][k];
-                    d = kA[v][k] * g2 - kB[v][k] - xh * kC[v][k];
+                    const float xh = (ov[v][k] - cv[5][k]) * cv[6][k];
+                    d = cv[2][k] * g2 - cv[3][k] - xh * cv[4][k];
                 } else {
                     d = g2;
                 }

@@ -274,20 +274,20 @@ int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm, int64_t n_
 /* Pre-split f16x3 operands (ABI 5). An f32 matrix x [rows, cols] (ld ldx) as its two f16 pieces,
  * the split the f16x3 GEMM does internally: with s = 2^k from *amax (max|x|, or any bound within
  * a modest factor above it: max|x| s lands in [2^14, 2^15) for the exact max), hi = f16(x s),
- * lo = f16(x s - hi), stored as [2][rows][ldp] f16 (lo plane pstride elements after hi). */
+ * lo = f16(x s - hi), stored k8-interleaved: row r = [cols/8][hi 8 | lo 8] f16 (row stride ldp
+ * >= 2 cols elements). cols % 8 == 0. */
 int bgnn_split_f16x2(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* amax,
-                     uint16_t* pieces, int64_t ldp, int64_t pstride, void* stream);
+                     uint16_t* pieces, int64_t ldp, void* stream);
 /* C[M,N] = alpha * A B^T (+ beta C or the drop-add source, + bias, ReLU, max|C| into c_amax)
- * with A [M,K] and B [N,K] given as f16 pieces (a / b: hi plane, lo plane a_ps / b_ps elements
- * later; lda / ldb elements per row, multiples of 8) and the maxima their pieces were scaled by.
+ * with A [M,K] and B [N,K] given as k8-interleaved f16 pieces (bgnn_split_f16x2's layout; lda /
+ * ldb elements per row, >= 2K, multiples of 8) and the maxima their pieces were scaled by.
  * Bit-identical to bgnn_gemm_f32_scaled(f16x3) on the f32 operands. bsrc != NULL: the drop-add
  * epilogue of bgnn_gemm_f32_dropadd (beta must be 1). K % 32 == 0. variant: 0 (default), 1, 2
  * (tile / slice-depth choices, measurement only), 12-14 timing ablations. */
-int bgnn_gemm_p16(int64_t M, int64_t N, int64_t K, const uint16_t* a, int64_t lda, int64_t a_ps,
-                  const float* a_amax, const uint16_t* b, int64_t ldb, int64_t b_ps, const float* b_amax,
-                  float alpha, float beta, float* C, int64_t ldc, const float* bias, int32_t relu,
-                  float* c_amax, const float* bsrc, int64_t ld_bsrc, float p, uint64_t seed,
-                  int32_t variant, void* stream);
+int bgnn_gemm_p16(int64_t M, int64_t N, int64_t K, const uint16_t* a, int64_t lda, const float* a_amax,
+                  const uint16_t* b, int64_t ldb, const float* b_amax, float alpha, float beta, float* C,
+                  int64_t ldc, const float* bias, int32_t relu, float* c_amax, const float* bsrc,
+                  int64_t ld_bsrc, float p, uint64_t seed, int32_t variant, void* stream);
 
 /* ------------------------------------------------------------------------
  * fp32 GEMM (f32 operands, f32 result, f32 accumulation):

@@ -304,3 +304,46 @@ def test_gemm_tail_split_matches_fp64(dev, mnk):
 
 def test_gemm_tail_knob():
     assert _lib.query("bgnn_get_tuning", 9) == 0
+
+
+def _pieces(x, amax):
+    p = torch.empty(x.size(0), 2 * x.size(1), dtype=torch.float16, device=x.device)
+    _lib.call("bgnn_split_f16x2", x.data_ptr(), x.size(0), x.size(1), x.stride(0), amax.data_ptr(), p.data_ptr(),
+              2 * x.size(1), torch.cuda.current_stream().cuda_stream)
+    return p
+
+
+@pytest.mark.parametrize("mnk", [(3000, 1024, 512), (2900, 512, 1024), (700, 1024, 128)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+def test_gemm_presplit_bit_identical(dev, mnk, variant):
+    """The pre-split f16x3 GEMM (bgnn_gemm_p16: operands as k8-interleaved f16 pieces from
+    bgnn_split_f16x2, LDS-DMA staged; variant 4 persistent) equals the register-staged f16x3
+    GEMM on the f32 operands bit for bit, edge tiles included, with bias + ReLU + max|C| and
+    the drop-add epilogue (measured and not adopted)."""
+    M, N, K = mnk
+    torch.manual_seed(M + variant)
+    A = torch.randn(M, K, device=dev)
+    B = torch.randn(N, K, device=dev) / K ** 0.5
+    bias = torch.randn(N, device=dev)
+    am, bm = fused.absmax(A), fused.absmax(B)
+    s = torch.cuda.current_stream().cuda_stream
+    ap, bp = _pieces(A, am), _pieces(B, bm)
+    ref_amax = torch.zeros(1, device=dev)
+    ref = fused.gemm(A, B, trans_a=False, trans_b=True, a_amax=am, b_amax=bm, bias=bias, relu=True, c_amax=ref_amax)
+    C = torch.full((M, N), float("nan"), device=dev)
+    c_amax = torch.zeros(1, device=dev)
+    _lib.call("bgnn_gemm_p16", M, N, K, ap.data_ptr(), 2 * K, am.data_ptr(), bp.data_ptr(), 2 * K, bm.data_ptr(),
+              1.0, 0.0, C.data_ptr(), N, bias.data_ptr(), 1, c_amax.data_ptr(), None, N, 0.0, 0, variant, s)
+    assert torch.equal(C, ref)
+    assert torch.equal(c_amax, ref_amax)
+    if N == 512 and variant in (0, 4):   # the dgrad drop-add epilogue
+        g = torch.randn(M, N, device=dev)
+        C1 = torch.empty(M, N, device=dev)
+        wsb = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, 0, 1, 0)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M, N, K, A.data_ptr(), K, B.data_ptr(), K, C1.data_ptr(), N,
+                  am.data_ptr(), bm.data_ptr(), g.data_ptr(), N, 0.1, 77, ws.data_ptr(), wsb, s)
+        C2 = torch.empty(M, N, device=dev)
+        _lib.call("bgnn_gemm_p16", M, N, K, ap.data_ptr(), 2 * K, am.data_ptr(), bp.data_ptr(), 2 * K, bm.data_ptr(),
+                  1.0, 1.0, C2.data_ptr(), N, None, 0, None, g.data_ptr(), N, 0.1, 77, variant, s)
+        assert torch.equal(C1, C2)
