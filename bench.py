@@ -384,13 +384,15 @@ def main():
     if is_ea:
         # the SAGE kernels above never run for EA_GNN. Its dominant kernels are the four per-edge
         # K = H products of every GraphNetBlock (Models/BuckGNN.py:552-566 after the transform-first
-        # split, bgnn/ea.py): 2*E*H^2 flops each, reading an [E, H] f32 operand and writing an
-        # [E, H] f32 result (8*E*H bytes), so at these sizes they are HBM-bound.
+        # split, bgnn/ea.py): 2*E*H^2 flops each, reading an [E, H] operand and writing an [E, H]
+        # result -- 8*E*H bytes in f32 storage, 4*E*H with the bf16 configuration's bf16 edge
+        # storage (ea.BF16_STORAGE) -- so at these sizes they are HBM-bound.
         for k in ("roofline_hbm", "roofline_agg_bwd", "roofline_gemm"):
             out.pop(k)
         ea_ms = avg_ms("ea_edge_fwd")
         n_ea = len(timers.get("ea_edge_fwd", []))
-        ea_bytes = 8.0 * E * H
+        from bgnn import ea as ea_mod
+        ea_bytes = (4.0 if (args.bf16 and ea_mod.BF16_STORAGE) else 8.0) * E * H
         ea_flop = 2.0 * E * H * H
         ea_gbs = ea_bytes / (ea_ms * 1e-3) / 1e9
         ea_tfs = ea_flop / (ea_ms * 1e-3) / 1e12

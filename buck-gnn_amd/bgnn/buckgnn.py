@@ -22,8 +22,9 @@ from typing import Optional
 import torch
 from torch import Tensor, nn
 
+from . import ea as ea_mod
 from .ea import graphnet_block, skip_dropout
-from .fused import mlp, prepare_weights, sage_layer
+from .fused import mlp, mlp_bf16, prepare_weights, sage_layer
 from .graph import SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
@@ -174,7 +175,8 @@ class BuckGNN(nn.Module):
         # fused-path switch (tests compare both paths)
         self.use_fused = True
         # EA_GNN GEMM precision on the fused path: False = f32-accurate (f16x3), True = bf16
-        # operands with f32 accumulation (BASELINE configs[4])
+        # operands with f32 accumulation and bf16 storage of the per-edge activations
+        # (BASELINE configs[4]; bgnn.ea.BF16_STORAGE)
         self.ea_bf16 = False
         self._step = 0
 
@@ -337,8 +339,11 @@ class BuckGNN(nn.Module):
             x = self.node_encoder(x)
         ea_fused = name in ("EA_GNN", "EA_GNN_Shared", "EAGNN_SAG") and self._fused_ok(x)
         if ea_fused:
-            e = (mlp(self.edge_encoder, edge_attr) if edge_attr.size(0) >= 1024 and FUSED_ENCODER
-                 else self.edge_encoder(edge_attr))
+            if self.ea_bf16 and ea_mod.BF16_STORAGE and edge_attr.size(0) >= 1024 and FUSED_ENCODER:
+                e = mlp_bf16(self.edge_encoder, edge_attr)   # bf16 edge activations from the start
+            else:
+                e = (mlp(self.edge_encoder, edge_attr) if edge_attr.size(0) >= 1024 and FUSED_ENCODER
+                     else self.edge_encoder(edge_attr))
         if name == "EA_GNN_Shared":
             if not ea_fused:
                 e = self.edge_encoder(edge_attr)

@@ -29,7 +29,7 @@ import torch
 
 from . import _lib
 from . import fused
-from .fused import gemm, linear, mlp, relu_bias_grad
+from .fused import b16_weight, gemm, gemm_bf16, linear, linear_bf16, mlp, relu_bias_grad
 from .graph import SegmentIndex, _index_cache, _stream
 from .ops import segment_reduce
 
@@ -80,30 +80,50 @@ class _LinearGatherReLU(torch.autograd.Function):
     dp1 / dp2 = deterministic segment sums of g' by i1 / i2."""
 
     @staticmethod
-    def forward(ctx, e, W, b, p1, seg1: SegmentIndex, p2, seg2: SegmentIndex, bf16: bool):
+    def forward(ctx, e, W, b, p1, seg1: SegmentIndex, p2, seg2: SegmentIndex, bf16: bool, out_bf16: bool = False):
         e = e.contiguous()
         Wc = W.contiguous()
         M, K = e.shape
         N = Wc.size(0)
         if p1.stride(1) != 1 or (p2 is not None and p2.stride(1) != 1):
             raise ValueError("gather rows must have unit column stride")
-        out = torch.empty(M, N, dtype=torch.float32, device=e.device)
+        Wg = b16_weight(e, Wc) if bf16 else Wc
+        storage = ((1 if e.dtype == torch.bfloat16 else 0) | (2 if Wg.dtype == torch.bfloat16 else 0)
+                   | (4 if out_bf16 else 0))
+        out = torch.empty(M, N, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=e.device)
         prec = 1 if bf16 else 0
         ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, 0, 1, prec)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=e.device) if ws_bytes else None
-        _lib.call("bgnn_gemm_gather_add", 0, 1, M, N, K, e.data_ptr(), e.stride(0), Wc.data_ptr(), Wc.stride(0),
-                  out.data_ptr(), N, None if b is None else b.contiguous().data_ptr(), 1,
-                  p1.data_ptr(), seg1.index.data_ptr(), p1.stride(0),
-                  None if p2 is None else p2.data_ptr(), None if p2 is None else seg2.index.data_ptr(),
-                  0 if p2 is None else p2.stride(0), prec, None if ws is None else ws.data_ptr(), ws_bytes,
-                  _stream())
+        args = (e.data_ptr(), e.stride(0), Wg.data_ptr(), Wg.stride(0), out.data_ptr(), N,
+                None if b is None else b.contiguous().data_ptr(), 1,
+                p1.data_ptr(), seg1.index.data_ptr(), p1.stride(0),
+                None if p2 is None else p2.data_ptr(), None if p2 is None else seg2.index.data_ptr(),
+                0 if p2 is None else p2.stride(0))
+        if storage:   # bf16 edge activations (bf16 operands only)
+            if not bf16:
+                raise ValueError("linear_gather_relu: bf16 storage needs bf16 operands")
+            _lib.call("bgnn_gemm_gather_add_bf16", M, N, K, *args, storage, None if ws is None else ws.data_ptr(),
+                      ws_bytes, _stream())
+        else:
+            _lib.call("bgnn_gemm_gather_add", 0, 1, M, N, K, *args, prec, None if ws is None else ws.data_ptr(),
+                      ws_bytes, _stream())
         ctx.seg1, ctx.seg2, ctx.has2, ctx.bf16, ctx.has_bias = seg1, seg2, p2 is not None, bf16, b is not None
+        ctx.storage = storage
         ctx.save_for_backward(e, W, out)
         return out
 
     @staticmethod
     def backward(ctx, g):
         e, W, out = ctx.saved_tensors
+        if ctx.storage:   # bf16 storage: mask + f32 bias sum in torch, GEMMs on bgnn_gemm_bf16
+            g = torch.ops.aten.threshold_backward(g.contiguous(), out, 0.0)
+            db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
+            de = (gemm_bf16(g, W.t().contiguous(), False, True, out_bf16=e.dtype == torch.bfloat16)
+                  if ctx.needs_input_grad[0] else None)
+            dW = gemm_bf16(g, e, True, False)
+            d1 = segment_reduce(g, ctx.seg1, "sum")
+            d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
+            return de, dW, db, d1, None, d2, None, None, None
         # ReLU mask, bias gradient and max|g'| (the f16x3 operand scale of both GEMMs) in one pass
         g, db, g_amax = relu_bias_grad(g, out, ctx.has_bias)
         bf16 = ctx.bf16
@@ -114,7 +134,7 @@ class _LinearGatherReLU(torch.autograd.Function):
         dW = gemm(g, e, trans_a=True, trans_b=False, a_amax=g_amax, bf16=bf16)
         d1 = segment_reduce(g, ctx.seg1, "sum")
         d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
-        return de, dW, db, d1, None, d2, None, None
+        return de, dW, db, d1, None, d2, None, None, None
 
 
 def _epilogue_gather_available() -> bool:
@@ -124,10 +144,12 @@ def _epilogue_gather_available() -> bool:
     return fused.GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) != 0
 
 
-def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False):
+def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False, out_bf16=False):
     if not _epilogue_gather_available():
+        if e.dtype == torch.bfloat16 or out_bf16:
+            raise ValueError("linear_gather_relu: bf16 storage needs the epilogue gather (split GEMM family)")
         return gather_add(linear(e, W, b, False, bf16=bf16), p1, seg1, p2, seg2, relu=True)
-    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16)
+    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16, out_bf16)
 
 
 class _ColumnBlocks(torch.autograd.Function):
@@ -154,12 +176,18 @@ class _ColumnBlocks(torch.autograd.Function):
 FUSED_GATHER = True
 # EA_GNN's skip add + dropout over [E, H] / [N, H] as one pass (bgnn_add_dropout)
 FUSED_SKIP_DROPOUT = True
+# bf16 configuration (model.ea_bf16): the per-edge activations (edge encoder output, h1, e',
+# m1, messages and their gradients) are STORED in bf16 as well, like torch autocast's bf16
+# Linear outputs; node-level tensors, weights and their gradients stay f32. False = bf16
+# operands with f32 storage (round-2 form, A/B)
+BF16_STORAGE = True
 
 
 def _add_dropout(a: torch.Tensor, b, p: float, seed: int) -> torch.Tensor:
     out = torch.empty_like(a)
-    _lib.call("bgnn_add_dropout", a.data_ptr(), None if b is None else b.data_ptr(), a.numel(), float(p), seed,
-              out.data_ptr(), _stream())
+    fn = "bgnn_add_dropout_bf16" if a.dtype == torch.bfloat16 else "bgnn_add_dropout"
+    _lib.call(fn, a.data_ptr(), None if b is None else b.data_ptr(), a.numel(), float(p), seed, out.data_ptr(),
+              _stream())
     return out
 
 
@@ -181,9 +209,10 @@ def skip_dropout(a: torch.Tensor, b, p: float, training: bool, seed: int) -> tor
     """Dropout_p(a + b) (b may be None) as one pass: Models/BuckGNN.py:382-387."""
     if not training or p == 0.0:
         return a + b if b is not None else a
-    ok = (FUSED_SKIP_DROPOUT and a.is_cuda and a.dtype == torch.float32 and a.is_contiguous()
-          and a.numel() % 4 == 0 and a.data_ptr() % 16 == 0
-          and (b is None or (b.is_contiguous() and b.shape == a.shape and b.data_ptr() % 16 == 0)))
+    ok = (FUSED_SKIP_DROPOUT and a.is_cuda and a.dtype in (torch.float32, torch.bfloat16) and a.is_contiguous()
+          and a.numel() % (8 if a.dtype == torch.bfloat16 else 4) == 0 and a.data_ptr() % 16 == 0
+          and (b is None or (b.is_contiguous() and b.shape == a.shape and b.dtype == a.dtype
+                             and b.data_ptr() % 16 == 0)))
     if not ok:
         return torch.nn.functional.dropout(a + b if b is not None else a, p, True)
     return _SkipDropout.apply(a, b, p, seed)
@@ -204,6 +233,20 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
     P_row, P_col, Q = _ColumnBlocks.apply(P, 3)
     # the four per-edge K = H forward products, timed for the bench's EA_GNN roofline (each reads
     # an [E, H] f32 operand and writes an [E, H] f32 result)
+    st = bf16 and BF16_STORAGE and FUSED_GATHER and _epilogue_gather_available() and H % 8 == 0
+    if st:   # bf16 edge activations end to end
+        with fused._timed("ea_edge_fwd"):
+            h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=True, out_bf16=True)
+        with fused._timed("ea_edge_fwd"):
+            e_out = linear_bf16(h1, W2, b2, False, True)
+        with fused._timed("ea_edge_fwd"):
+            m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=True, out_bf16=True)
+        with fused._timed("ea_edge_fwd"):
+            msg = linear_bf16(m1, Wp2, bp2, False, True)
+        agg = segment_reduce(msg, seg_row, "mean")
+        out = mlp(blk.node_mlp_gamma, torch.cat([x, agg], 1), bf16=True)
+        out = out + mlp(blk.node_mlp_beta, out, bf16=True)
+        return out, e_out
     with fused._timed("ea_edge_fwd"):
         if FUSED_GATHER:
             h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=bf16)

@@ -162,6 +162,101 @@ def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float
     return out
 
 
+_BF16_BUILT = {(0, 1): (0, 1, 3, 4, 5, 7), (1, 0): (0, 1, 2, 3)}
+# bf16-stored A times an f32 weight (A B^T, K % 64 == 0): round the weight to bf16 once (torch's
+# round-to-nearest-even, the rounding the GEMM applies in-tile) so that both operands are bf16 and
+# the LDS-DMA bf16 kernel (gemm_b16.hip, bit-identical) takes the product. False: the
+# register-staged kernel reads the f32 weight (A/B).
+B16_WEIGHTS = True
+
+
+def b16_weight(a: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """w (the B^T operand of a K-contiguous product with a) as bf16 when a is stored bf16 and
+    the LDS-DMA bf16 kernel applies; else w unchanged."""
+    if B16_WEIGHTS and a.dtype == torch.bfloat16 and w.dtype == torch.float32 and w.size(1) % 64 == 0:
+        return w.to(torch.bfloat16)
+    return w
+
+
+def gemm_bf16(a: torch.Tensor, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, out_bf16: bool = False,
+              bias: torch.Tensor = None, relu: bool = False):
+    """C = act(op(a) @ op(b) + bias) on the bf16-operand GEMM (one bf16 MFMA product, f32
+    accumulation) with each of a / b / C stored as float32 or bfloat16 (bgnn_gemm_bf16): the bf16
+    configuration of EA_GNN keeps its per-edge activations in bf16 (half the HBM bytes)."""
+    for t in (a, b):
+        if t.dtype not in (torch.float32, torch.bfloat16) or t.stride(1) != 1:
+            raise ValueError("gemm_bf16: operands must be float32 / bfloat16 with unit column stride")
+    M = a.size(1) if trans_a else a.size(0)
+    K = a.size(0) if trans_a else a.size(1)
+    N = b.size(0) if trans_b else b.size(1)
+    if (b.size(1) if trans_b else b.size(0)) != K:
+        raise ValueError("gemm_bf16: inner dims differ")
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=b.device)
+    if not trans_a and trans_b:
+        b = b16_weight(a, b)
+    storage = ((1 if a.dtype == torch.bfloat16 else 0) | (2 if b.dtype == torch.bfloat16 else 0)
+               | (4 if out.dtype == torch.bfloat16 else 0))
+    if storage not in _BF16_BUILT.get((int(trans_a), int(trans_b)), (0,)):
+        raise ValueError(f"gemm_bf16: storage {storage} with trans_a={trans_a}, trans_b={trans_b} is not built")
+    ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, int(trans_a), int(trans_b), 1)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=b.device) if ws_bytes else None
+    _lib.call("bgnn_gemm_bf16", int(trans_a), int(trans_b), M, N, K, 1.0, a.data_ptr(), a.stride(0), b.data_ptr(),
+              b.stride(0), 0.0, out.data_ptr(), out.stride(0), _ptr(bias), int(relu), storage, _ptr(ws), ws_bytes,
+              _stream())
+    return out
+
+
+class LinearBf16Fn(torch.autograd.Function):
+    """y = act(x W^T + b) with bf16 operands and bf16 storage of x and / or y (EA_GNN's bf16
+    configuration: per-edge activations in bf16, like torch autocast's bf16 Linear). Backward:
+    ReLU mask and bias gradient (f32 sum) in torch, dgrad / wgrad on bgnn_gemm_bf16 (dx in x's
+    dtype, dW f32)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu: bool, out_bf16: bool):
+        x = x.contiguous()
+        y = gemm_bf16(x, weight.contiguous(), False, True, out_bf16=out_bf16, bias=bias, relu=relu)
+        ctx.relu, ctx.has_bias = relu, bias is not None
+        ctx.save_for_backward(x, weight, y if relu else torch.empty(0, device=x.device))
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, y = ctx.saved_tensors
+        g = g.contiguous()
+        if ctx.relu:
+            g = torch.ops.aten.threshold_backward(g, y, 0.0)
+        db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm_bf16(g, weight.t().contiguous(), False, True, out_bf16=x.dtype == torch.bfloat16)
+        dw = gemm_bf16(g, x, True, False)
+        return dx, dw, db, None, None
+
+
+def linear_bf16(x, weight, bias=None, relu=False, out_bf16=True):
+    return LinearBf16Fn.apply(x, weight, bias, relu, out_bf16)
+
+
+def mlp_bf16(seq: torch.nn.Sequential, x: torch.Tensor, out_bf16: bool = True):
+    """An nn.Sequential of Linear/ReLU with bf16 operands, every activation stored in bf16
+    (out_bf16: also the last one), each ReLU fused into the preceding Linear's epilogue."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, torch.nn.Linear):
+            fuse = i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.ReLU)
+            last = i + (2 if fuse else 1) >= len(mods)
+            x = linear_bf16(x, m.weight, m.bias, fuse, out_bf16 or not last)
+            i += 2 if fuse else 1
+        else:
+            x = m(x)
+            i += 1
+    return x
+
+
 def relu_bias_grad(g: torch.Tensor, y=None, bias: bool = True):
     """(g', db, max|g'|) for the backward of act(x W^T + b): g' = g masked by y > 0 (y = the ReLU
     output; None = no ReLU), db = column sums of g' (None when bias is False). One pass over g

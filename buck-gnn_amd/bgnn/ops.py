@@ -114,7 +114,35 @@ class _SegmentReduce(torch.autograd.Function):
         return g.index_select(0, seg.index), None, None
 
 
+class _SegmentReduceBf16(torch.autograd.Function):
+    """sum / mean over segments of a bf16 [n, H] source into f32 [R, H] (bgnn_segment_sum_bf16);
+    backward: every position receives its segment's (scaled) gradient row, in bf16."""
+
+    @staticmethod
+    def forward(ctx, src, seg: SegmentIndex, mean: bool):
+        H = src.size(1)
+        out = torch.empty(seg.num_rows, H, dtype=torch.float32, device=src.device)
+        _lib.call("bgnn_segment_sum_bf16", seg.fwd.rowptr.data_ptr(), seg.fwd.col.data_ptr(), seg.num_rows,
+                  src.data_ptr(), src.stride(0), H, int(mean), out.data_ptr(), out.stride(0), _stream())
+        ctx.seg, ctx.mean = seg, mean
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        seg = ctx.seg
+        g = g.contiguous()
+        if ctx.mean:
+            g = g / seg.fwd.degree().clamp_min(1).to(g.dtype).unsqueeze(1)
+        return g.to(torch.bfloat16).index_select(0, seg.index), None, None
+
+
 def segment_reduce(src: torch.Tensor, seg: SegmentIndex, reduce: str = "sum") -> torch.Tensor:
+    if src.dtype == torch.bfloat16 and reduce in ("sum", "add", "mean"):
+        require_cuda(src, what="segment_reduce")
+        src = src.contiguous()
+        if src.dim() != 2 or src.size(0) != seg.n or src.size(1) % 8 or src.size(1) > 512:
+            raise ValueError("segment_reduce(bf16): need [n, H] with H % 8 == 0, H <= 512")
+        return _SegmentReduceBf16.apply(src, seg, reduce == "mean")
     src = _check_x(src, "segment_reduce")
     if src.size(0) != seg.n:
         raise ValueError(f"segment_reduce: src has {src.size(0)} rows, index has {seg.n} entries")

@@ -31,6 +31,99 @@ __global__ __launch_bounds__(256) void k_add_dropout(const float4* __restrict__ 
     }
 }
 
+// bf16 storage (the EA_GNN bf16 configuration's edge activations): 8 elements per thread, the
+// same mask (group index = element / 4), sums in f32, one round to nearest even per result
+__device__ __forceinline__ void bf16x8_unpack(const uint4 q, float (&f)[8]) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        f[2 * h] = __uint_as_float(w[h] << 16);
+        f[2 * h + 1] = __uint_as_float(w[h] & 0xffff0000u);
+    }
+}
+
+__device__ __forceinline__ uint32_t bf16_pack2(float x, float y) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const f32x2 v = {x, y};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
+__global__ __launch_bounds__(256) void k_add_dropout_bf16(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                          int64_t n8, uint32_t thr, float inv_keep, uint64_t seed,
+                                                          uint4* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        float v[8];
+        bf16x8_unpack(a[i], v);
+        if (b) {
+            float w[8];
+            bf16x8_unpack(b[i], w);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += w[k];
+        }
+        if (thr) {
+#pragma unroll
+            for (int hgrp = 0; hgrp < 2; ++hgrp) {
+                const uint32_t keep = keep_bits4(seed, (uint64_t)(2 * i + hgrp), thr);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[4 * hgrp + k] = ((keep >> k) & 1u) ? v[4 * hgrp + k] * inv_keep : 0.f;
+            }
+        }
+        out[i] = make_uint4(bf16_pack2(v[0], v[1]), bf16_pack2(v[2], v[3]), bf16_pack2(v[4], v[5]),
+                            bf16_pack2(v[6], v[7]));
+    }
+}
+
+// Segment sum / mean over rows of a bf16 [n, H] matrix (H <= 512, H % 8 == 0) into f32
+// out[R, H]: one wave per output row, 8 columns (16 B) per lane, the row's entries in CSR order
+// (deterministic), f32 accumulation; empty rows 0. scatter_mean / scatter_add of EA_GNN's bf16
+// messages (Models/BuckGNN.py:561) and their ReLU-masked gradients.
+__global__ __launch_bounds__(256) void k_seg_sum_bf16(const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ col, int64_t R,
+                                                      const uint16_t* __restrict__ x, int64_t ldx, int H, int mean,
+                                                      float* __restrict__ out, int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int c = lane * 8;
+    const bool ok = c < H;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < R; r += nw) {
+        const int32_t b = rowptr[r], e = rowptr[r + 1];
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int32_t p = b;
+        for (; p + 8 <= e; p += 8) {   // 8 rows in flight
+            uint4 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t j = col[p + u];
+                q[u] = ok ? *reinterpret_cast<const uint4*>(x + j * ldx + c) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                float f[8];
+                bf16x8_unpack(q[u], f);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] += f[k];
+            }
+        }
+        for (; p < e; ++p) {
+            const int64_t j = col[p];
+            float f[8];
+            bf16x8_unpack(ok ? *reinterpret_cast<const uint4*>(x + j * ldx + c) : make_uint4(0, 0, 0, 0), f);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += f[k];
+        }
+        if (mean) {
+            const float inv = __frcp_rn((float)(e - b > 0 ? e - b : 1));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] *= inv;
+        }
+        if (ok) {
+            *reinterpret_cast<float4*>(out + r * ldo + c) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            *reinterpret_cast<float4*>(out + r * ldo + c + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+        }
+    }
+}
+
 inline unsigned elem_blocks(int64_t n4) {
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 8192) blocks = 8192;   // grid-stride beyond 32 blocks per CU
@@ -55,6 +148,37 @@ extern "C" int bgnn_add_dropout(const float* a, const float* b, int64_t n, float
     hipLaunchKernelGGL(k_add_dropout, dim3(elem_blocks(n / 4)), dim3(256), 0, as_stream(stream),
                        reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(b), n / 4, thr, inv_keep,
                        seed, reinterpret_cast<float4*>(out));
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_add_dropout_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
+                                     void* stream) {
+    BGNN_REQUIRE(n >= 0 && n % 8 == 0, "add_dropout_bf16: n must be a multiple of 8");
+    BGNN_REQUIRE(p >= 0.f && p < 1.f, "add_dropout_bf16: p must be in [0, 1)");
+    if (n == 0) return BGNN_OK;
+    BGNN_REQUIRE(a && out && aligned16(a) && aligned16(out) && (!b || aligned16(b)),
+                 "add_dropout_bf16: 16-byte aligned a / b / out required");
+    const uint32_t thr = dropout_threshold(p);
+    const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
+    hipLaunchKernelGGL(k_add_dropout_bf16, dim3(elem_blocks(n / 8)), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const uint4*>(a), reinterpret_cast<const uint4*>(b), n / 8, thr, inv_keep,
+                       seed, reinterpret_cast<uint4*>(out));
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
+                                     int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream) {
+    BGNN_REQUIRE(rowptr && (n_rows == 0 || (col && x && out)), "segment_sum_bf16: null pointer");
+    BGNN_REQUIRE(H > 0 && H <= 512 && H % 8 == 0 && ldx % 8 == 0 && ldx >= H && ldo >= H && ldo % 4 == 0,
+                 "segment_sum_bf16: H must be a multiple of 8 up to 512, rows 16-B aligned");
+    BGNN_REQUIRE(aligned16(x) && aligned16(out), "segment_sum_bf16: 16-byte aligned x / out required");
+    if (n_rows == 0) return BGNN_OK;
+    int64_t blocks = (n_rows + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_seg_sum_bf16, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), rowptr, col, n_rows,
+                       static_cast<const uint16_t*>(x), ldx, H, mean, out, ldo);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

@@ -521,7 +521,7 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
                             int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
                             int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
                             const float* b_amax, float* c_amax, int32_t precision, void* ws,
-                            size_t ws_bytes, void* stream, const BetaSrc& bs);
+                            size_t ws_bytes, void* stream, const BetaSrc& bs, int st = 0);
 
 extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
                                     const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride, const float* B,
@@ -551,8 +551,11 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
                             int64_t ldb, float beta, float* C, int64_t ldc, int64_t c_blk,
                             int64_t c_pstride, const float* bias, int32_t relu, const float* a_amax,
                             const float* b_amax, float* c_amax, int32_t precision, void* ws,
-                            size_t ws_bytes, void* stream, const BetaSrc& bs) {
+                            size_t ws_bytes, void* stream, const BetaSrc& bs, int st) {
     BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm: bad transpose flags");
+    BGNN_REQUIRE(st == 0 || (precision == 1 && a_blk == 0 && c_blk == 0 && !bs.src && c_amax == nullptr &&
+                             (!(st & 4) || beta == 0.f)),
+                 "gemm: bf16 storage needs the bf16-operand family, dense operands, no max|C| and beta 0 for a bf16 C");
     BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
     const int64_t a_inner = a_blk > 0 ? a_blk : (ta ? M : K);
     BGNN_REQUIRE((ta == 0 && lda >= a_inner) || (ta == 1 && lda >= a_inner) || M == 0 || K == 0, "gemm: bad lda");
@@ -594,13 +597,25 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
     }
     int split = Mt > 0 ? 1 : pl.split;
     if (split > 1 && (slabs == nullptr || slab_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
+    if (st & 4) split = 1;   // (a bf16 C has no f32 slab reduce)
     if (bs.src) {   // the masked beta source lives in the split kernels' epilogue: no split-K, no tail
         BGNN_REQUIRE(pl.x6 && pl.prec == 1 && Mt == 0, "gemm_dropadd: needs the f16x3 kernels without a tail split");
         split = 1;
     }
+    if ((st & 3) == 3 && alpha == 1.f && beta == 0.f) {   // bf16-stored A and B: the LDS-DMA bf16 kernel, all rows
+        GemmArgs gb{A, B, C, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, K, 1, bias, relu,
+                    0, 0, 0, 0, nullptr, nullptr, nullptr};
+        gb.st = st;
+        if (b16_ok(gb, ta, tb)) {
+            launch_b16(s, gb);
+            BGNN_CHECK_LAUNCH();
+            return BGNN_OK;
+        }
+    }
     const int64_t Ma = pl.rows_a;
     GemmArgs g{A, B, C, slabs, Ma, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
                a_blk, a_pstride, c_blk, c_pstride, a_amax, b_amax, nullptr};
+    g.st = st;
     if (bs.src) {
         g.bsrc = bs.src;
         g.ld_bsrc = bs.ld;
@@ -627,7 +642,7 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
         const int rc = launch_splitk_reduce(slabs, split, M, N, alpha, beta, C, ldc, bias, relu, c_blk, c_pstride, s);
         if (rc != BGNN_OK) return rc;
     }
-    if (Mt > 0) {   // tail rows: 256x256 tiles, split-K over tail_split slabs, then the slab reduce
+    if (Mt > 0) {   // tail rows: 256x256 tiles, split-K over tail_split slabs, then the slab reduce (f16x3 only)
         GemmArgs t = g;
         t.A = A + Ma * lda;
         t.C = C + Ma * ldc;
@@ -676,11 +691,11 @@ extern "C" int bgnn_gemm_f32(int32_t ta, int32_t tb, int64_t M, int64_t N, int64
 // act(op(A) op(B) + bias + add0[idx0[row]] (+ add1[idx1[row]])) with the gathered rows added in
 // the epilogue of the split kernels (no split-K). precision: 0 = f32-accurate (the split family of
 // BGNN_TUNE_GEMM_MODE; the f32 MFMA family is not supported here), 1 = bf16 operands.
-extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
-                                    int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                                    const float* bias, int32_t relu, const float* add0, const int64_t* idx0,
-                                    int64_t ld0, const float* add1, const int64_t* idx1, int64_t ld1,
-                                    int32_t precision, void* ws, size_t ws_bytes, void* stream) {
+static int gather_add_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                           const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, int32_t relu,
+                           const float* add0, const int64_t* idx0, int64_t ld0, const float* add1,
+                           const int64_t* idx1, int64_t ld1, int32_t precision, void* ws, size_t ws_bytes,
+                           void* stream, int st) {
     BGNN_REQUIRE((ta == 0 || ta == 1) && (tb == 0 || tb == 1), "gemm_gather_add: bad transpose flags");
     BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_gather_add: negative size");
     BGNN_REQUIRE(precision == 0 || precision == 1, "gemm_gather_add: precision must be 0 or 1");
@@ -714,10 +729,55 @@ extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N
     }
     GemmArgs g{A, B, C, nullptr, M, N, K, lda, ldb, ldc, 1.f, 0.f, 0, 1, bias, relu,
                0, 0, 0, 0, a_amax, b_amax, nullptr, add0, idx0, ld0, add1, idx1, ld1};
+    g.st = st;
     g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;
     if (g.kchunk == 0) g.kchunk = pl.bk;
-    if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, M, N), s, g);
+    if (b16_ok(g, ta, tb)) launch_b16(s, g);   // bf16-stored A and B: the LDS-DMA bf16 kernel
+    else if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, M, N), s, g);
     else launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles, 1), s, g);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
+}
+
+extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
+                                    int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                                    const float* bias, int32_t relu, const float* add0, const int64_t* idx0,
+                                    int64_t ld0, const float* add1, const int64_t* idx1, int64_t ld1,
+                                    int32_t precision, void* ws, size_t ws_bytes, void* stream) {
+    return gather_add_impl(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, bias, relu, add0, idx0, ld0, add1, idx1, ld1,
+                           precision, ws, ws_bytes, stream, 0);
+}
+
+// bf16-operand GEMM with bf16 STORAGE of any of A / B / C (EA_GNN's per-edge activations in the
+// bf16 configuration, BASELINE configs[4]): storage bit 0 = A, bit 1 = B, bit 2 = C; lda / ldb /
+// ldc count elements of the stored type. Operands are rounded to bf16 (exact when stored so),
+// one MFMA product, f32 accumulation; a bf16 C is rounded to nearest even.
+extern "C" int bgnn_gemm_bf16(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                              int64_t lda, const void* B, int64_t ldb, float beta, void* C, int64_t ldc,
+                              const float* bias, int32_t relu, int32_t storage, void* ws, size_t ws_bytes,
+                              void* stream) {
+    BGNN_REQUIRE(storage >= 0 && storage < 8, "gemm_bf16: storage flags must be in [0, 8)");
+    // built: NT {0, 1, 3, 4, 5, 7} (A and / or C bf16; B bf16 only with A), TN {0, 1, 2, 3}
+    const bool nt_ok = ta == 0 && tb == 1 && storage != 2 && storage != 6;
+    const bool tn_ok = ta == 1 && tb == 0 && storage <= 3;
+    BGNN_REQUIRE(storage == 0 || nt_ok || tn_ok, "gemm_bf16: storage %d with ta=%d tb=%d is not built", storage, ta,
+                 tb);
+    return gemm_scaled_impl(ta, tb, M, N, K, alpha, static_cast<const float*>(A), lda, 0, 0,
+                            static_cast<const float*>(B), ldb, beta, static_cast<float*>(C), ldc, 0, 0, bias, relu,
+                            nullptr, nullptr, nullptr, 1, ws, ws_bytes, stream, BetaSrc{nullptr, 0, 0, 0.f}, storage);
+}
+
+// bgnn_gemm_gather_add on the bf16-operand family with bf16 storage of any of A (bit 0), B
+// (bit 1) and C (bit 2); C = A B^T only (ta 0, tb 1). A and B both bf16 (bits 0 and 1) with
+// K % 64 == 0 take the LDS-DMA bf16 kernel (gemm_b16.hip).
+extern "C" int bgnn_gemm_gather_add_bf16(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                                         int64_t ldb, void* C, int64_t ldc, const float* bias, int32_t relu,
+                                         const float* add0, const int64_t* idx0, int64_t ld0, const float* add1,
+                                         const int64_t* idx1, int64_t ld1, int32_t storage, void* ws,
+                                         size_t ws_bytes, void* stream) {
+    BGNN_REQUIRE(storage >= 0 && storage < 8 && storage != 2 && storage != 6,
+                 "gemm_gather_add_bf16: storage must be one of 0, 1, 3, 4, 5, 7");
+    return gather_add_impl(0, 1, M, N, K, static_cast<const float*>(A), lda, static_cast<const float*>(B), ldb,
+                           static_cast<float*>(C), ldc, bias,
+                           relu, add0, idx0, ld0, add1, idx1, ld1, 1, ws, ws_bytes, stream, storage);
 }

@@ -1,0 +1,506 @@
+// bf16 GEMM on bf16-STORED operands (round 3): C = act(A B^T + bias (+ gathered rows)) with
+// A [M, K] and B [N, K] both bf16, K contiguous -- the per-edge Linears of EA_GNN's bf16
+// configuration (Models/BuckGNN.py:528-566 through bgnn/ea.py and fused.linear_bf16, BASELINE
+// configs[4]): edge_mlp / node_mlp_phi forward (A = the bf16 edge activations, B = the weight
+// rounded to bf16 once) and their input gradients (A = the bf16 output gradient, B = W^T).
+//
+// Arithmetic: identical to k_gemm_x6<PREC 2> bit for bit -- the same bf16 operand values (stored
+// bf16 = the round-to-nearest-even x6_store applies in-tile), one v_mfma_f32_32x32x16_bf16 per
+// 32x32x16 block, k16 steps in increasing k, the same x6_epilogue (bias, gathered rows, ReLU,
+// bf16 or f32 C) -- so every test of the x6 storage path holds for this kernel unchanged.
+//
+// Why a second kernel: x6 stages operands through registers (load, widen, round, ds_write) at
+// prefetch distance 1, built for the f32-accurate split; with the operands already bf16 there is
+// nothing to convert, and at E = 2.86M rows the x6 form ran at ~370 TF/s (4.57 ms per edge GEMM,
+// 46 % of the cfg5 step). Here operand bytes go HBM -> LDS by global_load_lds_dwordx4 alone (no
+// VGPRs, no VALU), BK = 64 k per slice so every row segment is one whole 128-B line, NS slots in
+// flight, one raw barrier per slice (gemm_p16.hip's pipeline with one product instead of three).
+// LDS image per slice: [A rows (BM) | B rows (BN)] x BK/8 16-B chunks, chunk c of row r at
+// physical chunk c ^ ((r / RPQ) mod CPR) so the 16 lanes of a ds_read_b128 group hit 16 distinct
+// bank slots; glds writes lane-linearly, so the swizzle goes on the per-lane source address.
+#include "common.h"
+#include "gemm_common.h"
+#include "gemm_x6.h"
+
+namespace bgnn {
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <int N>
+__device__ __forceinline__ void b16_wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// raw barrier: no vmcnt(0) drain of the glds in flight (__syncthreads() would emit one)
+__device__ __forceinline__ void b16_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int BK>
+struct B16Slice {
+    static constexpr int CPR = BK / 8;     // 16-B chunks (8 k) per row
+    static constexpr int RPQ = 16 / CPR;   // rows per 256-B bank row
+    static constexpr int RPI = 64 / CPR;   // rows per glds instruction (64 lanes x 16 B)
+    static constexpr int H = BK / 16;      // k16 MFMA steps per slice
+    __device__ static int swz(int row) { return (row / RPQ) % CPR; }
+    __device__ static int at(int row, int c) { return row * CPR + (c ^ swz(row)); }
+};
+
+// the H k16 steps of one landed slice; S restrict-scoped so hipcc does not drain the glds in
+// flight (vmcnt(0)) before these LDS reads (see gemm_p16.hip, p16_mma)
+template <int BM, int BN, int BK, int WM, int WN>
+__device__ __forceinline__ void b16_mma(const uint4* __restrict__ S, floatx16 (&acc)[BM / WM / 32][BN / WN / 32],
+                                        int wm, int wn, int lane) {
+    using L = B16Slice<BK>;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int h = 0; h < L::H; ++h) {
+        const int kg = 2 * h + lh;
+        uint4 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = S[L::at(wm * (BM / WM) + i * 32 + li, kg)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = S[L::at(BM + wn * (BN / WN) + j * 32 + li, kg)];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a[i]), as_bf16x8(b[j]), acc[i][j], 0, 0, 0);
+    }
+}
+
+// Epilogue (alpha 1, beta 0, no split-K): per 32-column block, the wave's TM x 32 x 32
+// accumulators go through its LDS stage (x6_epilogue's C/D map and stage layout) and leave as
+// 16-B non-temporal row stores -- f32 C: 4 columns per lane (8 lanes per 128-B row segment), bf16
+// C: 8 columns per lane (4 lanes per 64-B row segment; x6_epilogue stores 8 B). Per element the
+// arithmetic and its order are x6_epilogue's: acc, + bias, + ga0[gi0[row]], + ga1[gi1[row]],
+// ReLU, one bf16 rounding (RNE). Edge blocks fall back to x6_epilogue's element-guarded path.
+template <int TM, int TN, bool C16>
+__device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
+                                             int64_t c0, int lane, float* __restrict__ stage) {
+    constexpr int CPL = C16 ? 8 : 4;        // columns per lane
+    constexpr int LPR = 32 / CPL;           // lanes per 32-column row segment
+    constexpr int RPP = 64 / LPR;           // rows per pass
+    const int li = lane & 31, lh = lane >> 5;
+    const int rq = lane / LPR, cq = (lane % LPR) * CPL;
+    const bool gvec = (!g.ga0 || ((((uintptr_t)g.ga0 & 15) == 0) && g.ldg0 % 4 == 0)) &&
+                      (!g.ga1 || ((((uintptr_t)g.ga1 & 15) == 0) && g.ldg1 % 4 == 0));
+    const bool fast = gvec && (((uintptr_t)g.C & 15) == 0) && g.ldc % 8 == 0 &&
+                      (!g.bias || (((uintptr_t)g.bias & 15) == 0)) && r0 + TM * 32 <= g.M && c0 + TN * 32 <= g.N;
+    if (!fast) {
+        x6_epilogue<TM, TN, 0, C16>(g, acc, r0, c0, c0, 0, lane, 1.f, 1.f, stage);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int64_t col = c0 + j * 32 + cq;
+        float bv[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; k += 4) {
+            const float4 t = g.bias ? *reinterpret_cast<const float4*>(g.bias + col + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            bv[k] = t.x; bv[k + 1] = t.y; bv[k + 2] = t.z; bv[k + 3] = t.w;
+        }
+#pragma unroll 2
+        for (int q = 0; q < TM * 32 / RPP; ++q) {
+            const int rr = q * RPP + rq;
+            const int64_t row = r0 + rr;
+            float e[CPL], x0[CPL], x1[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; k += 4) {
+                const float4 sv = *reinterpret_cast<const float4*>(stage + rr * 32 + cq + k);
+                e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
+            }
+            if (g.ga0) {
+                const float* s0 = g.ga0 + g.gi0[row] * g.ldg0 + col;
+#pragma unroll
+                for (int k = 0; k < CPL; k += 4) {
+                    const float4 t = *reinterpret_cast<const float4*>(s0 + k);
+                    x0[k] = t.x; x0[k + 1] = t.y; x0[k + 2] = t.z; x0[k + 3] = t.w;
+                }
+                if (g.ga1) {
+                    const float* s1 = g.ga1 + g.gi1[row] * g.ldg1 + col;
+#pragma unroll
+                    for (int k = 0; k < CPL; k += 4) {
+                        const float4 t = *reinterpret_cast<const float4*>(s1 + k);
+                        x1[k] = t.x; x1[k + 1] = t.y; x1[k + 2] = t.z; x1[k + 3] = t.w;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                float v = e[k];
+                if (g.bias) v += bv[k];
+                if (g.ga0) v += x0[k];
+                if (g.ga1) v += x1[k];
+                if (g.relu) v = fmaxf(v, 0.f);
+                e[k] = v;
+            }
+            if constexpr (C16) {
+                typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+                const u32x4_t w = {pack_bf16(e[0], e[1]), pack_bf16(e[2], e[3]), pack_bf16(e[4], e[5]),
+                                   pack_bf16(e[6], e[7])};
+                __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(reinterpret_cast<uint16_t*>(g.C) +
+                                                                          row * g.ldc + col));
+            } else {
+                st_nt4(g.C + row * g.ldc + col, e);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+}
+
+// ABL: 0 = the kernel; 1 = timing ablation without the epilogue (one value per wave stored)
+template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, int ABL = 0>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
+    using L = B16Slice<BK>;
+    constexpr int NW = WM * WN;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int GA = BM / (L::RPI * NW), GB = BN / (L::RPI * NW);   // glds per wave per slice
+    constexpr int G = GA + GB;
+    constexpr int SLICE_U4 = (BM + BN) * L::CPR;
+    static_assert(GA * L::RPI * NW == BM && GB * L::RPI * NW == BN, "rows must split evenly over the waves");
+    static_assert((NS - 2) * G < 64, "vmcnt range");
+    constexpr int EPI_U4 = NW * TM * 32 * 32 / 4;
+    constexpr int SMEM_U4 = NS * SLICE_U4 > EPI_U4 ? NS * SLICE_U4 : EPI_U4;
+    static_assert(SMEM_U4 * 16 <= 160 * 1024, "LDS over 160 KiB");
+    __shared__ uint4 smem[SMEM_U4];   // one array (a second __shared__ object costs a vmcnt(0) per slice)
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int64_t ntn = (g.N + BN - 1) / BN;
+    // XCD-aware order: one XCD's workgroups take consecutive tiles = the column tiles of one row
+    // block, so A's rows come from HBM into that XCD's L2 once
+    const int lt = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t tm = lt / ntn, tn = lt % ntn;
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+
+    // per-lane glds sources: byte offsets from the tile's first A / B row (rows past the edge
+    // re-read the last row; their results are never stored); wave-uniform LDS destinations
+    const char* abase = reinterpret_cast<const char*>(g.A) + m0 * g.lda * 2;
+    const char* bbase = reinterpret_cast<const char*>(g.B) + n0 * g.ldb * 2;
+    uint32_t off[G];
+    int dst[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+        const bool isa = q < GA;
+        const int r0 = (isa ? wave * GA + q : wave * GB + (q - GA)) * L::RPI;
+        int r = r0 + lane / L::CPR;
+        const int c = (lane % L::CPR) ^ L::swz((isa ? 0 : BM) + r);
+        const int64_t rmax = (isa ? g.M - m0 : g.N - n0) - 1;
+        if (r > rmax) r = (int)rmax;
+        off[q] = (uint32_t)((r * (isa ? g.lda : g.ldb) + 8 * c) * 2);
+        dst[q] = ((isa ? 0 : BM) + r0) * L::CPR;
+    }
+    const int64_t nm = g.K / BK;
+    auto issue = [&](int64_t m) {
+        if (m >= nm) return;
+        const uint32_t kb = (uint32_t)(m * BK * 2);
+        uint4* slot = smem + (int)(m % NS) * SLICE_U4;
+#pragma unroll
+        for (int q = 0; q < G; ++q)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)((q < GA ? abase : bbase) + (off[q] + kb)),
+                                             (lds_void_t*)(slot + dst[q]), 16, 0, 0);
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // slice m lives in slot m % NS: wait for this wave's part of slice m (the NS - 2 newer
+    // slices stay in flight), one barrier (every wave's part landed, every wave done with slice
+    // m - 1, whose slot slice m + NS - 1 now refills), issue m + NS - 1, multiply slice m
+    for (int m = 0; m < NS - 1; ++m) issue(m);
+    for (int64_t m = 0; m < nm; ++m) {
+        if (m + NS - 2 < nm) b16_wait_vmcnt<(NS - 2) * G>();
+        else b16_wait_vmcnt<0>();
+        b16_barrier();
+        issue(m + NS - 1);
+        b16_mma<BM, BN, BK, WM, WN>(smem + (int)(m % NS) * SLICE_U4, acc, wm, wn, lane);
+    }
+    if constexpr (ABL == 1) {
+        float t0 = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) t0 += acc[i][j][0] + acc[i][j][15];
+        if (lane == 0) reinterpret_cast<float*>(g.C)[wave] = t0;
+        return;
+    }
+    __syncthreads();   // every wave's fragment reads done before the epilogue reuses the LDS
+    float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
+    b16_epilogue<TM, TN, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
+}
+
+// Epilogue of one wave's TM x TN blocks for the persistent kernel: each 32x32 block through a
+// wave-private 4 KiB LDS stage (separate from the operand slots, so the next tile's slices can be
+// in flight meanwhile), out as 16-B non-temporal row stores (f32: 4 columns per lane, bf16: 8);
+// x6_epilogue's per-element arithmetic and order; edge blocks store element-wise within bounds.
+template <int TM, int TN, bool C16>
+__device__ __forceinline__ void b16p_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
+                                              int64_t c0, int lane, float* __restrict__ stage) {
+    constexpr int CPL = C16 ? 8 : 4;
+    constexpr int LPR = 32 / CPL;
+    constexpr int RPP = 64 / LPR;
+    const int li = lane & 31, lh = lane >> 5;
+    const int rq = lane / LPR, cq = (lane % LPR) * CPL;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int64_t col = c0 + j * 32 + cq;
+        const bool cfull = c0 + j * 32 + 32 <= g.N;
+        float bv[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) bv[k] = (g.bias && (cfull || col + k < g.N)) ? g.bias[col + k] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const bool full = cfull && r0 + i * 32 + 32 <= g.M;
+#pragma unroll
+            for (int q = 0; q < 32 / RPP; ++q) {
+                const int rr = q * RPP + rq;
+                const int64_t row = r0 + i * 32 + rr;
+                float e[CPL];
+#pragma unroll
+                for (int k = 0; k < CPL; k += 4) {
+                    const float4 sv = *reinterpret_cast<const float4*>(stage + rr * 32 + cq + k);
+                    e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
+                }
+                if (!full && row >= g.M) continue;
+                float x0[CPL], x1[CPL];
+                if (g.ga0) {
+                    const float* s0 = g.ga0 + g.gi0[row] * g.ldg0 + col;
+                    const float* s1 = g.ga1 ? g.ga1 + g.gi1[row] * g.ldg1 + col : nullptr;
+                    if (full) {
+#pragma unroll
+                        for (int k = 0; k < CPL; k += 4) {
+                            const float4 t = *reinterpret_cast<const float4*>(s0 + k);
+                            x0[k] = t.x; x0[k + 1] = t.y; x0[k + 2] = t.z; x0[k + 3] = t.w;
+                            const float4 u = s1 ? *reinterpret_cast<const float4*>(s1 + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                            x1[k] = u.x; x1[k + 1] = u.y; x1[k + 2] = u.z; x1[k + 3] = u.w;
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < CPL; ++k) {
+                            x0[k] = col + k < g.N ? s0[k] : 0.f;
+                            x1[k] = (s1 && col + k < g.N) ? s1[k] : 0.f;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < CPL; ++k) {
+                    float v = e[k];
+                    if (g.bias) v += bv[k];
+                    if (g.ga0) v += x0[k];
+                    if (g.ga1) v += x1[k];
+                    if (g.relu) v = fmaxf(v, 0.f);
+                    e[k] = v;
+                }
+                if constexpr (C16) {
+                    uint16_t* p = reinterpret_cast<uint16_t*>(g.C) + row * g.ldc + col;
+                    if (full) {
+                        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+                        const u32x4_t w = {pack_bf16(e[0], e[1]), pack_bf16(e[2], e[3]), pack_bf16(e[4], e[5]),
+                                           pack_bf16(e[6], e[7])};
+                        __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < CPL; ++k)
+                            if (col + k < g.N) p[k] = (uint16_t)(pack_bf16(e[k], 0.f) & 0xffffu);
+                    }
+                } else {
+                    float* p = g.C + row * g.ldc + col;
+                    if (full) {
+                        st_nt4(p, e);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < CPL; ++k)
+                            if (col + k < g.N) p[k] = e[k];
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+}
+
+// Persistent form (variant 6): one workgroup per CU walks tiles first, first + grid, ... (XCD-aware:
+// at each step one XCD's 32 workgroups hold consecutive tiles, i.e. whole row blocks, so A's rows
+// are shared in its L2). The slice pipeline runs across tile boundaries: at a tile's last slice
+// the next tile's first slices are issued before the MFMAs and the epilogue, so their HBM latency
+// hides under this tile's epilogue instead of being exposed at every workgroup start, and the
+// workgroup never ends between tiles. (The epilogue's own loads -- bias, gathered rows -- wait
+// behind those slices in the in-order vmcnt, but both latencies run concurrently.)
+template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_b16p(GemmArgs g) {
+    using L = B16Slice<BK>;
+    constexpr int NW = WM * WN;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int GA = BM / (L::RPI * NW), GB = BN / (L::RPI * NW);
+    constexpr int G = GA + GB;
+    constexpr int SLICE_U4 = (BM + BN) * L::CPR;
+    constexpr int STAGE_U4 = NW * 32 * 32 / 4;   // one 32x32 f32 block per wave
+    static_assert(GA * L::RPI * NW == BM && GB * L::RPI * NW == BN, "rows must split evenly over the waves");
+    static_assert((NS - 2) * G < 64, "vmcnt range");
+    static_assert((NS * SLICE_U4 + STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
+    __shared__ uint4 smem[NS * SLICE_U4 + STAGE_U4];
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int wave = t >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int64_t ntn = (g.N + BN - 1) / BN;
+    const int64_t ntiles = ((g.M + BM - 1) / BM) * ntn;
+    const int64_t first = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t stride = gridDim.x;
+    if (first >= ntiles) return;   // (workgroup-uniform: the whole workgroup leaves together)
+    const int64_t my_tiles = (ntiles - first + stride - 1) / stride;
+    const int64_t nm = g.K / BK;
+    const int64_t total = my_tiles * nm;
+
+    uint32_t off[G];
+    int dst[G];
+    const char* abase = nullptr;
+    const char* bbase = nullptr;
+    int64_t off_tile = -1;
+    auto set_tile = [&](int64_t k) {
+        const int64_t lt = first + k * stride;
+        const int64_t m0 = (lt / ntn) * BM, n0 = (lt % ntn) * BN;
+        abase = reinterpret_cast<const char*>(g.A) + m0 * g.lda * 2;
+        bbase = reinterpret_cast<const char*>(g.B) + n0 * g.ldb * 2;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            const bool isa = q < GA;
+            const int r0 = (isa ? wave * GA + q : wave * GB + (q - GA)) * L::RPI;
+            int r = r0 + lane / L::CPR;
+            const int c = (lane % L::CPR) ^ L::swz((isa ? 0 : BM) + r);
+            const int64_t rmax = (isa ? g.M - m0 : g.N - n0) - 1;
+            if (r > rmax) r = (int)rmax;
+            off[q] = (uint32_t)((r * (isa ? g.lda : g.ldb) + 8 * c) * 2);
+            dst[q] = ((isa ? 0 : BM) + r0) * L::CPR;
+        }
+        off_tile = k;
+    };
+    auto issue = [&](int64_t S) {
+        if (S >= total) return;
+        const int64_t k = S / nm;
+        if (k != off_tile) set_tile(k);
+        const uint32_t kb = (uint32_t)((S % nm) * BK * 2);
+        uint4* slot = smem + (int)(S % NS) * SLICE_U4;
+#pragma unroll
+        for (int q = 0; q < G; ++q)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)((q < GA ? abase : bbase) + (off[q] + kb)),
+                                             (lds_void_t*)(slot + dst[q]), 16, 0, 0);
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    float* stage = reinterpret_cast<float*>(smem + NS * SLICE_U4) + wave * (32 * 32);
+
+    for (int S = 0; S < NS - 1; ++S) issue(S);
+    for (int64_t S = 0; S < total; ++S) {
+        if (S + NS - 2 < total) b16_wait_vmcnt<(NS - 2) * G>();
+        else b16_wait_vmcnt<0>();
+        b16_barrier();
+        issue(S + NS - 1);
+        b16_mma<BM, BN, BK, WM, WN>(smem + (int)(S % NS) * SLICE_U4, acc, wm, wn, lane);
+        if (S % nm == nm - 1) {   // the tile's last slice: its epilogue, the next tile's slices in flight
+            const int64_t lt = first + (S / nm) * stride;
+            const int64_t m0 = (lt / ntn) * BM, n0 = (lt % ntn) * BN;
+            b16p_epilogue<TM, TN, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        }
+    }
+}
+
+int g_b16_variant = 0;
+constexpr int64_t kPersistentWgs = 256;   // MI355X CUs   // -1: bf16-stored NT products on k_gemm_x6 instead (A/B)
+
+}  // namespace
+
+bool b16_ok(const GemmArgs& g, int ta, int tb) {
+    constexpr int64_t kMaxTileBytes = int64_t(1) << 31;
+    return g_b16_variant >= 0 && ta == 0 && tb == 1 && (g.st & 3) == 3 && g.split <= 1 && g.K > 0 && g.K % 64 == 0 &&
+           g.a_blk == 0 && g.c_blk == 0 && g.bsrc == nullptr && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+           aligned16(g.A) && aligned16(g.B) && 256 * g.lda * 2 < kMaxTileBytes && 256 * g.ldb * 2 < kMaxTileBytes;
+}
+
+// variant 0 (default) picks per call: the persistent kernel when the epilogue stores bf16 or
+// gathers rows (measured at E = 715,872 x 512 x 512: gathered bf16 1141 -> 1012 us, bf16 C 601 ->
+// 574 us), the one-tile-per-workgroup kernel for a plain f32 C (608 vs 649 us)
+static int b16_pick(const GemmArgs& g) {
+    if (g_b16_variant != 0) return g_b16_variant;
+    return ((g.st & 4) || g.ga0) ? 6 : 7;
+}
+
+static int b16_bm(int v) { return (v == 2 || v == 3 || v == 5) ? 128 : 256; }
+
+static int64_t b16_grid(int v, int64_t M, int64_t N) {
+    const int bm = b16_bm(v);
+    const int64_t tiles = ((M + bm - 1) / bm) * ((N + 255) / 256);
+    if (v == 6) return tiles < kPersistentWgs ? tiles : kPersistentWgs;   // persistent: one per CU
+    return tiles;
+}
+
+template <bool C16>
+static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    switch (v) {
+        case 1:   // 256x256, k32 slices (64-B row segments) x 4 slots
+            hipLaunchKernelGGL((k_gemm_b16<256, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        case 2:   // 128x256, k32 x 3 slots (72 KiB of LDS, <= 128 VGPRs: two workgroups per CU)
+            hipLaunchKernelGGL((k_gemm_b16<128, 256, 32, 3, 2, 4, C16, 4>), grid, dim3(512), 0, s, g); break;
+        case 3:   // 128x256, k64 x 2 slots (96 KiB: one workgroup per CU)
+            hipLaunchKernelGGL((k_gemm_b16<128, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        case 4:   // ablation: variant 0 without the epilogue
+            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 1>), grid, dim3(512), 0, s, g); break;
+        case 5:   // ablation: variant 2 without the epilogue
+            hipLaunchKernelGGL((k_gemm_b16<128, 256, 32, 3, 2, 4, C16, 4, 1>), grid, dim3(512), 0, s, g); break;
+        case 6:   // persistent 256x256, k64 x 2 slots (+ 32 KiB epilogue stage)
+            hipLaunchKernelGGL((k_gemm_b16p<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        default:  // 7: 256x256, k64 slices (whole 128-B row segments) x 2 slots
+            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+    }
+}
+
+void launch_b16(hipStream_t s, const GemmArgs& g) {
+    const int v = b16_pick(g);
+    const dim3 grid((unsigned)b16_grid(v, g.M, g.N));
+    if (g.st & 4) launch_b16_t<true>(v, grid, s, g);
+    else launch_b16_t<false>(v, grid, s, g);
+}
+
+}  // namespace bgnn
+
+extern "C" int bgnn_gemm_b16_variant(int32_t variant) {
+    BGNN_REQUIRE(variant >= -1 && variant <= 7, "gemm_b16_variant: must be -1 (off) or 0..7");
+    bgnn::g_b16_variant = variant;
+    return BGNN_OK;
+}

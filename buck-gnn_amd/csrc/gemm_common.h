@@ -32,6 +32,9 @@ struct GemmArgs {
     // layer's counter-based mask (keep_bits4(dseed, (row * ld_bsrc + col) / 4, dthr), kept
     // values scaled by dkeep; dthr = 0: no mask), so bgnn_sage_bwd_rows need not write it
     const float* bsrc; int64_t ld_bsrc; uint64_t dseed; uint32_t dthr; float dkeep;
+    // bf16-operand family (PREC 2) only: bf16 STORAGE of A (bit 0), B (bit 1), C (bit 2) -- the
+    // pointers then address bf16 elements and lda / ldb / ldc count bf16 elements
+    int st;
 };
 
 // the beta operand of 4 consecutive columns (col % 4 == 0) of row `row`: masked bsrc
@@ -71,6 +74,11 @@ bool h3g_ok(const GemmArgs& g, int ta, int tb);
 int64_t h3g_tiles(int variant, int64_t M, int64_t N);
 void launch_h3g(int variant, int64_t tiles, hipStream_t s, const GemmArgs& g);
 constexpr int kNumH3gVariants = 2;
+// bf16-operand GEMM on bf16-STORED A and B (gemm_b16.hip): b16_ok = the call qualifies (ta 0,
+// tb 1, storage bits 0 and 1, K % 64 == 0, dense 16-B aligned rows, no split-K / drop-add);
+// launch_b16 covers all M rows (no tail split; tile / persistent form picked per call)
+bool b16_ok(const GemmArgs& g, int ta, int tb);
+void launch_b16(hipStream_t s, const GemmArgs& g);
 // folds max |P| over the rows x cols matrix (ld; plane-split by blk / pstride when blk > 0)
 // into *out (f32 bits, unsigned atomic max; *out must hold a non-negative value)
 void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64_t blk, int64_t pstride,

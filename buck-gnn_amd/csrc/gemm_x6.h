@@ -75,13 +75,25 @@ __device__ __forceinline__ void st_nt4(float* p, const float (&e)[4]) {
 // and reads it back as float4 rows (8 lanes per 128-B row segment, conflict-free
 // ds_read_b128), so C leaves as 16-B stores, 1 KiB per wave instruction. Unscale (f16x3),
 // alpha, beta, bias, ReLU and the max |C| (c_amax) are applied per float4.
-template <int TM, int TN, int ABL = 0>
+// C16: C stored as bf16 (round to nearest even), 8-B stores; no beta / split-K with it.
+__device__ __forceinline__ void st_bf16x4(float* p, const float (&e)[4]) {
+    uint2 q;
+    q.x = pack_bf16(e[0], e[1]);
+    q.y = pack_bf16(e[2], e[3]);
+    *reinterpret_cast<uint2*>(p) = q;
+}
+
+template <int TM, int TN, int ABL = 0, bool C16 = false>
 __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
                                             int64_t c0, int64_t n0, int ks, int lane, float ia, float ib,
                                             float* __restrict__ stage) {
     const bool split = g.split > 1;
     float* __restrict__ dst = split ? g.ws + (int64_t)ks * g.M * g.N
                                     : const_cast<float*>(plane_base(g.C, n0, g.c_blk, g.c_pstride));
+    // bf16 C: element (row, col) at (uint16_t*)C + row * ldc + col
+    auto c16_at = [&](int64_t row, int64_t col) -> float* {
+        return reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(g.C) + row * g.ldc + col);
+    };
     const int64_t ldd = split ? g.N : g.ldc;
     const bool vec = (((uintptr_t)dst & 15) == 0) && (ldd % 4 == 0);
     const bool bias_vec = g.bias && (((uintptr_t)g.bias & 15) == 0);
@@ -144,7 +156,9 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                     cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
                 }
                 if (ABL == 5 && e[0] != 1234.5f) continue;   // ablation: no C stores
-                if constexpr (ABL == 6) {   // ablation: cached (write-allocate) C stores
+                if constexpr (C16) {
+                    st_bf16x4(c16_at(r0 + q * 8 + rq, col), e);
+                } else if constexpr (ABL == 6) {   // ablation: cached (write-allocate) C stores
                     *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
                 } else {
                     st_nt4(p, e);
@@ -208,7 +222,16 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                     if (col + k < g.N) cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
                 }
             }
-            if (full) {
+            if constexpr (C16) {
+                if (full && !split) {
+                    st_bf16x4(c16_at(row, col), e);
+                } else {
+                    uint16_t* p16 = reinterpret_cast<uint16_t*>(c16_at(row, col));
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (col + k < g.N) p16[k] = (uint16_t)(pack_bf16(e[k], 0.f) & 0xffffu);
+                }
+            } else if (full) {
                 st_nt4(p, e);
             } else {
 #pragma unroll

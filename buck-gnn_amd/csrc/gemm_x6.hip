@@ -49,13 +49,46 @@ __device__ __forceinline__ int x6_pos(int row, int chunk) { return row * 4 + (ch
 // One staging unit = 8 consecutive k of one row r (r = m or n) of the tile.
 //   KCONTIG = 1: element (r, k) at P[r * ld + k];   unit idx -> r = idx / 4, chunk = idx % 4
 //   KCONTIG = 0: element (r, k) at P[k * ld + r];   unit idx -> r = idx % R, chunk = idx / R
-template <int KCONTIG, int R, int NT, bool FULL>
+// bf16 element e of operand storage P16 (exact in f32)
+__device__ __forceinline__ float bf16_at(const uint16_t* __restrict__ P16, int64_t e) {
+    return __uint_as_float((uint32_t)P16[e] << 16);
+}
+
+// BF: the operand is stored as bf16 (ld in bf16 elements; the EA_GNN edge activations of the
+// bf16 configuration): loaded at half the bytes and widened exactly to f32 in registers.
+template <int KCONTIG, int R, int NT, bool FULL, bool BF = false>
 __device__ __forceinline__ void x6_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0,
                                         int64_t k0, int64_t kend, bool vec_ok, float (&v)[R * 4 / NT][8], int t) {
     constexpr int NU = R * 4 / NT;
+    const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int idx = t + NT * u;
+        if constexpr (BF) {
+            if constexpr (KCONTIG) {
+                const int r = idx >> 2, c = idx & 3;
+                const int64_t gr = r0 + r, gk = k0 + c * 8;
+                if (FULL || (vec_ok && gr < Rlim && gk + 7 < kend)) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(P16 + gr * ld + gk);
+                    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        v[u][2 * h] = __uint_as_float(w[h] << 16);
+                        v[u][2 * h + 1] = __uint_as_float(w[h] & 0xffff0000u);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) v[u][q] = (gr < Rlim && gk + q < kend) ? bf16_at(P16, gr * ld + gk + q) : 0.f;
+                }
+            } else {
+                const int r = idx % R, c = idx / R;
+                const int64_t gr = r0 + r, gk = k0 + c * 8;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    v[u][q] = (FULL || (gr < Rlim && gk + q < kend)) ? bf16_at(P16, (gk + q) * ld + gr) : 0.f;
+            }
+            continue;
+        }
         if constexpr (KCONTIG) {
             const int r = idx >> 2, c = idx & 3;
             const int64_t gr = r0 + r, gk = k0 + c * 8;
@@ -135,11 +168,27 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
 // 8-k units, written as the same [row][32 k] swizzled images as the K-contiguous path (so
 // the MFMA reads are unchanged). Quads of A go to threads [0, BM), of B to [BM, BM + BN).
 // Measured (wgrad 1024x512x80656, 256x256 tiles): 804 -> 300 us against per-lane dword loads.
-template <int R, bool FULL>
+template <int R, bool FULL, bool BF = false>
 __device__ __forceinline__ void kq_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
                                         int64_t kend, bool vec_ok, float (&v)[4][8], int q) {
     const int r4 = q % (R / 4), c = q / (R / 4);
     const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
+    if constexpr (BF) {   // bf16 storage: 4 consecutive rows = one 8-B load per k
+        const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
+                const uint2 f = *reinterpret_cast<const uint2*>(P16 + (gk + k) * ld + gr);
+                v[0][k] = __uint_as_float(f.x << 16); v[1][k] = __uint_as_float(f.x & 0xffff0000u);
+                v[2][k] = __uint_as_float(f.y << 16); v[3][k] = __uint_as_float(f.y & 0xffff0000u);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[i][k] = (gr + i < Rlim && gk + k < kend) ? bf16_at(P16, (gk + k) * ld + gr + i) : 0.f;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
@@ -217,8 +266,14 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
 // barriers), 4 = MFMA + barriers only, 5 = everything but the C stores, 6 = cached C stores,
 // 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands,
 // 9 / 10 = s_setprio(1) around the MFMA block forced on / off (scheduling only; results unchanged).
-template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL = 0>
+// ABL >= 16: not an ablation but the bf16 STORAGE flags ST = ABL - 16 of the bf16-operand family
+// (PREC 2): bit 0 = A, bit 1 = B, bit 2 = C stored as bf16 (EA_GNN's per-edge activations).
+template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL_ = 0>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
+    constexpr int ST = ABL_ >= 16 ? ABL_ - 16 : 0;
+    constexpr int ABL = ABL_ >= 16 ? 0 : ABL_;
+    constexpr bool A16 = (ST & 1) != 0, B16 = (ST & 2) != 0, C16 = (ST & 4) != 0;
+    static_assert(ST == 0 || PREC == 2, "bf16 storage is for the bf16-operand family only");
     constexpr int NT = 64 * WM * WN;
     constexpr int NP = PREC == 1 ? 2 : (PREC == 2 ? 1 : 3);   // pieces per operand
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -251,8 +306,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     const int64_t kb = (int64_t)ks * g.kchunk;
     const int64_t ke = min(g.K, kb + g.kchunk);
 
-    const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % 4 == 0);
-    const bool b_vec = (((uintptr_t)g.B & 15) == 0) && (g.ldb % 4 == 0);
+    // vector loads need 16-B aligned rows (bf16 storage: 8 elements; k-major quads: 8 B, 4 elements)
+    const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % ((A16 && AK) ? 8 : 4) == 0);
+    const bool b_vec = (((uintptr_t)g.B & 15) == 0) && (g.ldb % ((B16 && BKc) ? 8 : 4) == 0);
 
     float sa = 1.f, sb = 1.f, ia = 1.f, ib = 1.f;
     if constexpr (PREC == 1) {
@@ -295,11 +351,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         auto load_ab = [&](int64_t k0, Regs& r) {
             const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
             if constexpr (KQ) {
-                if (t < BM) kq_load<BM, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
-                else if (t < BM + BN) kq_load<BN, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+                if (t < BM) kq_load<BM, FULL, A16>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
+                else if (t < BM + BN) kq_load<BN, FULL, B16>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
             } else {
-                x6_load<AK, BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
-                x6_load<BKc, BN, NT, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
+                x6_load<AK, BM, NT, FULL, A16>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
+                x6_load<BKc, BN, NT, FULL, B16>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
             }
         };
         auto store_ab = [&](int buf, const Regs& r) {
@@ -372,7 +428,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     else mainloop(std::false_type{});
     // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
-    x6_epilogue<TM, TN, ABL>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
+    x6_epilogue<TM, TN, ABL, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
 }
 
 // bm, bn, waves, workgroups per CU; configs 3 and 4 (128 KB of LDS) are built for f16x3 only
@@ -431,6 +487,19 @@ static void launch_x6_t(int cfg, int abl, dim3 grid, hipStream_t s, const GemmAr
     }
 }
 
+// bf16 storage (PREC 2): st = bit 0 A, bit 1 B, bit 2 C; the combinations EA_GNN uses
+static void launch_x6_bf16_storage(int ta, int tb, int cfg, int st, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if (ta == 0 && tb == 1 && st == 7) launch_x6_a<2, 0, 1, 16 + 7>(cfg, grid, s, g);        // (gemm_b16.hip when K % 64 == 0)
+    else if (ta == 0 && tb == 1 && st == 3) launch_x6_a<2, 0, 1, 16 + 3>(cfg, grid, s, g);
+    else if (ta == 0 && tb == 1 && st == 5) launch_x6_a<2, 0, 1, 16 + 5>(cfg, grid, s, g);   // edge fwd / dgrad
+    else if (ta == 0 && tb == 1 && st == 4) launch_x6_a<2, 0, 1, 16 + 4>(cfg, grid, s, g);   // f32 in, bf16 out
+    else if (ta == 0 && tb == 1 && st == 1) launch_x6_a<2, 0, 1, 16 + 1>(cfg, grid, s, g);   // bf16 in, f32 out
+    else if (ta == 1 && tb == 0 && st == 3) launch_x6_a<2, 1, 0, 16 + 3>(cfg, grid, s, g);   // wgrad g^T e
+    else if (ta == 1 && tb == 0 && st == 1) launch_x6_a<2, 1, 0, 16 + 1>(cfg, grid, s, g);
+    else if (ta == 1 && tb == 0 && st == 2) launch_x6_a<2, 1, 0, 16 + 2>(cfg, grid, s, g);
+    else launch_x6_a<2, 0, 1, 16 + 5>(cfg, grid, s, g);   // (not reached: bgnn_gemm_bf16 validates st)
+}
+
 template <int PREC>
 static void launch_prec(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if (ta == 0 && tb == 0) launch_x6_t<PREC, 0, 0>(cfg, abl, grid, s, g);
@@ -440,7 +509,8 @@ static void launch_prec(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t
 }
 
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    if (prec == 2) launch_prec<2>(ta, tb, cfg, 0, grid, s, g);
+    if (prec == 2 && g.st != 0) launch_x6_bf16_storage(ta, tb, cfg, g.st, grid, s, g);
+    else if (prec == 2) launch_prec<2>(ta, tb, cfg, 0, grid, s, g);
     else if (prec == 1) launch_prec<1>(ta, tb, cfg, abl, grid, s, g);
     else launch_prec<0>(ta, tb, cfg > 2 ? 1 : cfg, abl, grid, s, g);
 }

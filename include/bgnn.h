@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 5
+#define BGNN_ABI_VERSION 6
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -270,6 +270,35 @@ int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
  * max |dh|). nrm is bgnn_sage_fwd's row-norm output. */
 int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm, int64_t n_rows, int32_t H,
                     float* dh, int64_t lddh, float* partial_db, float* amax, void* stream);
+
+/* bf16 storage of EA_GNN's per-edge activations (ABI 5; BASELINE configs[4], bf16):
+ * bgnn_gemm_bf16: C = act(alpha op(A) op(B) + beta C + bias) on the bf16-operand GEMM family
+ *   (operands rounded to bf16, one MFMA product, f32 accumulation) with `storage` bits 0 / 1 / 2
+ *   = A / B / C stored as bf16 (ld in elements of the stored type; a bf16 C needs beta 0 and is
+ *   rounded to nearest even). Built: storage 0; ta 0 tb 1 with 1, 3, 4, 5, 7; ta 1 tb 0 with 1, 2, 3.
+ *   ta 0 tb 1 with A and B both bf16 (storage 3 / 7), K % 64 == 0, alpha 1, beta 0: the LDS-DMA
+ *   bf16 kernel (ABI 6, gemm_b16.hip), bit-identical to the register-staged one.
+ * bgnn_gemm_gather_add_bf16: bgnn_gemm_gather_add (C = A B^T, bf16 operands) with storage
+ *   0/1/3/4/5/7 (B bf16 = the weight rounded once by the caller; ABI 6 takes B as const void*).
+ * bgnn_gemm_b16_variant (ABI 6, measurement): -1 = the bf16-stored NT products on the
+ *   register-staged kernel instead; 0 = per call (default: persistent LDS-DMA kernel for a bf16 C
+ *   or a gathered epilogue, else one 256x256 tile per workgroup); 1-7 = fixed forms (A/B).
+ * bgnn_add_dropout_bf16: bgnn_add_dropout over bf16 (same mask; f32 sum, one rounding).
+ * bgnn_segment_sum_bf16: out[r] = sum (mean: / max(deg, 1)) of the bf16 rows x[col[p]], p in
+ *   [rowptr[r], rowptr[r+1]), in CSR order, f32 result (H % 8 == 0, H <= 512). */
+int bgnn_gemm_bf16(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                   const void* A, int64_t lda, const void* B, int64_t ldb, float beta, void* C, int64_t ldc,
+                   const float* bias, int32_t relu, int32_t storage, void* ws, size_t ws_bytes, void* stream);
+int bgnn_gemm_gather_add_bf16(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                              int64_t ldb, void* C, int64_t ldc, const float* bias, int32_t relu,
+                              const float* add0, const int64_t* idx0, int64_t ld0, const float* add1,
+                              const int64_t* idx1, int64_t ld1, int32_t storage, void* ws, size_t ws_bytes,
+                              void* stream);
+int bgnn_gemm_b16_variant(int32_t variant);
+int bgnn_add_dropout_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
+                          void* stream);
+int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
+                          int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream);
 
 /* Pre-split f16x3 operands (ABI 5). An f32 matrix x [rows, cols] (ld ldx) as its two f16 pieces,
  * the split the f16x3 GEMM does internally: with s = 2^k from *amax (max|x|, or any bound within

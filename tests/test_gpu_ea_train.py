@@ -17,11 +17,12 @@ from oracle import buckgnn_ref as R
 pytestmark = pytest.mark.gpu
 
 
-def run_both(dev, hidden, lr, steps, bf16, n=12, graphs=4):
+def run_both(dev, hidden, lr, steps, bf16, n=12, graphs=4, oracle_dev="cpu"):
     b = S.make_batch(n, graphs)
     torch.manual_seed(0)
     m = bgnn.BuckGNN(16, 5, hidden_channels=hidden, num_layers=6, dropout_rate=0.0, model_name="EA_GNN")
-    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    sd = {k: v.detach().clone().to(oracle_dev, torch.float64 if oracle_dev != "cpu" and v.is_floating_point()
+                                   else v.dtype) for k, v in m.state_dict().items()}
     model = m.to(dev).train()
     model.ea_bf16 = bf16
     opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-8)
@@ -33,11 +34,14 @@ def run_both(dev, hidden, lr, steps, bf16, n=12, graphs=4):
             v.requires_grad_(True)
             params.append(v)
     opt_c = torch.optim.Adam(params, lr=lr, weight_decay=1e-8)
+    bo = b.to(oracle_dev) if oracle_dev != "cpu" else b
     ours, ref = [], []
     for _ in range(steps):
         ours.append(float(bgnn.train_step(model, bd, opt, crit, norm)))
-        pred = R.ea_forward(sd, b.x, b.edge_index, b.edge_attr, b.batch, True, 0.0)
-        loss = R.relative_error_loss(norm.denormalize_eigenvalue(pred), norm.denormalize_eigenvalue(b.y))
+        pred = R.ea_forward(sd, bo.x.to(params[0].dtype), bo.edge_index, bo.edge_attr.to(params[0].dtype), bo.batch,
+                            True, 0.0)
+        loss = R.relative_error_loss(norm.denormalize_eigenvalue(pred),
+                                     norm.denormalize_eigenvalue(bo.y.to(params[0].dtype)))
         opt_c.zero_grad(set_to_none=True)
         loss.backward()
         opt_c.step()
@@ -63,3 +67,15 @@ def test_ea_h512_lr1e2_diverges_in_the_reference_too(dev):
     assert ours[0] == pytest.approx(ref[0], rel=1e-3)
     assert max(ref[1:]) > 10 * ref[0], ref
     assert max(ours[1:]) > 10 * ours[0], ours
+
+
+@pytest.mark.parametrize("bf16,rtol", [(False, 1e-3), (True, 5e-2)], ids=["f32", "bf16"])
+def test_ea_h512_cfg2_meshes_adam_steps_follow_oracle(dev, bf16, rtol):
+    """h = 512 on 4 cfg2-sized meshes (4 x 71x71 with virtual edges: E = 178,968 edges, the
+    production per-edge GEMM shapes and, with --bf16, the bf16 edge storage), 3 Adam steps at
+    lr 1e-3: the loss follows the fp64 oracle (run on the device: ~40 GB of fp64 activations)
+    step by step, and falls."""
+    ours, ref = run_both(dev, 512, 1e-3, 3, bf16, n=71, graphs=4, oracle_dev=dev)
+    for s, (a, r) in enumerate(zip(ours, ref)):
+        assert a == pytest.approx(r, rel=rtol), (s, ours, ref)
+    assert ref[-1] < ref[0] and ours[-1] < ours[0]

@@ -134,6 +134,7 @@ def test_ea_fused_gather_epilogue_matches_two_step(dev, monkeypatch, bf16):
     from bgnn import ea
     from bgnn import synthetic as S
     from bgnn.buckgnn import GraphNetBlock
+    monkeypatch.setattr(ea, "BF16_STORAGE", False)   # (both forms store the activations in f32)
     b = S.make_batch(30, 3).to(dev)
     torch.manual_seed(1)
     blk = GraphNetBlock(128).to(dev)

@@ -1,0 +1,107 @@
+#!/usr/bin/env python
+"""Per-launch time of the bf16-operand GEMM with each bf16 storage combination on EA_GNN's
+per-edge shapes (default E = 715,872 = cfg2-sized edges; H = 512): NT (edge Linear fwd / dgrad)
+and TN (wgrad g^T e), plus the bf16-stored NT product on the LDS-DMA kernel (gemm_b16.hip,
+variants 0 / 1) against the register-staged kernel (variant -1), checked bit-identical.
+Interleaved launches, HIP events on the launch stream, medians, cache flushed before each launch.
+
+    python tools/bf16_storage_ab.py [E] [R]
+"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+from bgnn import _lib, fused  # noqa: E402
+
+E = int(sys.argv[1]) if len(sys.argv) > 1 else 715872
+R = int(sys.argv[2]) if len(sys.argv) > 2 else 9
+H = 512
+dev = torch.device("cuda", 0)
+flush = torch.empty(128 * 1024 * 1024, dtype=torch.float32, device=dev)
+torch.manual_seed(0)
+x32 = torch.randn(E, H, device=dev)
+x16 = x32.to(torch.bfloat16)
+g32 = torch.randn(E, H, device=dev)
+g16 = g32.to(torch.bfloat16)
+W = torch.randn(H, H, device=dev) / H ** 0.5
+W16 = W.to(torch.bfloat16)
+bias = torch.randn(H, device=dev)
+
+
+def v(k, fn):
+    def run():
+        _lib.call("bgnn_gemm_b16_variant", k)
+        try:
+            return fn()
+        finally:
+            _lib.call("bgnn_gemm_b16_variant", 0)
+    return run
+
+
+NN = 80656
+P1 = torch.randn(NN, H, device=dev)
+P2 = torch.randn(NN, H, device=dev)
+i1 = torch.sort(torch.randint(0, NN, (E,), device=dev))[0]
+i2 = torch.randint(0, NN, (E,), device=dev)
+
+
+def gather7():
+    out = torch.empty(E, H, dtype=torch.bfloat16, device=dev)
+    _lib.call("bgnn_gemm_gather_add_bf16", E, H, H, x16.data_ptr(), H, W16.data_ptr(), H, out.data_ptr(), H,
+              bias.data_ptr(), 1, P1.data_ptr(), i1.data_ptr(), H, P2.data_ptr(), i2.data_ptr(), H, 7, None, 0,
+              torch.cuda.current_stream().cuda_stream)
+    return out
+
+
+st7 = lambda: fused.gemm_bf16(x16, W16, False, True, out_bf16=True, bias=bias, relu=True)   # noqa: E731
+st3 = lambda: fused.gemm_bf16(x16, W16, False, True, bias=bias, relu=True)                  # noqa: E731
+cases = {
+    "NT st0 (f32 A, f32 C)": lambda: fused.gemm_bf16(x32, W, False, True),
+    "NT st4 (f32 A, bf16 C)": lambda: fused.gemm_bf16(x32, W, False, True, out_bf16=True),
+    "NT st5 x6 (bf16 A, bf16 C)": v(-1, lambda: fused.gemm_bf16(x16, W, False, True, out_bf16=True)),
+    "NT st7 x6": v(-1, st7),
+    "NT st7 b16 v0": v(0, st7),
+    "NT st7 b16 v1": v(1, st7),
+    "NT st7 b16 v2": v(2, st7),
+    "NT st7 b16 v3": v(3, st7),
+    "NT st7 b16 v6 (persistent)": v(6, st7),
+    "NT st7 b16 v4 (no epi)": v(4, st7),
+    "NT st7 b16 v5 (no epi)": v(5, st7),
+    "NT st3 x6 (f32 C)": v(-1, st3),
+    "NT st3 b16 v0": v(0, st3),
+    "NT st3 b16 v2": v(2, st3),
+    "NT st3 b16 v6": v(6, st3),
+    "gather st7 x6": v(-1, lambda: gather7()),
+    "gather st7 b16 v0": v(0, lambda: gather7()),
+    "gather st7 b16 v2": v(2, lambda: gather7()),
+    "gather st7 b16 v6": v(6, lambda: gather7()),
+    "TN st0 (f32 g, f32 e)": lambda: fused.gemm_bf16(g32, x32, True, False),
+    "TN st3 (bf16 g, bf16 e)": lambda: fused.gemm_bf16(g16, x16, True, False),
+}
+ref7, ref3 = cases["NT st7 x6"](), cases["NT st3 x6 (f32 C)"]()
+for k in ("NT st7 b16 v0", "NT st7 b16 v1", "NT st7 b16 v2", "NT st7 b16 v3", "NT st7 b16 v6 (persistent)"):
+    print(f"{k:28s} bit-identical to x6: {torch.equal(cases[k](), ref7)}", flush=True)
+print(f"{'NT st3 b16 v0':28s} bit-identical to x6: {torch.equal(cases['NT st3 b16 v0'](), ref3)}", flush=True)
+print(f"{'NT st3 b16 v6':28s} bit-identical to x6: {torch.equal(cases['NT st3 b16 v6'](), ref3)}", flush=True)
+refg = cases["gather st7 x6"]()
+for k in ("gather st7 b16 v0", "gather st7 b16 v2", "gather st7 b16 v6"):
+    print(f"{k:28s} bit-identical to x6: {torch.equal(cases[k](), refg)}", flush=True)
+del ref7, ref3, refg
+ts = {k: [] for k in cases}
+for i in range(R):
+    for k, fn in cases.items():
+        flush.fill_(float(i))
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts[k].append(a.elapsed_time(b) * 1e3)
+flop = 2.0 * E * H * H
+for k, t in ts.items():
+    t.sort()
+    med = t[len(t) // 2]
+    print(f"{k:28s} {med:9.1f} us  {flop / med * 1e-6:7.1f} TF/s", flush=True)
