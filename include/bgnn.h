@@ -79,6 +79,10 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_GROUP_U 10      /* row-group kernel: source rows per gather batch, 8 or 16    */
 #define BGNN_TUNE_GROUP_ZR_EARLY 11 /* row-group SAGE epilogue: z_r loads issued before the gathers
                                     (1) or after them (0)                                    */
+#define BGNN_TUNE_SEG_COLSLICE 12   /* row-group kernel, plain epilogue (transpose aggregation),
+                                    H = 256 / 512: 1 = every XCD reduces one 128-column slice of
+                                    its row region (a graph's slice of rows fits that XCD's L2),
+                                    0 = whole rows                                           */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);

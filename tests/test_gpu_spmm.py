@@ -279,3 +279,44 @@ def test_group_kernel_knobs_bit_identical(dev, knobs, graph):
         assert torch.equal(a, b)
     for r in ("sum", "mean"):
         assert torch.equal(ref[3][r][0], got[3][r][0]) and torch.equal(ref[3][r][1], got[3][r][1]), r
+
+
+@pytest.mark.parametrize("cs", [1, 2], ids=["u16", "u8"])
+@pytest.mark.parametrize("H", [512, 256])
+@pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
+def test_column_slice_kernel_bit_identical(dev, cs, H, graph):
+    """BGNN_TUNE_SEG_COLSLICE (per-XCD 128-column slices of the row-group kernel, plain epilogue)
+    changes only which XCD reads which columns: the plain aggregations (sum, mean) and their
+    transposes (the training step's bgnn_spmm_bwd, sum and mean) are bit-identical to the
+    whole-row kernel, and the folded max|out| is the same."""
+    from bgnn import _lib, ops
+    ei, n = _variant_graph(dev, graph)
+    g = Graph.build(ei, n)
+    assert g.fwd.groups is not None and g.bwd.groups is not None
+    torch.manual_seed(11)
+    x = torch.randn(n, H, device=dev)
+    gy = torch.randn(n, H, device=dev)
+
+    def run():
+        red = {}
+        for r in ("sum", "mean"):
+            xx = x.clone().requires_grad_(True)
+            y = bgnn.aggregate(xx, g, r)
+            y.backward(gy)
+            red[r] = (y.detach(), xx.grad)
+        amax = torch.zeros(1, device=dev)
+        gx = ops.spmm_bwd(g.bwd, g.perm_t, g.fwd.rowptr, gy, 0, None, n, amax=amax)
+        return red, gx, amax
+
+    ref = run()
+    old = _lib.query("bgnn_get_tuning", 12)
+    try:
+        _lib.call("bgnn_set_tuning", 12, cs)
+        got = run()
+    finally:
+        _lib.call("bgnn_set_tuning", 12, old)
+    for r in ("sum", "mean"):
+        assert torch.equal(ref[0][r][0], got[0][r][0]), (r, "fwd")
+        assert torch.equal(ref[0][r][1], got[0][r][1]), (r, "bwd")
+    assert torch.equal(ref[1], got[1])
+    assert ref[2].item() == got[2].item() == ref[1].abs().max().item()
