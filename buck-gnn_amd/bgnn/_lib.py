@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lock = threading.Lock()
 _lib = None
@@ -81,6 +81,8 @@ SIGNATURES = {
     "bgnn_reduce_partials": (c_i32, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p]),
     "bgnn_linear_bwd_prep_slots": (c_i32, []),
     "bgnn_linear_bwd_prep": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
+    "bgnn_linear_bwd_prep_bf16": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p]),
+    "bgnn_absmax_items_f32": (c_i32, [c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p]),
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
                                    c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p]),
     "bgnn_l2norm_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p]),

@@ -115,9 +115,12 @@ class _LinearGatherReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         e, W, out = ctx.saved_tensors
-        if ctx.storage:   # bf16 storage: mask + f32 bias sum in torch, GEMMs on bgnn_gemm_bf16
-            g = torch.ops.aten.threshold_backward(g.contiguous(), out, 0.0)
-            db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
+        if ctx.storage:   # bf16 storage: mask + f32 bias sum in one pass, GEMMs on bgnn_gemm_bf16
+            if g.dtype == torch.bfloat16 and fused.BF16_PREP:
+                g, db = fused.relu_bias_grad_bf16(g, out, ctx.has_bias)
+            else:
+                g = torch.ops.aten.threshold_backward(g.contiguous(), out, 0.0)
+                db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
             de = (gemm_bf16(g, W.t().contiguous(), False, True, out_bf16=e.dtype == torch.bfloat16)
                   if ctx.needs_input_grad[0] else None)
             dW = gemm_bf16(g, e, True, False)

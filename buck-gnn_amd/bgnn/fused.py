@@ -47,6 +47,12 @@ FOLD_WEIGHTS_TORCH = False
 # (bgnn_gemm_f32_dropadd) instead of reading a skip gradient bgnn_sage_bwd_rows wrote
 DGRAD_DROPADD = True
 
+# bf16-stored Linear backward (EA_GNN's bf16 configuration): ReLU mask + f32 bias-gradient sums
+# in one bgnn pass (bgnn_linear_bwd_prep_bf16) instead of torch threshold_backward + sum (A/B switch)
+BF16_PREP = True
+# per-layer weight maxima of a SAGE layer loop in one launch (bgnn_absmax_items_f32)
+ABSMAX_ITEMS = True
+
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
 TIMERS = None
@@ -224,10 +230,13 @@ class LinearBf16Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, weight, y = ctx.saved_tensors
-        g = g.contiguous()
-        if ctx.relu:
-            g = torch.ops.aten.threshold_backward(g, y, 0.0)
-        db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
+        if g.dtype == torch.bfloat16 and BF16_PREP:
+            g, db = relu_bias_grad_bf16(g, y if ctx.relu else None, ctx.has_bias)
+        else:
+            g = g.contiguous()
+            if ctx.relu:
+                g = torch.ops.aten.threshold_backward(g, y, 0.0)
+            db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
         dx = None
         if ctx.needs_input_grad[0]:
             dx = gemm_bf16(g, weight.t().contiguous(), False, True, out_bf16=x.dtype == torch.bfloat16)
@@ -255,6 +264,34 @@ def mlp_bf16(seq: torch.nn.Sequential, x: torch.Tensor, out_bf16: bool = True):
             x = m(x)
             i += 1
     return x
+
+
+def relu_bias_grad_bf16(g: torch.Tensor, y=None, bias: bool = True):
+    """(g', db) for the backward of act(x W^T + b) with bf16 g (and bf16 ReLU output y): g' = g
+    masked by y > 0 (bf16; g itself when y is None), db = f32 column sums of g' (None when bias is
+    False). One pass over g (bgnn_linear_bwd_prep_bf16) instead of torch's threshold_backward plus
+    a float32 sum, each of which torch splits in two launches at E x 512 bf16 (> 2^31 bytes)."""
+    g = g.contiguous()
+    C = g.size(1)
+    ok = (C % 8 == 0 and 8 <= C <= 2048 and 256 % (C // 8) == 0 and g.data_ptr() % 16 == 0
+          and (y is None or (y.dtype == torch.bfloat16 and y.is_contiguous() and y.data_ptr() % 16 == 0)))
+    if not ok:
+        if y is not None:
+            g = torch.ops.aten.threshold_backward(g, y, 0.0)
+        return g, (torch.sum(g, 0, dtype=torch.float32) if bias else None)
+    if y is None and not bias:
+        return g, None
+    gm = torch.empty_like(g) if y is not None else g
+    slots = _lib.query("bgnn_linear_bwd_prep_slots")
+    part = torch.empty(slots, 2, C, dtype=torch.float32, device=g.device)
+    s = _stream()
+    _lib.call("bgnn_linear_bwd_prep_bf16", g.data_ptr(), None if y is None else y.data_ptr(), g.size(0), C,
+              gm.data_ptr() if y is not None else None, part.data_ptr(), s)
+    db = None
+    if bias:
+        db = torch.empty(C, dtype=torch.float32, device=g.device)
+        _lib.call("bgnn_reduce_partials", part.data_ptr(), slots, C, db.data_ptr(), None, 0, s)
+    return gm, db
 
 
 def relu_bias_grad(g: torch.Tensor, y=None, bias: bool = True):
@@ -659,10 +696,15 @@ def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
     with torch.no_grad():   # operands only: the layers return the weight gradients themselves
         W = torch.cat([t for pr in pairs for t in pr], 0).view(L, 2 * H, H)
         Wt = W.transpose(1, 2).contiguous() if DGRAD_WT else None
-        # max|W| per layer with bgnn_absmax (torch's dim=(1, 2) max-reduction took 128 us here)
-        for i, f in enumerate(fill_amax):
-            if f:
-                absmax(W[i], amax_bufs[i, 0:1], accumulate=True)
+        # max|W| per layer with bgnn_absmax (torch's dim=(1, 2) max-reduction took 128 us here), all
+        # layers in one launch when every layer takes it
+        if ABSMAX_ITEMS and all(fill_amax) and amax_bufs.is_contiguous() and H % 4 == 0:
+            _lib.call("bgnn_absmax_items_f32", W.data_ptr(), L, 2 * H * H, 2 * H, H, H, amax_bufs.data_ptr(),
+                      amax_bufs.stride(0), _stream())
+        else:
+            for i, f in enumerate(fill_amax):
+                if f:
+                    absmax(W[i], amax_bufs[i, 0:1], accumulate=True)
     return [(W[i], Wt[i] if Wt is not None else None) for i in range(L)]
 
 

@@ -553,6 +553,34 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ P, int
     }
 }
 
+// max |W_i| of n items of equal shape (rows x cols, ld; item i at P + i * item_stride) in one
+// launch: grid.y = item, each block of an item as in k_absmax (the per-layer weight maxima of a
+// SAGE loop, bgnn.fused.prepare_weights); out[i * out_stride] = max(out[.], max |W_i|).
+__global__ __launch_bounds__(256) void k_absmax_items(const float* __restrict__ P, int64_t item_stride, int64_t rows,
+                                                      int64_t cols4, int64_t ld, int tpr, uint32_t* __restrict__ out,
+                                                      int64_t out_stride) {
+    const float* Pi = P + (int64_t)blockIdx.y * item_stride;
+    const int rpi = 256 / tpr;
+    const int tc = threadIdx.x % tpr;
+    uint32_t m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * rpi + threadIdx.x / tpr; r < rows; r += (int64_t)gridDim.x * rpi) {
+        const float4* row = reinterpret_cast<const float4*>(Pi + r * ld);
+        for (int64_t c = tc; c < cols4; c += tpr) {
+            const float4 v = row[c];
+            m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                           max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, kWave));
+    __shared__ uint32_t red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (m) atomicMax(out + (int64_t)blockIdx.y * out_stride, m);
+    }
+}
+
 void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64_t blk, int64_t pstride,
                    float* out, hipStream_t s) {
     const bool vec = blk == 0 && cols % 4 == 0 && ld % 4 == 0 && (((uintptr_t)P & 15) == 0);
@@ -569,3 +597,24 @@ void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64
 }
 
 }  // namespace bgnn
+
+using namespace bgnn;
+
+extern "C" int bgnn_absmax_items_f32(const float* x, int32_t n_items, int64_t item_stride, int64_t rows, int64_t cols,
+                                     int64_t ld, float* out, int64_t out_stride, void* stream) {
+    BGNN_REQUIRE(x && out && n_items >= 0 && rows >= 0 && cols >= 0 && ld >= cols, "absmax_items: bad args");
+    BGNN_REQUIRE(cols % 4 == 0 && ld % 4 == 0 && item_stride % 4 == 0 && (((uintptr_t)x & 15) == 0),
+                 "absmax_items: cols, ld and item_stride must be multiples of 4 and x 16-B aligned");
+    BGNN_REQUIRE(n_items <= 65535, "absmax_items: at most 65535 items");
+    if (n_items == 0 || rows == 0 || cols == 0) return BGNN_OK;
+    const int64_t cols4 = cols / 4;
+    int tpr = 1;
+    while (tpr < 256 && tpr < cols4) tpr <<= 1;
+    const int64_t rpi = 256 / tpr;
+    int64_t blocks = (rows + rpi - 1) / rpi;
+    if (blocks > 512) blocks = 512;
+    hipLaunchKernelGGL(k_absmax_items, dim3((unsigned)blocks, (unsigned)n_items), dim3(256), 0, as_stream(stream), x,
+                       item_stride, rows, cols4, ld, tpr, reinterpret_cast<uint32_t*>(out), out_stride);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}

@@ -465,6 +465,72 @@ __global__ __launch_bounds__(256) void k_linear_bwd_prep(const float4* __restric
     }
 }
 
+// bf16 form (EA_GNN's bf16 configuration, bgnn.fused.LinearBf16Fn / bgnn.ea's gathered Linear):
+// g, y, g_out bf16 [N, C] (8 elements per 16-B access, C8 = C / 8 threads per row), column sums
+// in f32 (each bf16 value is exact in f32), no max|g| (the bf16 GEMMs need no operand scale).
+// Replaces torch's threshold_backward + sum(g, 0, dtype=float32): one pass instead of three.
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+__global__ __launch_bounds__(256) void k_linear_bwd_prep_bf16(const uint4* __restrict__ g, const uint4* __restrict__ y,
+                                                              int64_t N, int C8, uint4* __restrict__ gout,
+                                                              float* __restrict__ part) {
+    __shared__ float red[256][8];
+    const int t = threadIdx.x;
+    const int rpi = 256 / C8;
+    const int c8 = t % C8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int64_t r = (int64_t)blockIdx.x * rpi + t / C8; r < N; r += (int64_t)gridDim.x * rpi) {
+        uint4 v = g[r * C8 + c8];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        if (y) {
+            const uint4 q = y[r * C8 + c8];
+            const uint32_t qy[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t lo = bf16_lo(qy[k]) > 0.f ? 0x0000ffffu : 0u;
+                const uint32_t hi = bf16_hi(qy[k]) > 0.f ? 0xffff0000u : 0u;
+                w[k] &= lo | hi;
+            }
+            if (gout) gout[r * C8 + c8] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            acc[2 * k] += bf16_lo(w[k]);
+            acc[2 * k + 1] += bf16_hi(w[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[t][k] = acc[k];
+    __syncthreads();
+    if (t < C8) {
+        float s8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s8[k] = red[t][k];
+        for (int q = 1; q < rpi; ++q)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s8[k] += red[t + q * C8][k];
+        float4* dst = reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * (8 * C8)) + 2 * t;
+        dst[0] = make_float4(s8[0], s8[1], s8[2], s8[3]);
+        dst[1] = make_float4(s8[4], s8[5], s8[6], s8[7]);
+    }
+}
+
+extern "C" int bgnn_linear_bwd_prep_bf16(const void* g, const void* y, int64_t N, int32_t C, void* g_out,
+                                         float* partial, void* stream) {
+    BGNN_REQUIRE(g && partial && N >= 0, "linear_bwd_prep_bf16: null pointer or negative size");
+    BGNN_REQUIRE(y == nullptr || g_out != nullptr, "linear_bwd_prep_bf16: a ReLU mask needs g_out");
+    BGNN_REQUIRE(C >= 8 && C <= 2048 && C % 8 == 0 && (256 % (C / 8)) == 0,
+                 "linear_bwd_prep_bf16: C = %d must be 8 * a power of two <= 2048", C);
+    BGNN_REQUIRE((((uintptr_t)g | (uintptr_t)(g_out ? g_out : g) | (uintptr_t)partial | (uintptr_t)(y ? y : g)) & 15) == 0,
+                 "linear_bwd_prep_bf16: pointers must be 16-B aligned");
+    hipStream_t s = as_stream(stream);
+    hipLaunchKernelGGL(k_linear_bwd_prep_bf16, dim3(kPrepBlocks), dim3(256), 0, s, reinterpret_cast<const uint4*>(g),
+                       reinterpret_cast<const uint4*>(y), N, C / 8, reinterpret_cast<uint4*>(g_out), partial);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
 extern "C" int32_t bgnn_linear_bwd_prep_slots(void) { return kPrepBlocks; }
 
 extern "C" int bgnn_linear_bwd_prep(const float* g, const float* y, int64_t N, int32_t C, float* g_out,

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 6
+#define BGNN_ABI_VERSION 7
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -243,6 +243,12 @@ int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, cons
 int32_t bgnn_linear_bwd_prep_slots(void);
 int bgnn_linear_bwd_prep(const float* g, const float* y, int64_t N, int32_t C, float* g_out,
                          float* partial, float* amax, void* stream);
+/* bf16 form (ABI 7; EA_GNN's bf16 edge activations, replaces torch's threshold_backward +
+ * sum(g, 0, dtype=float32)): g, y, g_out bf16 [N, C] (C = 8 * a power of two <= 2048, 16-B aligned);
+ * g_out = y > 0 ? g : 0 (y NULL: no mask and g_out may be NULL), f32 column sums of g_out into
+ * partial[bgnn_linear_bwd_prep_slots()][2][C] (first half of each slot, for bgnn_reduce_partials). */
+int bgnn_linear_bwd_prep_bf16(const void* g, const void* y, int64_t N, int32_t C, void* g_out,
+                              float* partial, void* stream);
 int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
                          float* out0, float* out1, int32_t accumulate, void* stream);
 
@@ -396,6 +402,11 @@ int bgnn_gemm_gather_add(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N,
 /* *out = max(accumulate ? *out : 0, max |x|) over a row-major [rows, cols] matrix (ld). */
 int bgnn_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* out,
                     int32_t accumulate, void* stream);
+/* ABI 7: out[i * out_stride] = max(out[i * out_stride], max |x_i|) for n_items matrices of equal
+ * shape [rows, cols] (ld), item i at x + i * item_stride (cols, ld, item_stride multiples of 4,
+ * x 16-B aligned), in one launch (the per-layer weight maxima of a SAGE layer loop). */
+int bgnn_absmax_items_f32(const float* x, int32_t n_items, int64_t item_stride, int64_t rows, int64_t cols,
+                          int64_t ld, float* out, int64_t out_stride, void* stream);
 int bgnn_gemm_f32_planes(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                          float alpha, const float* A, int64_t lda, int64_t a_blk, int64_t a_pstride,
                          const float* B, int64_t ldb, float beta, float* C, int64_t ldc,

@@ -166,3 +166,40 @@ def test_b16_weight_rounding_matches_in_tile_rounding(dev, b16_variant):
     finally:
         fused.B16_WEIGHTS = True
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("shape", [(3001, 512), (777, 64), (5, 2048)])
+def test_linear_bwd_prep_bf16_matches_torch(dev, relu, shape):
+    """bgnn_linear_bwd_prep_bf16 (fused.relu_bias_grad_bf16): the ReLU-masked gradient is
+    bit-identical to torch's threshold_backward on the same bf16 data (zeros, negative zeros and
+    exact-zero outputs included) and the f32 bias-gradient sums match an fp64 sum of it."""
+    torch.manual_seed(21)
+    N, C = shape
+    g = torch.randn(N, C, device=dev).to(torch.bfloat16)
+    y = torch.randn(N, C, device=dev).clamp_min(0).to(torch.bfloat16)   # a ReLU output: many exact zeros
+    y[::7, ::3] = -0.0
+    ref_g = torch.ops.aten.threshold_backward(g, y, 0.0) if relu else g
+    got_g, db = fused.relu_bias_grad_bf16(g, y if relu else None, True)
+    assert got_g.dtype == torch.bfloat16
+    assert torch.equal(got_g, ref_g)
+    ref_db = ref_g.double().sum(0)
+    torch.testing.assert_close(db.double(), ref_db, rtol=1e-5, atol=1e-4 * (1 + ref_db.abs().max().item()) * 1e-2)
+    g2, none = fused.relu_bias_grad_bf16(g, y if relu else None, False)
+    assert none is None and torch.equal(g2, ref_g)
+
+
+def test_absmax_items_matches_per_item(dev):
+    """bgnn_absmax_items_f32 (all layers' max|[W_l;W_r]| of a SAGE loop in one launch) folds the
+    same maxima into the strided slots as one bgnn_absmax per item."""
+    torch.manual_seed(22)
+    L, H = 6, 512
+    W = torch.randn(L, 2 * H, H, device=dev) * torch.logspace(-3, 3, L, device=dev).view(L, 1, 1)
+    bufs = torch.zeros(L, 3, device=dev)
+    bufs[2, 0] = 1e9   # accumulate: an existing larger value stays
+    _lib.call("bgnn_absmax_items_f32", W.data_ptr(), L, 2 * H * H, 2 * H, H, H, bufs.data_ptr(), 3,
+              torch.cuda.current_stream().cuda_stream)
+    want = W.abs().amax(dim=(1, 2))
+    want[2] = 1e9
+    assert torch.equal(bufs[:, 0], want)
+    assert torch.equal(bufs[:, 1:], torch.zeros(L, 2, device=dev))
