@@ -82,7 +82,7 @@ __device__ __forceinline__ void b16_mma(const uint4* __restrict__ S, floatx16 (&
 // C: 8 columns per lane (4 lanes per 64-B row segment; x6_epilogue stores 8 B). Per element the
 // arithmetic and its order are x6_epilogue's: acc, + bias, + ga0[gi0[row]], + ga1[gi1[row]],
 // ReLU, one bf16 rounding (RNE). Edge blocks fall back to x6_epilogue's element-guarded path.
-template <int TM, int TN, bool C16>
+template <int TM, int TN, bool C16, bool WIDE = false>
 __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
                                              int64_t c0, int lane, float* __restrict__ stage) {
     constexpr int CPL = C16 ? 8 : 4;        // columns per lane
@@ -96,6 +96,78 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (
                       (!g.bias || (((uintptr_t)g.bias & 15) == 0)) && r0 + TM * 32 <= g.M && c0 + TN * 32 <= g.N;
     if (!fast) {
         x6_epilogue<TM, TN, 0, C16>(g, acc, r0, c0, c0, 0, lane, 1.f, 1.f, stage);
+        return;
+    }
+    if constexpr (C16 && TN % 2 == 0 && WIDE) {
+        // bf16 C in whole 128-B lines: two adjacent 32-column blocks (64 bf16 columns) of 32 rows
+        // staged together ([32][68] f32: the row pad keeps the two half-waves' ds_write_b32 rows
+        // on different banks), then 8 lanes x 16 B per row -- a 32-column block alone is a 64-B
+        // half line per row, and half-line non-temporal stores cost the HBM side about twice
+        // (tools/bf16_storage_ab.py: epilogue 835 of 2161 us at E = 2.86M). Same per-element
+        // arithmetic and order as below.
+        constexpr int LDW = 68;
+        const int rq8 = lane >> 3, cq8 = (lane & 7) * 8;
+#pragma unroll
+        for (int j = 0; j < TN; j += 2) {
+            const int64_t col = c0 + j * 32 + cq8;
+            float bv[8];
+#pragma unroll
+            for (int k = 0; k < 8; k += 4) {
+                const float4 t = g.bias ? *reinterpret_cast<const float4*>(g.bias + col + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                bv[k] = t.x; bv[k + 1] = t.y; bv[k + 2] = t.z; bv[k + 3] = t.w;
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        stage[((r & 3) + 8 * (r >> 2) + 4 * lh) * LDW + h * 32 + li] = acc[i][j + h][r];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = q * 8 + rq8;
+                    const int64_t row = r0 + i * 32 + rr;
+                    float e[8], x0[8], x1[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k += 4) {
+                        const float4 sv = *reinterpret_cast<const float4*>(stage + rr * LDW + cq8 + k);
+                        e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
+                    }
+                    if (g.ga0) {
+                        const float* s0 = g.ga0 + g.gi0[row] * g.ldg0 + col;
+#pragma unroll
+                        for (int k = 0; k < 8; k += 4) {
+                            const float4 t = *reinterpret_cast<const float4*>(s0 + k);
+                            x0[k] = t.x; x0[k + 1] = t.y; x0[k + 2] = t.z; x0[k + 3] = t.w;
+                        }
+                        if (g.ga1) {
+                            const float* s1 = g.ga1 + g.gi1[row] * g.ldg1 + col;
+#pragma unroll
+                            for (int k = 0; k < 8; k += 4) {
+                                const float4 t = *reinterpret_cast<const float4*>(s1 + k);
+                                x1[k] = t.x; x1[k + 1] = t.y; x1[k + 2] = t.z; x1[k + 3] = t.w;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        float v = e[k];
+                        if (g.bias) v += bv[k];
+                        if (g.ga0) v += x0[k];
+                        if (g.ga1) v += x1[k];
+                        if (g.relu) v = fmaxf(v, 0.f);
+                        e[k] = v;
+                    }
+                    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+                    const u32x4_t w = {pack_bf16(e[0], e[1]), pack_bf16(e[2], e[3]), pack_bf16(e[4], e[5]),
+                                       pack_bf16(e[6], e[7])};
+                    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(reinterpret_cast<uint16_t*>(g.C) +
+                                                                              row * g.ldc + col));
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
         return;
     }
 #pragma unroll
@@ -162,7 +234,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (
 }
 
 // ABL: 0 = the kernel; 1 = timing ablation without the epilogue (one value per wave stored)
-template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, int ABL = 0>
+template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, int ABL = 0, bool WIDE = false>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     using L = B16Slice<BK>;
     constexpr int NW = WM * WN;
@@ -246,7 +318,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     }
     __syncthreads();   // every wave's fragment reads done before the epilogue reuses the LDS
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
-    b16_epilogue<TM, TN, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
+    b16_epilogue<TM, TN, C16, WIDE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
 }
 
 // Epilogue of one wave's TM x TN blocks for the persistent kernel: each 32x32 block through a
@@ -453,20 +525,23 @@ bool b16_ok(const GemmArgs& g, int ta, int tb) {
            aligned16(g.A) && aligned16(g.B) && 256 * g.lda * 2 < kMaxTileBytes && 256 * g.ldb * 2 < kMaxTileBytes;
 }
 
-// variant 0 (default) picks per call: the persistent kernel when the epilogue stores bf16 or
-// gathers rows (measured at E = 715,872 x 512 x 512: gathered bf16 1141 -> 1012 us, bf16 C 601 ->
-// 574 us), the one-tile-per-workgroup kernel for a plain f32 C (608 vs 649 us)
+// variant 0 (default) picks variant 11 (one tile per workgroup, whole-line bf16 C stores): at
+// E = 2,863,488 x 512 x 512 (cfg5, tools/bf16_storage_ab.py, same box, medians) bf16 C 1985 us
+// against 2145 (variant 7's half-line stores) and 2200 (persistent, variant 6); gathered bf16 C
+// 3620 against 3700 (variant 6). Round 2's pick at E = 715,872 was variant 6 for bf16 C and
+// gathers (gathered 1141 -> 1012 us, bf16 C 601 -> 574 us); for f32 C variants 7 and 11 are the
+// same kernel.
 static int b16_pick(const GemmArgs& g) {
     if (g_b16_variant != 0) return g_b16_variant;
-    return ((g.st & 4) || g.ga0) ? 6 : 7;
+    return 11;
 }
 
-static int b16_bm(int v) { return (v == 2 || v == 3 || v == 5) ? 128 : 256; }
+static int b16_bm(int v) { return (v == 2 || v == 3 || v == 5 || v == 10) ? 128 : 256; }
 
 static int64_t b16_grid(int v, int64_t M, int64_t N) {
     const int bm = b16_bm(v);
     const int64_t tiles = ((M + bm - 1) / bm) * ((N + 255) / 256);
-    if (v == 6) return tiles < kPersistentWgs ? tiles : kPersistentWgs;   // persistent: one per CU
+    if (v == 6 || v == 8 || v == 9 || v == 10) return tiles < kPersistentWgs ? tiles : kPersistentWgs;   // persistent: one per CU
     return tiles;
 }
 
@@ -485,6 +560,16 @@ static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
             hipLaunchKernelGGL((k_gemm_b16<128, 256, 32, 3, 2, 4, C16, 4, 1>), grid, dim3(512), 0, s, g); break;
         case 6:   // persistent 256x256, k64 x 2 slots (+ 32 KiB epilogue stage)
             hipLaunchKernelGGL((k_gemm_b16p<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        case 8:   // persistent 256x256, k32 x 4 slots (prefetch distance 3; 128 + 32 KiB of LDS)
+            hipLaunchKernelGGL((k_gemm_b16p<256, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        case 9:   // persistent 256x256, k32 x 3 slots
+            hipLaunchKernelGGL((k_gemm_b16p<256, 256, 32, 3, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        case 10:  // persistent 128x256, k32 x 4 slots (96 + 32 KiB)
+            hipLaunchKernelGGL((k_gemm_b16p<128, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
+        case 11:  // variant 7 with whole-line bf16 C stores (b16_epilogue WIDE)
+            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
+        case 12:  // variant 1 with whole-line bf16 C stores
+            hipLaunchKernelGGL((k_gemm_b16<256, 256, 32, 4, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
         default:  // 7: 256x256, k64 slices (whole 128-B row segments) x 2 slots
             hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
     }
@@ -500,7 +585,7 @@ void launch_b16(hipStream_t s, const GemmArgs& g) {
 }  // namespace bgnn
 
 extern "C" int bgnn_gemm_b16_variant(int32_t variant) {
-    BGNN_REQUIRE(variant >= -1 && variant <= 7, "gemm_b16_variant: must be -1 (off) or 0..7");
+    BGNN_REQUIRE(variant >= -1 && variant <= 12, "gemm_b16_variant: must be -1 (off) or 0..12");
     bgnn::g_b16_variant = variant;
     return BGNN_OK;
 }

@@ -112,7 +112,7 @@ def b16_variant():
 def test_b16_kernel_bit_identical_to_register_staged(dev, b16_variant, mnk, c16, gather):
     """bf16-stored A and B (storage 3 / 7, the EA_GNN edge products): every form of the LDS-DMA
     kernel (gemm_b16.hip: per-call default, persistent, one tile per workgroup, k32 slices,
-    128-row tiles) equals the register-staged k_gemm_x6 bit for bit -- bias, gathered node rows,
+    128-row tiles, whole-line bf16 C stores) equals the register-staged k_gemm_x6 bit for bit -- bias, gathered node rows,
     ReLU, f32 or bf16 C, ragged M and N -- and the register-staged result is the bf16-operand
     product (fp64 reference on the same bf16 operands)."""
     M, N, K = mnk
@@ -127,7 +127,8 @@ def test_b16_kernel_bit_identical_to_register_staged(dev, b16_variant, mnk, c16,
     st = 3 | (4 if c16 else 0)
 
     def run():
-        out = torch.empty(M, N, dtype=torch.bfloat16 if c16 else torch.float32, device=dev)
+        # NaN-filled: a variant that leaves part of C unwritten cannot pass on stale bytes
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16 if c16 else torch.float32, device=dev)
         if gather:
             _lib.call("bgnn_gemm_gather_add_bf16", M, N, K, a.data_ptr(), K, w.data_ptr(), K, out.data_ptr(), N,
                       bias.data_ptr(), 1, p1.data_ptr(), i1.data_ptr(), N, p2.data_ptr(), i2.data_ptr(), N, st, None, 0,
@@ -138,7 +139,7 @@ def test_b16_kernel_bit_identical_to_register_staged(dev, b16_variant, mnk, c16,
 
     b16_variant(-1)
     ref = run()
-    for v in (0, 6, 7, 1, 2, 3):
+    for v in (0, 6, 7, 1, 2, 3, 8, 9, 10, 11, 12):
         b16_variant(v)
         assert torch.equal(run(), ref), v
     exact = a.double() @ w.double().t() + bias.double()

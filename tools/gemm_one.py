@@ -15,7 +15,10 @@ import torch  # noqa: E402
 from bgnn import _lib, fused  # noqa: E402
 
 SHAPES = {"fwd": (80656, 1024, 512, False, True), "dgrad": (80656, 512, 1024, False, True),
-          "wgrad": (1024, 512, 80656, True, False)}
+          "wgrad": (1024, 512, 80656, True, False),
+          # the folded first layer (encoder Linear folded into [W_l;W_r]: K_in = 128)
+          "fold_fwd": (80656, 1024, 128, False, True), "fold_dgrad": (80656, 128, 1024, False, True),
+          "fold_wgrad": (1024, 128, 80656, True, False)}
 
 
 def main():
