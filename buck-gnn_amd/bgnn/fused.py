@@ -52,6 +52,8 @@ DGRAD_DROPADD = True
 BF16_PREP = True
 # per-layer weight maxima of a SAGE layer loop in one launch (bgnn_absmax_items_f32)
 ABSMAX_ITEMS = True
+# [W_l;W_r] of all layers packed by a multi-tensor copy into a persistent buffer (not torch.cat)
+PERSISTENT_WPACK = True
 
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
@@ -685,26 +687,64 @@ class SageLayerFn(torch.autograd.Function):
                 None, None, None, None, None, None, None, None)
 
 
+_WPACK = {}   # (weight pointers, shape, device) -> persistent ([L, 2H, H], its transpose) pack buffers
+
+
+def _weight_pack(pairs, L: int, H: int):
+    """Persistent [L, 2H, H] / [L, H, 2H] buffers for one layer loop's [W_l;W_r] (and transpose),
+    refilled every step by copies: a fresh torch.cat of the 2L weights each step blocked the host
+    ~0.4 ms (tools/host_profile.py). Reuse is safe on one stream: step t's backward, which reads
+    the pack, is enqueued before step t+1's refill."""
+    dev = pairs[0][0].device
+    key = (tuple((a.data_ptr(), b.data_ptr()) for a, b in pairs), L, H, dev, DGRAD_WT)
+    buf = _WPACK.get(key)
+    if buf is None:
+        if len(_WPACK) > 16:
+            _WPACK.clear()
+        W = torch.empty(L, 2 * H, H, dtype=torch.float32, device=dev)
+        Wt = torch.empty(L, H, 2 * H, dtype=torch.float32, device=dev) if DGRAD_WT else None
+        buf = _WPACK[key] = (W, Wt)
+    return buf
+
+
 def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
-    """[W_l;W_r] and its transpose for every layer of a loop in one concatenation, one transpose
-    and one max|W| pass per layer, instead of three launches per layer. pairs: [(w_l, w_r)]
-    per layer; amax_bufs: the loop's zeroed [L, 3] operand-max slots, whose slot 0 receives
-    max|[W_l;W_r]| for the layers where fill_amax[i] (a folded layer scales by max|Wf| instead).
+    """[W_l;W_r] and its transpose for every layer of a loop in a few launches (one multi-tensor
+    copy into a persistent pack, one transpose, one max|W| launch per run of layers that take it)
+    instead of three launches per layer. pairs: [(w_l, w_r)] per layer; amax_bufs: the loop's
+    zeroed [L, 3] operand-max slots, whose slot 0 receives max|[W_l;W_r]| for the layers where
+    fill_amax[i] (a folded layer scales by max|Wf| instead).
     Returns [(wcat, wcat_t)] per layer (views of two [L, ...] buffers)."""
     L = len(pairs)
     H = pairs[0][0].size(0)
     with torch.no_grad():   # operands only: the layers return the weight gradients themselves
-        W = torch.cat([t for pr in pairs for t in pr], 0).view(L, 2 * H, H)
-        Wt = W.transpose(1, 2).contiguous() if DGRAD_WT else None
-        # max|W| per layer with bgnn_absmax (torch's dim=(1, 2) max-reduction took 128 us here), all
-        # layers in one launch when every layer takes it
-        if ABSMAX_ITEMS and all(fill_amax) and amax_bufs.is_contiguous() and H % 4 == 0:
-            _lib.call("bgnn_absmax_items_f32", W.data_ptr(), L, 2 * H * H, 2 * H, H, H, amax_bufs.data_ptr(),
-                      amax_bufs.stride(0), _stream())
+        if PERSISTENT_WPACK and all(a.dtype == torch.float32 and b.dtype == torch.float32 and a.is_contiguous()
+                                    and b.is_contiguous() and a.shape == (H, H) and b.shape == (H, H)
+                                    for a, b in pairs):
+            W, Wt = _weight_pack(pairs, L, H)
+            torch._foreach_copy_([W[i, k * H:(k + 1) * H] for i in range(L) for k in (0, 1)],
+                                 [t for pr in pairs for t in pr])
+            if Wt is not None:
+                Wt.copy_(W.transpose(1, 2))
         else:
-            for i, f in enumerate(fill_amax):
-                if f:
-                    absmax(W[i], amax_bufs[i, 0:1], accumulate=True)
+            W = torch.cat([t for pr in pairs for t in pr], 0).view(L, 2 * H, H)
+            Wt = W.transpose(1, 2).contiguous() if DGRAD_WT else None
+        # max|W| per layer with bgnn_absmax (torch's dim=(1, 2) max-reduction took 128 us here),
+        # one launch per run of consecutive layers that take it (the folded first layer does not)
+        i = 0
+        while i < L:
+            if not fill_amax[i]:
+                i += 1
+                continue
+            j = i
+            while j < L and fill_amax[j]:
+                j += 1
+            if ABSMAX_ITEMS and amax_bufs.is_contiguous() and H % 4 == 0:
+                _lib.call("bgnn_absmax_items_f32", W[i].data_ptr(), j - i, 2 * H * H, 2 * H, H, H,
+                          amax_bufs[i].data_ptr(), amax_bufs.stride(0), _stream())
+            else:
+                for k in range(i, j):
+                    absmax(W[k], amax_bufs[k, 0:1], accumulate=True)
+            i = j
     return [(W[i], Wt[i] if Wt is not None else None) for i in range(L)]
 
 
