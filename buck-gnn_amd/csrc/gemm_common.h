@@ -49,6 +49,18 @@ __device__ __forceinline__ void beta_src4(const GemmArgs& g, int64_t row, int64_
     pv[3] = (m & 8u) ? t.w * kf : 0.f;
 }
 
+// beta_src4 on an already loaded float4 t of bsrc at (row, col) (the drop-add epilogue's prefetch)
+__device__ __forceinline__ void beta_mask4(const GemmArgs& g, int64_t row, int64_t col, const float4& t,
+                                           float (&pv)[4]) {
+    const int64_t i = row * g.ld_bsrc + col;
+    const uint32_t m = g.dthr ? keep_bits4(g.dseed, (uint64_t)(i >> 2), g.dthr) : 0xFu;
+    const float kf = g.dthr ? g.dkeep : 1.f;
+    pv[0] = (m & 1u) ? t.x * kf : 0.f;
+    pv[1] = (m & 2u) ? t.y * kf : 0.f;
+    pv[2] = (m & 4u) ? t.z * kf : 0.f;
+    pv[3] = (m & 8u) ? t.w * kf : 0.f;
+}
+
 // Base pointer that makes plane-split storage addressable with global coordinates:
 // element with split-dim index x lives at P + (x / blk) * pstride + (x % blk); for all x of
 // one plane that is Q + x with Q = P + plane * (pstride - blk).

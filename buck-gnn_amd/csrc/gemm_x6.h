@@ -109,6 +109,21 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
     const bool fast = !split && vec && gvec && (!g.bias || bias_vec) && r0 + TM * 32 <= g.M && c0 + TN * 32 <= g.N;
     const float iab = ia * ib;   // exact unless the two scales over/underflow together
     const bool one_mul = iab != 0.f && iab < 3.0e38f;
+    // drop-add dgrad (ABL 8), interior tile: every bsrc float4 this lane adds is loaded before the
+    // first staging pass, so the HBM latency overlaps the LDS staging and only the first 32-column
+    // block waits for it (the main loop's staging registers are dead here: 16 float4 fit)
+    constexpr bool kPre = ABL == 8 && !C16;
+    float4 gpre[kPre ? TN : 1][kPre ? TM * 4 : 1];
+    if constexpr (kPre) {
+        if (fast && g.beta != 0.f) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int q = 0; q < TM * 4; ++q)
+                    gpre[j][q] = *reinterpret_cast<const float4*>(g.bsrc + (r0 + q * 8 + rq) * g.ld_bsrc + c0 + j * 32 +
+                                                                  c4);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
 #pragma unroll
@@ -136,7 +151,9 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
                 const float x0[4] = {a0.x, a0.y, a0.z, a0.w}, x1[4] = {a1.x, a1.y, a1.z, a1.w};
                 float pv[4] = {0.f, 0.f, 0.f, 0.f};
                 if (g.beta != 0.f) {
-                    if constexpr (ABL == 8) {   // beta operand = masked bsrc (bgnn_gemm_f32_dropadd)
+                    if constexpr (kPre) {   // beta operand = masked bsrc (bgnn_gemm_f32_dropadd)
+                        beta_mask4(g, r0 + q * 8 + rq, col, gpre[j][q], pv);
+                    } else if constexpr (ABL == 8) {
                         beta_src4(g, r0 + q * 8 + rq, col, pv);
                     } else {
                         const float4 c4 = *reinterpret_cast<const float4*>(p);
