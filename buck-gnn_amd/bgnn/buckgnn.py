@@ -23,8 +23,8 @@ import torch
 from torch import Tensor, nn
 
 from . import ea as ea_mod
-from .ea import graphnet_block, skip_dropout
-from .fused import mlp, mlp_bf16, prepare_weights, sage_layer
+from .ea import GradSlot as EAGradSlot, graphnet_block, skip_dropout
+from .fused import mlp, mlp_bf16, prepare_weights, sage_layer, small_mlp
 from .graph import SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
@@ -216,6 +216,15 @@ class BuckGNN(nn.Module):
         # dropout mask seed drawn from torch's CPU generator: reproducible under torch.manual_seed
         return int(torch.randint(0, 2 ** 62, (1,)).item())
 
+    def _decode(self, h: Tensor) -> Tensor:
+        """The decoder on the pooled per-graph features: bgnn small-batch Linear layers on the
+        fused path (bgnn.fused.small_mlp), the torch modules otherwise."""
+        dec = self.decoder
+        # (a module with hooks is called as a module, so the hooks see its input and output)
+        hooked = bool(dec._forward_pre_hooks or dec._forward_hooks)
+        out = small_mlp(dec, h) if (self.use_fused and not hooked) else None
+        return dec(h) if out is None else out
+
     def _fused_ok(self, x: Tensor) -> bool:
         return self.use_fused and x.is_cuda and self.hidden_channels % 4 == 0 and self.hidden_channels <= 512
 
@@ -304,16 +313,17 @@ class BuckGNN(nn.Module):
                 x = x + identity
         return x
 
-    def _skip_dropout(self, x, e, x_prev, e_prev, skip: bool, fused: bool):
+    def _skip_dropout(self, x, e, x_prev, e_prev, skip: bool, fused: bool, e_slot=None):
         """EA_GNN's `if 0 < i < L-1: x, e = x + x_prev, e + e_prev` then Dropout on both
-        (Models/BuckGNN.py:382-387); one bgnn_add_dropout pass each on the fused path."""
+        (Models/BuckGNN.py:382-387); one bgnn_add_dropout pass each on the fused path (e_slot:
+        the edge gradient goes to the block's edge Linears, bgnn.ea.GradSlot)."""
         if not fused:
             if skip:
                 x, e = x + x_prev, e + e_prev
             return self.dropout(x), self.dropout(e)
         p = self.dropout.p
         return (skip_dropout(x, x_prev if skip else None, p, self.training, self._seed()),
-                skip_dropout(e, e_prev if skip else None, p, self.training, self._seed()))
+                skip_dropout(e, e_prev if skip else None, p, self.training, self._seed(), slot=e_slot))
 
     def _ea_block(self, blk, x, e, edge_index, fused: bool):
         return graphnet_block(blk, x, e, edge_index, self.ea_bf16) if fused else blk(x, edge_index, e)
@@ -362,11 +372,13 @@ class BuckGNN(nn.Module):
             L = len(self.gn_blocks)
             for i, blk in enumerate(self.gn_blocks):
                 x_prev, e_prev = x, e
+                # the last block's edge output feeds nothing: no gradient hand-off there
+                slot = EAGradSlot() if (ea_fused and self.ea_bf16 and self.training and i < L - 1) else None
                 if ea_fused:   # transform-first GraphNetBlock on bgnn GEMMs (bgnn/ea.py)
-                    x, e = graphnet_block(blk, x, e, edge_index, self.ea_bf16)
+                    x, e = graphnet_block(blk, x, e, edge_index, self.ea_bf16, slot=slot, slot_in=0 < i < L - 1)
                 else:
                     x, e = blk(x, edge_index, e)
-                x, e = self._skip_dropout(x, e, x_prev, e_prev, 0 < i < L - 1, ea_fused)
+                x, e = self._skip_dropout(x, e, x_prev, e_prev, 0 < i < L - 1, ea_fused, e_slot=slot)
         elif name in _SAGE_VARIANTS:
             attr, aggr, _ = _SAGE_VARIANTS[name]
             x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax, x_in)
@@ -396,7 +408,7 @@ class BuckGNN(nn.Module):
 
         if self.prediction_type == "buckling":
             pooled = self.get_pooling_layer(x, edge_index, batch)
-            return self.decoder(pooled).squeeze(), batch
+            return self._decode(pooled).squeeze(), batch
         if "static" in self.prediction_type or "mode_shape" in self.prediction_type:
             if "super" in self.pooling_layer:
                 return self.decoder(x[is_real_node]), real_node_batch

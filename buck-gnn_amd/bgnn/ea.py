@@ -80,7 +80,8 @@ class _LinearGatherReLU(torch.autograd.Function):
     dp1 / dp2 = deterministic segment sums of g' by i1 / i2."""
 
     @staticmethod
-    def forward(ctx, e, W, b, p1, seg1: SegmentIndex, p2, seg2: SegmentIndex, bf16: bool, out_bf16: bool = False):
+    def forward(ctx, e, W, b, p1, seg1: SegmentIndex, p2, seg2: SegmentIndex, bf16: bool, out_bf16: bool = False,
+                slot=None):
         e = e.contiguous()
         Wc = W.contiguous()
         M, K = e.shape
@@ -109,6 +110,7 @@ class _LinearGatherReLU(torch.autograd.Function):
                       ws_bytes, _stream())
         ctx.seg1, ctx.seg2, ctx.has2, ctx.bf16, ctx.has_bias = seg1, seg2, p2 is not None, bf16, b is not None
         ctx.storage = storage
+        ctx.slot = slot
         ctx.save_for_backward(e, W, out)
         return out
 
@@ -123,10 +125,12 @@ class _LinearGatherReLU(torch.autograd.Function):
                 db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
             de = (gemm_bf16(g, W.t().contiguous(), False, True, out_bf16=e.dtype == torch.bfloat16)
                   if ctx.needs_input_grad[0] else None)
+            if de is not None and ctx.slot is not None:
+                de = ctx.slot.add_to(de)   # + the skip + dropout's share of e's gradient, one pass
             dW = gemm_bf16(g, e, True, False)
             d1 = segment_reduce(g, ctx.seg1, "sum")
             d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
-            return de, dW, db, d1, None, d2, None, None, None
+            return de, dW, db, d1, None, d2, None, None, None, None
         # ReLU mask, bias gradient and max|g'| (the f16x3 operand scale of both GEMMs) in one pass
         g, db, g_amax = relu_bias_grad(g, out, ctx.has_bias)
         bf16 = ctx.bf16
@@ -137,7 +141,7 @@ class _LinearGatherReLU(torch.autograd.Function):
         dW = gemm(g, e, trans_a=True, trans_b=False, a_amax=g_amax, bf16=bf16)
         d1 = segment_reduce(g, ctx.seg1, "sum")
         d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
-        return de, dW, db, d1, None, d2, None, None, None
+        return de, dW, db, d1, None, d2, None, None, None, None
 
 
 def _epilogue_gather_available() -> bool:
@@ -147,12 +151,59 @@ def _epilogue_gather_available() -> bool:
     return fused.GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) != 0
 
 
-def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False, out_bf16=False):
+def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False, out_bf16=False, slot=None):
     if not _epilogue_gather_available():
         if e.dtype == torch.bfloat16 or out_bf16:
             raise ValueError("linear_gather_relu: bf16 storage needs the epilogue gather (split GEMM family)")
         return gather_add(linear(e, W, b, False, bf16=bf16), p1, seg1, p2, seg2, relu=True)
-    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16, out_bf16)
+    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16, out_bf16, slot)
+
+
+class GradSlot:
+    """Hand-off of one edge activation's skip + dropout gradient to the edge Linear that also
+    consumes it (EA_GNN bf16 storage, `FUSED_GRAD_ADD`). EA_GNN's block output e' (and, with the
+    skip, its input e) feeds both an edge Linear of the block (phi's first Linear; edge_mlp's) and
+    `Dropout(e' + e)` (Models/BuckGNN.py:382-387). Autograd would sum the two gradients with an
+    add over [E, H] after a dropout pass wrote drop(g); here the skip + dropout's backward leaves g
+    in the slot and returns no gradient for e' / e, and the Linear's backward adds drop(g) to its
+    input gradient in one pass (bgnn_add_dropped_bf16: the same mask, nothing stored).
+    Order: the skip + dropout node is created after the block's Linears, so autograd runs its
+    backward first; a consumer that finds the slot armed but empty raises instead of dropping a
+    gradient."""
+    __slots__ = ("armed", "g", "p", "seed")
+
+    def __init__(self):
+        self.armed, self.g, self.p, self.seed = False, None, 0.0, 0
+
+    def add_to(self, de: torch.Tensor) -> torch.Tensor:
+        if not self.armed:
+            return de
+        if self.g is None:
+            raise RuntimeError("GradSlot: the skip + dropout gradient had not arrived when the edge Linear's "
+                               "backward ran (autograd order)")
+        de = de.contiguous()
+        g = self.g
+        if g.shape != de.shape or g.dtype != torch.bfloat16 or de.dtype != torch.bfloat16:
+            raise RuntimeError("GradSlot: gradient shape / dtype mismatch")
+        _lib.call("bgnn_add_dropped_bf16", de.data_ptr(), g.data_ptr(), de.numel(), float(self.p), self.seed,
+                  de.data_ptr(), _stream())
+        return de
+
+
+class _SkipDropoutToSlot(torch.autograd.Function):
+    """drop(a + b) like _SkipDropout, whose backward hands g to `slot` (see GradSlot) instead of
+    returning drop(g) for a and b."""
+
+    @staticmethod
+    def forward(ctx, a, b, p: float, seed: int, slot: GradSlot):
+        ctx.slot = slot
+        slot.armed, slot.g, slot.p, slot.seed = True, None, p, seed
+        return _add_dropout(a, b, p, seed)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.slot.g = g.contiguous()
+        return None, None, None, None, None
 
 
 class _ColumnBlocks(torch.autograd.Function):
@@ -184,6 +235,9 @@ FUSED_SKIP_DROPOUT = True
 # Linear outputs; node-level tensors, weights and their gradients stay f32. False = bf16
 # operands with f32 storage (round-2 form, A/B)
 BF16_STORAGE = True
+# bf16 storage: the two gradients of every edge activation (an edge Linear's input gradient and the
+# skip + dropout's) summed by the Linear's backward in one pass (GradSlot) instead of autograd's add
+FUSED_GRAD_ADD = True
 
 
 def _add_dropout(a: torch.Tensor, b, p: float, seed: int) -> torch.Tensor:
@@ -208,8 +262,10 @@ class _SkipDropout(torch.autograd.Function):
         return gd, (gd if ctx.has_b else None), None, None
 
 
-def skip_dropout(a: torch.Tensor, b, p: float, training: bool, seed: int) -> torch.Tensor:
-    """Dropout_p(a + b) (b may be None) as one pass: Models/BuckGNN.py:382-387."""
+def skip_dropout(a: torch.Tensor, b, p: float, training: bool, seed: int, slot: GradSlot = None) -> torch.Tensor:
+    """Dropout_p(a + b) (b may be None) as one pass: Models/BuckGNN.py:382-387. With a slot
+    (EA_GNN bf16 storage), the backward hands the gradient to the edge Linears that consume a and b
+    (GradSlot) -- only for bf16 a / b, whose consumers were given the same slot."""
     if not training or p == 0.0:
         return a + b if b is not None else a
     ok = (FUSED_SKIP_DROPOUT and a.is_cuda and a.dtype in (torch.float32, torch.bfloat16) and a.is_contiguous()
@@ -218,12 +274,17 @@ def skip_dropout(a: torch.Tensor, b, p: float, training: bool, seed: int) -> tor
                              and b.data_ptr() % 16 == 0)))
     if not ok:
         return torch.nn.functional.dropout(a + b if b is not None else a, p, True)
+    if slot is not None and a.dtype == torch.bfloat16 and FUSED_GRAD_ADD:
+        return _SkipDropoutToSlot.apply(a, b, p, seed, slot)
     return _SkipDropout.apply(a, b, p, seed)
 
 
-def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tensor, bf16: bool = False):
+def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tensor, bf16: bool = False,
+                   slot: GradSlot = None, slot_in: bool = False):
     """(x_out, e_out) of one GraphNetBlock `blk` (bgnn.buckgnn.GraphNetBlock: same parameters
-    as the reference's) on the bgnn kernels."""
+    as the reference's) on the bgnn kernels. slot (bf16 storage): the GradSlot the caller passes to
+    the skip + dropout of this block's edge output; phi's first Linear (consumer of e_out) adds its
+    gradient, and edge_mlp's first Linear (consumer of e) too when slot_in (the skip uses e)."""
     N, H = x.shape
     seg_row, seg_col = edge_segments(edge_index, N)
     W1, b1 = blk.edge_mlp[0].weight, blk.edge_mlp[0].bias
@@ -239,11 +300,12 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
     st = bf16 and BF16_STORAGE and FUSED_GATHER and _epilogue_gather_available() and H % 8 == 0
     if st:   # bf16 edge activations end to end
         with fused._timed("ea_edge_fwd"):
-            h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=True, out_bf16=True)
+            h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=True, out_bf16=True,
+                                    slot=slot if slot_in else None)
         with fused._timed("ea_edge_fwd"):
             e_out = linear_bf16(h1, W2, b2, False, True)
         with fused._timed("ea_edge_fwd"):
-            m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=True, out_bf16=True)
+            m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=True, out_bf16=True, slot=slot)
         with fused._timed("ea_edge_fwd"):
             msg = linear_bf16(m1, Wp2, bp2, False, True)
         agg = segment_reduce(msg, seg_row, "mean")

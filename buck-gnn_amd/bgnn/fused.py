@@ -420,6 +420,82 @@ class _Mlp2Fn(torch.autograd.Function):
         return None, dW1, db1, dW2, db2
 
 
+class SmallMLPFn(torch.autograd.Function):
+    """An nn.Sequential of Linear (+ ReLU) layers on a few rows (the decoder on the pooled
+    [graphs, H] features, Models/BuckGNN.py:94-100) with one bgnn_small_linear_fwd launch per layer
+    (bias and ReLU inside) and one bgnn_small_linear_bwd per layer backward (ReLU mask, dW, db and
+    dx together) instead of a library GEMM, a ReLU kernel, bias reductions and ReLU-mask kernels
+    per layer. Inputs: x, then (W, b, relu) per layer flattened as weights / biases."""
+
+    @staticmethod
+    def forward(ctx, x, relus, *params):
+        x = x.contiguous()
+        B = x.size(0)
+        s = _stream()
+        acts = [x]
+        for i, relu in enumerate(relus):
+            W, b = params[2 * i], params[2 * i + 1]
+            N, K = W.shape
+            y = torch.empty(B, N, dtype=torch.float32, device=x.device)
+            _lib.call("bgnn_small_linear_fwd", acts[-1].data_ptr(), B, K, W.data_ptr(), _ptr(b), N, int(relu),
+                      y.data_ptr(), s)
+            acts.append(y)
+        ctx.relus = relus
+        ctx.has_bias = [params[2 * i + 1] is not None for i in range(len(relus))]
+        ctx.save_for_backward(*acts, *[params[2 * i] for i in range(len(relus))])
+        return acts[-1]
+
+    @staticmethod
+    def backward(ctx, g):
+        L = len(ctx.relus)
+        saved = ctx.saved_tensors
+        acts, Ws = saved[:L + 1], saved[L + 1:]
+        s = _stream()
+        g = g.contiguous()
+        B = g.size(0)
+        grads = [None] * (2 * L)
+        gx = None
+        for i in reversed(range(L)):
+            W = Ws[i]
+            N, K = W.shape
+            dW = torch.empty_like(W)
+            db = torch.empty(N, dtype=torch.float32, device=W.device) if ctx.has_bias[i] else None
+            need_dx = i > 0 or ctx.needs_input_grad[0]
+            dx = torch.empty(B, K, dtype=torch.float32, device=W.device) if need_dx else None
+            _lib.call("bgnn_small_linear_bwd", g.data_ptr(), acts[i + 1].data_ptr() if ctx.relus[i] else None,
+                      acts[i].data_ptr(), B, K, W.data_ptr(), N, _ptr(dx), dW.data_ptr(), _ptr(db), s)
+            grads[2 * i], grads[2 * i + 1] = dW, db
+            g = dx
+            gx = dx
+        return (gx, None, *grads)
+
+
+# the decoder on the pooled features as bgnn_small_linear layers (SmallMLPFn) when it qualifies
+SMALL_MLP = True
+SMALL_MLP_MAX_ROWS = 256
+
+
+def small_mlp(seq: torch.nn.Sequential, x: torch.Tensor):
+    """seq(x) through SmallMLPFn when seq is Linear (ReLU) ... Linear with f32 weights, x on the
+    GPU with at most SMALL_MLP_MAX_ROWS rows and every in_features a multiple of 4; else None."""
+    if not (SMALL_MLP and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+            and 0 < x.size(0) <= SMALL_MLP_MAX_ROWS):
+        return None
+    mods = list(seq)
+    relus, params = [], []
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if not (isinstance(m, torch.nn.Linear) and m.weight.dtype == torch.float32 and m.in_features % 4 == 0
+                and m.weight.is_contiguous()):
+            return None
+        relu = i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.ReLU)
+        relus.append(relu)
+        params += [m.weight, m.bias]
+        i += 2 if relu else 1
+    return SmallMLPFn.apply(x, tuple(relus), *params)
+
+
 def _mlp2_prefix(mods, x: torch.Tensor) -> bool:
     """Whether mods starts with Linear . ReLU . Linear . ReLU that bgnn_mlp2 covers for x."""
     if not FUSED_MLP2 or len(mods) < 4 or x.requires_grad or x.dtype != torch.float32 or x.dim() != 2:

@@ -37,6 +37,48 @@ class RelativeErrorLoss(nn.Module):
         return torch.mean(torch.abs(pred - target) / (torch.abs(target) + self.epsilon))
 
 
+class _RelErrorLossFn(torch.autograd.Function):
+    """RelativeErrorLoss of the denormalised prediction and target in one launch
+    (bgnn_rel_error_loss: loss and d loss / d pred together); backward one multiply."""
+
+    @staticmethod
+    def forward(ctx, pred, y, scale: float, center: float, eps: float):
+        from . import _lib
+        from .graph import _stream
+        pred = pred.contiguous()
+        y = y.contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=pred.device)
+        dpred = torch.empty_like(pred)
+        _lib.call("bgnn_rel_error_loss", pred.data_ptr(), y.data_ptr(), pred.numel(), float(scale), float(center),
+                  float(eps), loss.data_ptr(), dpred.data_ptr(), _stream())
+        ctx.save_for_backward(dpred)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dpred,) = ctx.saved_tensors
+        return dpred * g, None, None, None, None
+
+
+# train_step's loss: RelativeErrorLoss on EigenvalueScaler-denormalised values as one HIP launch
+FUSED_LOSS = True
+
+
+def _fused_loss(criterion, normalizer, pred, y):
+    """criterion(denorm(pred), denorm(y)) through _RelErrorLossFn when that is exactly what the
+    reference computes (TRAIN_FINAL.py:267-270 with Utils/Losses.py:755-761), else None."""
+    if not (FUSED_LOSS and type(criterion) is RelativeErrorLoss and pred.is_cuda and pred.dtype == torch.float32
+            and y.dtype == torch.float32 and pred.shape == y.shape and pred.numel() > 0):
+        return None
+    if normalizer is None:
+        scale, center = 1.0, 0.0
+    elif type(normalizer) is EigenvalueScaler:
+        scale, center = normalizer.scale, normalizer.center
+    else:
+        return None
+    return _RelErrorLossFn.apply(pred, y, scale, center, criterion.epsilon)
+
+
 def mape_error(pred, target, normalizer=None):
     """MAPE in percent for buckling targets (Dataset_Preparation/Metrics.py:4-12)."""
     if normalizer is not None:
@@ -224,10 +266,12 @@ def train_step(model, batch, optimizer, criterion, normalizer=None, allreduce: O
     # graph + pooling structure for this batch, one host sync (cached per tensor)
     prepare(batch.edge_index, batch.x.size(0), batch.batch, getattr(batch, "num_graphs", None) or None)
     pred, _ = model(batch.x, batch.edge_index, batch.edge_attr, batch.batch)
-    if normalizer is not None:
-        loss = criterion(normalizer.denormalize_eigenvalue(pred), normalizer.denormalize_eigenvalue(batch.y))
-    else:
-        loss = criterion(pred, batch.y)
+    loss = _fused_loss(criterion, normalizer, pred, batch.y)
+    if loss is None:
+        if normalizer is not None:
+            loss = criterion(normalizer.denormalize_eigenvalue(pred), normalizer.denormalize_eigenvalue(batch.y))
+        else:
+            loss = criterion(pred, batch.y)
     optimizer.zero_grad(set_to_none=True)
     loss.backward()
     if allreduce is not None:

@@ -168,6 +168,87 @@ extern "C" int bgnn_add_dropout_bf16(const void* a, const void* b, int64_t n, fl
     return BGNN_OK;
 }
 
+// out = a + drop(b) over bf16 (ABI 8): the gradient of an edge activation that feeds both an edge
+// Linear (a = that Linear's input gradient) and EA_GNN's skip + dropout (b = the dropout output's
+// gradient, masked here with the forward's mask: keep_bits4(seed, i / 4), kept values / (1 - p)),
+// in one pass instead of a dropout pass writing drop(b) and autograd's add reading it back.
+__global__ __launch_bounds__(256) void k_add_dropped_bf16(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                          int64_t n8, uint32_t thr, float inv_keep, uint64_t seed,
+                                                          uint4* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        float v[8], w[8];
+        bf16x8_unpack(a[i], v);
+        bf16x8_unpack(b[i], w);
+        if (thr) {
+#pragma unroll
+            for (int hgrp = 0; hgrp < 2; ++hgrp) {
+                const uint32_t keep = keep_bits4(seed, (uint64_t)(2 * i + hgrp), thr);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[4 * hgrp + k] = ((keep >> k) & 1u) ? w[4 * hgrp + k] * inv_keep : 0.f;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += w[k];
+        out[i] = make_uint4(bf16_pack2(v[0], v[1]), bf16_pack2(v[2], v[3]), bf16_pack2(v[4], v[5]),
+                            bf16_pack2(v[6], v[7]));
+    }
+}
+
+// RelativeErrorLoss on denormalised values (Utils/Losses.py:755-761 after Normalizer.py:203-215's
+// value * scale + center on prediction and target), forward and gradient in one launch (ABI 8):
+// loss = mean(|p' - t'| / (|t'| + eps)), p' = pred * scale + center, t' = y * scale + center;
+// dpred[i] = sign(p'_i - t'_i) * scale / ((|t'_i| + eps) * n). One block; the per-thread partial
+// sums (f64) are reduced in a fixed order. Replaces ~16 single-element torch launches per step.
+__global__ __launch_bounds__(256) void k_rel_error_loss(const float* __restrict__ pred, const float* __restrict__ y,
+                                                        int64_t n, float scale, float center, float eps,
+                                                        float* __restrict__ loss, float* __restrict__ dpred) {
+    __shared__ double red[256];
+    const int t = threadIdx.x;
+    double acc = 0.0;
+    const float inv_n = 1.f / (float)n;
+    for (int64_t i = t; i < n; i += 256) {
+        const float p = pred[i] * scale + center;
+        const float q = y[i] * scale + center;
+        const float d = fabsf(q) + eps;
+        const float diff = p - q;
+        acc += (double)(fabsf(diff) / d);
+        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+        if (dpred) dpred[i] = sg * scale / d * inv_n;
+    }
+    red[t] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) red[t] += red[t + o];
+        __syncthreads();
+    }
+    if (t == 0) *loss = (float)(red[0] / (double)n);
+}
+
+extern "C" int bgnn_add_dropped_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
+                                     void* stream) {
+    BGNN_REQUIRE(n >= 0 && n % 8 == 0, "add_dropped_bf16: n must be a multiple of 8");
+    BGNN_REQUIRE(p >= 0.f && p < 1.f, "add_dropped_bf16: p must be in [0, 1)");
+    if (n == 0) return BGNN_OK;
+    BGNN_REQUIRE(a && b && out && aligned16(a) && aligned16(b) && aligned16(out),
+                 "add_dropped_bf16: 16-byte aligned a / b / out required");
+    const uint32_t thr = dropout_threshold(p);
+    const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
+    hipLaunchKernelGGL(k_add_dropped_bf16, dim3(elem_blocks(n / 8)), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const uint4*>(a), reinterpret_cast<const uint4*>(b), n / 8, thr, inv_keep,
+                       seed, reinterpret_cast<uint4*>(out));
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_rel_error_loss(const float* pred, const float* y, int64_t n, float scale, float center, float eps,
+                                   float* loss, float* dpred, void* stream) {
+    BGNN_REQUIRE(pred && y && loss && n > 0, "rel_error_loss: null pointer or empty input");
+    hipLaunchKernelGGL(k_rel_error_loss, dim3(1), dim3(256), 0, as_stream(stream), pred, y, n, scale, center, eps, loss,
+                       dpred);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
 extern "C" int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
                                      int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream) {
     BGNN_REQUIRE(rowptr && (n_rows == 0 || (col && x && out)), "segment_sum_bf16: null pointer");

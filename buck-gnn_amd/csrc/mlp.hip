@@ -294,6 +294,88 @@ inline int mlp_blocks(int64_t N, int cap = kMlpBlocks) {
     return (int)(tiles < cap ? (tiles > 0 ? tiles : 1) : cap);
 }
 
+// ---------------------------------------------------------------------------
+// Small-batch Linear layers (ABI 8): the decoder MLP Linear(512,128).ReLU.Linear(128,64).ReLU.
+// Linear(64,1) (Models/BuckGNN.py:94-100) runs on the pooled [B = graphs, H] features -- a few
+// thousand outputs per layer, where a library GEMM launch plus a separate ReLU kernel (and the
+// backward's bias reductions and ReLU masks) cost ~8 us each for nanoseconds of work. Here one
+// launch per layer and direction, bias and ReLU (mask) inside; every output is reduced by one wave
+// in a fixed order (deterministic).
+
+// y[b, n] = act(sum_k x[b, k] W[n, k] + bias[n]): one wave per output, lanes split K (K % 4 == 0)
+__global__ __launch_bounds__(256) void k_small_linear_fwd(const float* __restrict__ x, int64_t B, int K,
+                                                          const float* __restrict__ W, const float* __restrict__ bias,
+                                                          int N, int relu, float* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= B * N) return;
+    const int64_t b = o / N;
+    const int n = (int)(o % N);
+    const float4* xr = reinterpret_cast<const float4*>(x + b * K);
+    const float4* wr = reinterpret_cast<const float4*>(W + (int64_t)n * K);
+    float acc = 0.f;
+    for (int k4 = lane; k4 < K / 4; k4 += 64) {
+        const float4 a = xr[k4], w = wr[k4];
+        acc = fmaf(a.x, w.x, acc);
+        acc = fmaf(a.y, w.y, acc);
+        acc = fmaf(a.z, w.z, acc);
+        acc = fmaf(a.w, w.w, acc);
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+        float v = acc + (bias ? bias[n] : 0.f);
+        y[o] = relu ? fmaxf(v, 0.f) : v;
+    }
+}
+
+// backward of y = act(x W^T + bias), g = gy masked by y > 0 when act is a ReLU (y != NULL):
+//   dW[n, k] = sum_b g[b, n] x[b, k]     (threads 0 .. N K / 4: one float4 of k each, loop over b)
+//   db[n]    = sum_b g[b, n]             (the k4 == 0 thread of each n)
+//   dx[b, k] = sum_n g[b, n] W[n, k]     (one wave per (b, 64 float4 of k), lanes over k, loop over n)
+__global__ __launch_bounds__(256) void k_small_linear_bwd_w(const float* __restrict__ gy, const float* __restrict__ y,
+                                                            const float* __restrict__ x, int64_t B, int K, int N,
+                                                            float* __restrict__ dW, float* __restrict__ db) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int K4 = K / 4;
+    if (t >= (int64_t)N * K4) return;
+    const int n = (int)(t / K4), k4 = (int)(t % K4);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float bs = 0.f;
+    for (int64_t b = 0; b < B; ++b) {
+        float g = gy[b * N + n];
+        if (y && !(y[b * N + n] > 0.f)) g = 0.f;
+        const float4 a = reinterpret_cast<const float4*>(x + b * K)[k4];
+        acc.x = fmaf(g, a.x, acc.x);
+        acc.y = fmaf(g, a.y, acc.y);
+        acc.z = fmaf(g, a.z, acc.z);
+        acc.w = fmaf(g, a.w, acc.w);
+        bs += g;
+    }
+    reinterpret_cast<float4*>(dW + (int64_t)n * K)[k4] = acc;
+    if (db && k4 == 0) db[n] = bs;
+}
+
+__global__ __launch_bounds__(256) void k_small_linear_bwd_x(const float* __restrict__ gy, const float* __restrict__ y,
+                                                            const float* __restrict__ W, int64_t B, int K, int N,
+                                                            float* __restrict__ dx) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int K4 = K / 4;
+    if (t >= B * K4) return;
+    const int64_t b = t / K4;
+    const int k4 = (int)(t % K4);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int n = 0; n < N; ++n) {
+        float g = gy[b * N + n];
+        if (y && !(y[b * N + n] > 0.f)) g = 0.f;
+        const float4 w = reinterpret_cast<const float4*>(W + (int64_t)n * K)[k4];
+        acc.x = fmaf(g, w.x, acc.x);
+        acc.y = fmaf(g, w.y, acc.y);
+        acc.z = fmaf(g, w.z, acc.z);
+        acc.w = fmaf(g, w.w, acc.w);
+    }
+    reinterpret_cast<float4*>(dx + b * K)[k4] = acc;
+}
+
 }  // namespace
 
 }  // namespace bgnn
@@ -352,5 +434,36 @@ extern "C" int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, i
     hipLaunchKernelGGL(k_sum_slots, dim3((kPartLen + 255) / 256), dim3(256), 0, s, tmp, kPartLen, kD2 * kD1, kD2,
                        kD1 * kF, dW2, db2, dW1, db1);
     BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_small_linear_fwd(const float* x, int64_t B, int32_t K, const float* W, const float* bias, int32_t N,
+                                     int32_t relu, float* y, void* stream) {
+    BGNN_REQUIRE(x && W && y && B >= 0 && K > 0 && N > 0, "small_linear_fwd: bad args");
+    BGNN_REQUIRE(K % 4 == 0 && aligned16(x) && aligned16(W), "small_linear_fwd: K %% 4 == 0 and 16-B aligned x, W");
+    if (B == 0) return BGNN_OK;
+    const int64_t waves = B * N;
+    hipLaunchKernelGGL(k_small_linear_fwd, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, as_stream(stream), x, B, K,
+                       W, bias, N, relu, y);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_small_linear_bwd(const float* gy, const float* y, const float* x, int64_t B, int32_t K,
+                                     const float* W, int32_t N, float* dx, float* dW, float* db, void* stream) {
+    BGNN_REQUIRE(gy && x && W && dW && B >= 0 && K > 0 && N > 0, "small_linear_bwd: bad args");
+    BGNN_REQUIRE(K % 4 == 0 && aligned16(x) && aligned16(W) && aligned16(dW) && (!dx || aligned16(dx)),
+                 "small_linear_bwd: K %% 4 == 0 and 16-B aligned x, W, dW, dx");
+    hipStream_t s = as_stream(stream);
+    const int64_t tw = (int64_t)N * (K / 4);
+    hipLaunchKernelGGL(k_small_linear_bwd_w, dim3((unsigned)((tw + 255) / 256)), dim3(256), 0, s, gy, y, x, B, K, N, dW,
+                       db);
+    BGNN_CHECK_LAUNCH();
+    if (dx && B > 0) {
+        const int64_t tx = B * (K / 4);
+        hipLaunchKernelGGL(k_small_linear_bwd_x, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, s, gy, y, W, B, K, N,
+                           dx);
+        BGNN_CHECK_LAUNCH();
+    }
     return BGNN_OK;
 }

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 7
+#define BGNN_ABI_VERSION 8
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -307,6 +307,11 @@ int bgnn_gemm_gather_add_bf16(int64_t M, int64_t N, int64_t K, const void* A, in
 int bgnn_gemm_b16_variant(int32_t variant);
 int bgnn_add_dropout_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
                           void* stream);
+/* ABI 8: out = a + drop(b) over bf16 (n a multiple of 8, 16-B aligned; out may alias a): b masked
+ * with bgnn_add_dropout_bf16's mask for (p, seed) -- EA_GNN's edge-activation gradient that sums
+ * an edge Linear's input gradient (a) and the skip + dropout's gradient (b) in one pass. */
+int bgnn_add_dropped_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
+                          void* stream);
 int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
                           int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream);
 
@@ -512,6 +517,25 @@ int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, int32_t D2, 
  * ---------------------------------------------------------------------- */
 int bgnn_add_dropout(const float* a, const float* b, int64_t n, float p, uint64_t seed, float* out,
                      void* stream);
+
+/* ABI 8: RelativeErrorLoss on denormalised values (Utils/Losses.py:755-761 applied to
+ * Normalizer.py:203-215's value * scale + center, TRAIN_FINAL.py:267-270): *loss =
+ * mean(|p' - t'| / (|t'| + eps)) with p' = pred * scale + center, t' = y * scale + center over n
+ * values (f32, device), and (dpred != NULL) dpred[i] = d loss / d pred[i]
+ * = sign(p'_i - t'_i) * scale / ((|t'_i| + eps) * n). One launch, deterministic. */
+int bgnn_rel_error_loss(const float* pred, const float* y, int64_t n, float scale, float center, float eps,
+                        float* loss, float* dpred, void* stream);
+
+/* ABI 8: small-batch Linear layers (the decoder MLP on the pooled [B = graphs, H] features,
+ * Models/BuckGNN.py:94-100): y[B, N] = act(x[B, K] W[N, K]^T + bias) (act = ReLU if relu; bias may
+ * be NULL); backward with g = gy masked by y > 0 when y != NULL (the layer's ReLU output):
+ * dW = g^T x, db = column sums of g (NULL: skipped), dx = g W (NULL: skipped). K % 4 == 0, x / W /
+ * dW / dx 16-B aligned; one wave or thread per output, fixed reduction order (deterministic).
+ * Meant for B up to a few hundred rows. */
+int bgnn_small_linear_fwd(const float* x, int64_t B, int32_t K, const float* W, const float* bias, int32_t N,
+                          int32_t relu, float* y, void* stream);
+int bgnn_small_linear_bwd(const float* gy, const float* y, const float* x, int64_t B, int32_t K, const float* W,
+                          int32_t N, float* dx, float* dW, float* db, void* stream);
 
 #ifdef __cplusplus
 }

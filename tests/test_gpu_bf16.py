@@ -204,3 +204,48 @@ def test_absmax_items_matches_per_item(dev):
     want[2] = 1e9
     assert torch.equal(bufs[:, 0], want)
     assert torch.equal(bufs[:, 1:], torch.zeros(L, 2, device=dev))
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1, 0.5])
+def test_add_dropped_bf16_matches_dropout_then_add(dev, p):
+    """bgnn_add_dropped_bf16 (a + drop(b), EA_GNN's edge-gradient hand-off): drop(b) uses the same
+    mask as bgnn_add_dropout_bf16 for (p, seed); one f32 sum, one bf16 rounding; in place on a."""
+    torch.manual_seed(31)
+    n = 4096 * 8 + 64
+    a = torch.randn(n, device=dev).to(torch.bfloat16)
+    b = torch.randn(n, device=dev).to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+    db = torch.empty_like(b)
+    _lib.call("bgnn_add_dropout_bf16", b.data_ptr(), None, n, float(p), 1234, db.data_ptr(), s)
+    ref = (a.float() + db.float()).to(torch.bfloat16)
+    out = a.clone()
+    _lib.call("bgnn_add_dropped_bf16", out.data_ptr(), b.data_ptr(), n, float(p), 1234, out.data_ptr(), s)
+    # drop(b) rounded to bf16 first in the reference: equal up to that one rounding
+    torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    dropped = db == 0   # dropped (or zero) elements of b leave a unchanged, exactly
+    assert torch.equal(out[dropped], a[dropped])
+    if p > 0:
+        assert 0.5 * p < dropped.float().mean().item() < 1.5 * p
+    if p == 0.0:
+        assert torch.equal(out, ref)
+
+
+def test_rel_error_loss_kernel_matches_torch(dev):
+    """bgnn_rel_error_loss (train_step's fused RelativeErrorLoss on EigenvalueScaler-denormalised
+    values, Utils/Losses.py:755-761): loss and d loss / d pred equal torch autograd's on the same
+    denormalisation, to f32 rounding."""
+    from bgnn import train as T
+    torch.manual_seed(32)
+    pred = torch.randn(16, 1, device=dev, requires_grad=True)
+    y = torch.randn(16, 1, device=dev)
+    y[3] = -0.5 / 2.0   # a target whose denormalised value is 0 (eps in the denominator)
+    crit, norm = T.RelativeErrorLoss(), T.EigenvalueScaler(center=0.5, scale=2.0)
+    ref = crit(norm.denormalize_eigenvalue(pred), norm.denormalize_eigenvalue(y))
+    (gref,) = torch.autograd.grad(ref, pred)
+    p2 = pred.detach().clone().requires_grad_(True)
+    got = T._fused_loss(crit, norm, p2, y)
+    assert got is not None
+    (ggot,) = torch.autograd.grad(got * 3.0, p2)
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=0)
+    torch.testing.assert_close(ggot, 3.0 * gref, rtol=1e-6, atol=0)
+    assert T._fused_loss(crit, norm, p2, y.view(-1)) is None   # broadcasting shapes: torch path

@@ -242,3 +242,32 @@ def test_ea_skip_dropout(dev, p, with_b):
     torch.testing.assert_close(a.grad, want, rtol=0, atol=0)
     if with_b:
         assert torch.equal(b.grad, a.grad)
+
+
+@pytest.mark.parametrize("dims", [(512, 128, 64, 1), (1024, 128, 64, 1), (64, 64, 3)])
+@pytest.mark.parametrize("rows", [1, 16, 200])
+def test_small_mlp_matches_fp64(dev, dims, rows):
+    """The decoder on the pooled features (bgnn.fused.small_mlp: bgnn_small_linear_fwd / _bwd,
+    Models/BuckGNN.py:94-100): output and every gradient (input, weights, biases) against an fp64
+    torch run of the same nn.Sequential, ReLUs included (inputs with many exact zeros)."""
+    from bgnn import fused
+    torch.manual_seed(rows + dims[0])
+    layers = []
+    for a, b in zip(dims[:-1], dims[1:]):
+        layers += [torch.nn.Linear(a, b), torch.nn.ReLU()]
+    seq = torch.nn.Sequential(*layers[:-1]).to(dev)
+    x = torch.randn(rows, dims[0], device=dev).clamp_min(0).requires_grad_(True)
+    out = fused.small_mlp(seq, x)
+    assert out is not None
+    gy = torch.randn_like(out)
+    grads = torch.autograd.grad(out, [x] + list(seq.parameters()), gy)
+    seq64 = copy.deepcopy(seq).double()
+    x64 = x.detach().double().requires_grad_(True)
+    out64 = seq64(x64)
+    grads64 = torch.autograd.grad(out64, [x64] + list(seq64.parameters()), gy.double())
+    torch.testing.assert_close(out.double(), out64, rtol=1e-5, atol=1e-5)
+    for g, g64 in zip(grads, grads64):
+        torch.testing.assert_close(g.double(), g64, rtol=1e-5, atol=1e-5 * (1 + g64.abs().max().item()))
+    again = torch.autograd.grad(fused.small_mlp(seq, x), [x] + list(seq.parameters()), gy)
+    for g, g2 in zip(grads, again):   # deterministic
+        assert torch.equal(g, g2)
