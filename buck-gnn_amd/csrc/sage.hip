@@ -425,22 +425,37 @@ __global__ __launch_bounds__(256) void k_linear_bwd_prep(const float4* __restric
     const int c4 = t % C4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     uint32_t m = 0;
-    for (int64_t r = (int64_t)blockIdx.x * rpi + t / C4; r < N; r += (int64_t)gridDim.x * rpi) {
-        float4 v = g[r * C4 + c4];
-        if (y) {
-            const float4 q = y[r * C4 + c4];
-            v.x = q.x > 0.f ? v.x : 0.f;
-            v.y = q.y > 0.f ? v.y : 0.f;
-            v.z = q.z > 0.f ? v.z : 0.f;
-            v.w = q.w > 0.f ? v.w : 0.f;
+    // UR rows per iteration with their loads issued together (one load per row in flight left
+    // this pass latency-bound on tall inputs: EA_GNN's node-level [N, 512] gradients)
+    constexpr int UR = 4;
+    const int64_t stride = (int64_t)gridDim.x * rpi;
+    for (int64_t r0 = (int64_t)blockIdx.x * rpi + t / C4; r0 < N; r0 += UR * stride) {
+        float4 vv[UR], qq[UR];
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int64_t r = r0 + u * stride;
+            vv[u] = r < N ? g[r * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (y) qq[u] = r < N ? y[r * C4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if (gout) gout[r * C4 + c4] = v;
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-        m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
-                       max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int64_t r = r0 + u * stride;
+            float4 v = vv[u];
+            if (y) {
+                const float4 q = qq[u];
+                v.x = q.x > 0.f ? v.x : 0.f;
+                v.y = q.y > 0.f ? v.y : 0.f;
+                v.z = q.z > 0.f ? v.z : 0.f;
+                v.w = q.w > 0.f ? v.w : 0.f;
+            }
+            if (gout && r < N) gout[r * C4 + c4] = v;
+            acc.x += v.x;
+            acc.y += v.y;
+            acc.z += v.z;
+            acc.w += v.w;
+            m = max(m, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                           max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+        }
     }
     red[t] = acc;
     // one atomic per block (same-address atomics serialise in L2)
@@ -480,24 +495,37 @@ __global__ __launch_bounds__(256) void k_linear_bwd_prep_bf16(const uint4* __res
     const int rpi = 256 / C8;
     const int c8 = t % C8;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int64_t r = (int64_t)blockIdx.x * rpi + t / C8; r < N; r += (int64_t)gridDim.x * rpi) {
-        uint4 v = g[r * C8 + c8];
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        if (y) {
-            const uint4 q = y[r * C8 + c8];
-            const uint32_t qy[4] = {q.x, q.y, q.z, q.w};
+    // UR rows per iteration, their loads issued together: one 16-B load per row and a grid of
+    // 512 blocks left a bias-only pass (no y) latency-bound at ~2 TB/s
+    constexpr int UR = 4;
+    const int64_t stride = (int64_t)gridDim.x * rpi;
+    for (int64_t r0 = (int64_t)blockIdx.x * rpi + t / C8; r0 < N; r0 += UR * stride) {
+        uint4 v[UR], q[UR];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t lo = bf16_lo(qy[k]) > 0.f ? 0x0000ffffu : 0u;
-                const uint32_t hi = bf16_hi(qy[k]) > 0.f ? 0xffff0000u : 0u;
-                w[k] &= lo | hi;
-            }
-            if (gout) gout[r * C8 + c8] = make_uint4(w[0], w[1], w[2], w[3]);
+        for (int u = 0; u < UR; ++u) {
+            const int64_t r = r0 + u * stride;
+            v[u] = r < N ? g[r * C8 + c8] : make_uint4(0u, 0u, 0u, 0u);
+            if (y) q[u] = r < N ? y[r * C8 + c8] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            acc[2 * k] += bf16_lo(w[k]);
-            acc[2 * k + 1] += bf16_hi(w[k]);
+        for (int u = 0; u < UR; ++u) {
+            const int64_t r = r0 + u * stride;
+            uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            if (y) {
+                const uint32_t qy[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t lo = bf16_lo(qy[k]) > 0.f ? 0x0000ffffu : 0u;
+                    const uint32_t hi = bf16_hi(qy[k]) > 0.f ? 0xffff0000u : 0u;
+                    w[k] &= lo | hi;
+                }
+                if (gout && r < N) gout[r * C8 + c8] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                acc[2 * k] += bf16_lo(w[k]);
+                acc[2 * k + 1] += bf16_hi(w[k]);
+            }
         }
     }
 #pragma unroll

@@ -79,3 +79,41 @@ def test_ea_h512_cfg2_meshes_adam_steps_follow_oracle(dev, bf16, rtol):
     for s, (a, r) in enumerate(zip(ours, ref)):
         assert a == pytest.approx(r, rel=rtol), (s, ours, ref)
     assert ref[-1] < ref[0] and ours[-1] < ours[0]
+
+
+def test_ea_bf16_grad_handoff_matches_autograd_add(dev, monkeypatch):
+    """EA_GNN bf16 with dropout 0.1 (the cfg5 training configuration): the edge-gradient hand-off
+    (bgnn.ea.GradSlot: an edge Linear's input gradient + the skip/dropout gradient in one pass) is
+    taken in every block but the last, and every parameter gradient matches the path where
+    autograd adds the two (same dropout masks) to bf16 rounding."""
+    from bgnn import ea
+    b = S.make_batch(12, 4).to(dev)
+    crit, norm = bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5)
+    torch.manual_seed(0)
+    model = bgnn.BuckGNN(16, 5, hidden_channels=64, num_layers=6, dropout_rate=0.1, model_name="EA_GNN").to(dev)
+    model.train()
+    model.ea_bf16 = True
+    used = []
+    orig = ea.GradSlot.add_to
+
+    def counting(self, de):
+        used.append(self.armed)
+        return orig(self, de)
+    monkeypatch.setattr(ea.GradSlot, "add_to", counting)
+
+    def grads(handoff):
+        monkeypatch.setattr(ea, "FUSED_GRAD_ADD", handoff)
+        model.zero_grad(set_to_none=True)
+        torch.manual_seed(123)   # the same dropout seeds (bgnn.BuckGNN._seed) in both runs
+        pred, _ = model(b.x, b.edge_index, b.edge_attr, b.batch)
+        crit(norm.denormalize_eigenvalue(pred), norm.denormalize_eigenvalue(b.y)).backward()
+        return {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+
+    ref = grads(False)
+    assert not any(used)
+    got = grads(True)
+    # blocks 0..4 hand e_out's gradient to phi's Linear, blocks 1..4 e's to edge_mlp's: 9 hand-offs
+    assert sum(used) == 9
+    assert got.keys() == ref.keys()
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k], rtol=3e-2, atol=3e-2 * (1e-6 + ref[k].abs().max().item()), msg=k)
