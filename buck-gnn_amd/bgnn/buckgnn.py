@@ -248,7 +248,9 @@ class BuckGNN(nn.Module):
             graph = graph_for(edge_index, x.size(0))
             red = 1 if aggr == "mean" else 0
             amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
-            bufs = torch.zeros(L, 3, dtype=torch.float32, device=x.device)   # per-layer operand maxima, one fill
+            # per-layer operand maxima and the folded layer's weight-product maxima, one fill
+            scratch = torch.zeros(3 * L + 5, dtype=torch.float32, device=x.device)
+            bufs, fold_amax = scratch[:3 * L].view(L, 3), scratch[3 * L:]
             layers = [convs[i] if convs is not None else self.shared_graphsage_block for i in range(L)]
             wprep = prepare_weights([(c.lin_l.weight, c.lin_r.weight) for c in layers], bufs,
                                     [not (i == 0 and x_in is not None) for i in range(L)])
@@ -261,7 +263,8 @@ class BuckGNN(nn.Module):
                 x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
                                      skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
                                      amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
-                                     b_in=None if fold is None else fold.bias, wprep=wprep[i], count_batch=False)
+                                     b_in=None if fold is None else fold.bias, wprep=wprep[i], count_batch=False,
+                                     fold_amax=fold_amax)
             return x
         if x_in is not None:   # (only reached when the caller folded the encoder's last Linear)
             x = x_in(x)

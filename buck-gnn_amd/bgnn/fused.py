@@ -545,7 +545,7 @@ def _ptr(t):
 
 
 class LayerConfig:
-    __slots__ = ("reduce", "bn", "training", "momentum", "eps", "skip", "p", "seed")
+    __slots__ = ("reduce", "bn", "training", "momentum", "eps", "skip", "p", "seed", "famax")
 
     def __init__(self, reduce: int, bn: bool, training: bool, momentum: float, eps: float, skip: bool,
                  p: float, seed: int):
@@ -557,6 +557,10 @@ class LayerConfig:
         self.skip = skip
         self.p = p if training else 0.0
         self.seed = seed
+        # folded layer: 5 zeroed device slots for the maxima of the weight-product operands
+        # (max|Wcat|, max|W_in|, max|b_in|, max|dWf|, max|dbf|), so those small f16x3 GEMMs need no
+        # max pass (and no zero fill) of their own
+        self.famax = None
 
 
 class SageLayerFn(torch.autograd.Function):
@@ -589,10 +593,17 @@ class SageLayerFn(torch.autograd.Function):
                 wf = torch.mm(wcat, w_in)
                 bf = torch.mv(wcat, b_in)
             else:
-                wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False)
+                fs = cfg.famax
+                fa = (fs[0:1], fs[1:2], fs[2:3]) if fs is not None else (None, None, None)
+                if fs is not None:   # the same maxima the GEMMs would compute, without their fills
+                    absmax(wcat, fa[0], accumulate=True)
+                    absmax(w_in, fa[1], accumulate=True)
+                    absmax(b_in.view(1, -1), fa[2], accumulate=True)
+                wf = gemm(wcat, w_in.contiguous(), trans_a=False, trans_b=False, a_amax=fa[0], b_amax=fa[1])
                 # (bgnn GEMM, not torch.mv: rocBLAS's GEMV moved the BN-amplified gradients of the
                 # Shared variant 50x further from fp64, tests/test_gpu_fold.py)
-                bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False).view(-1)
+                bf = gemm(wcat, b_in.contiguous().view(H, 1), trans_a=False, trans_b=False, a_amax=fa[0],
+                          b_amax=fa[2]).view(-1)
             absmax(wf, w_amax, accumulate=True)
             wmat = wf
         else:
@@ -703,11 +714,12 @@ class SageLayerFn(torch.autograd.Function):
                   float(cfg.p), cfg.seed, int(cfg.skip and not dropadd), N, H, dh.data_ptr(), lddz, _ptr(gskip),
                   part_db.data_ptr(), dz_amax.data_ptr(), graph.fwd.rowptr.data_ptr() if ctx.folded else None,
                   (2 if cfg.reduce == 1 else 1) if ctx.folded else 0, s)
-        db = torch.empty(2 if ctx.folded else 1, H, dtype=torch.float32, device=dev)
-        # db[0] = sum of dh (db_l); folded input transform: db[1] = column sums of dz_l = A^T dh
-        _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db[0].data_ptr(),
-                  db[1].data_ptr() if ctx.folded else None, 0, s)
-        db, db_zl = db[0], (db[1] if ctx.folded else None)
+        db2 = torch.empty(2 if ctx.folded else 1, H, dtype=torch.float32, device=dev)
+        # sum of dh (db_l) into the last row; folded input transform: the column sums of dz_l = A^T dh
+        # into row 0, so that db2 viewed flat is [sum dz_l ; sum dh], the folded layer's dbf
+        _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db2[-1].data_ptr(),
+                  db2[0].data_ptr() if ctx.folded else None, 0, s)
+        db, db_zl = db2[-1], (db2[0] if ctx.folded else None)
         # dz_l = A^T dh (transpose CSR; MEAN scales by the target's in-degree)
         bw = graph.bwd
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
@@ -723,18 +735,25 @@ class SageLayerFn(torch.autograd.Function):
             wf_t = wf.t().contiguous() if DGRAD_WT else wf
             with _timed("gemm_dgrad_fold"):
                 dx = gemm(dz, wf_t, trans_a=False, trans_b=DGRAD_WT, a_amax=dz_amax, b_amax=w_amax)
+            fs = cfg.famax
+            fa = (fs[0:1], fs[1:2], fs[2:3], fs[3:4], fs[4:5]) if fs is not None else (None,) * 5
             with _timed("gemm_wgrad_fold"):
-                dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)   # [2H, K_in]
-            dbf = torch.cat([db_zl, db])                                                    # Σ dz_l ; Σ dh
+                dwf = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax,
+                           c_amax=fa[3])                                                   # [2H, K_in]
+            dbf = db2.view(-1)                                                              # Σ dz_l ; Σ dh
+            if fs is not None:
+                absmax(db2, fa[4], accumulate=True)
             if FOLD_WEIGHTS_TORCH:
                 dw = torch.addmm(torch.outer(dbf, b_in), dwf, w_in.t())                    # [2H, H]
                 dw_in = torch.mm(wcat.t(), dwf)                                            # [H, K_in]
                 db_in = torch.mv(wcat.t(), dbf)                                            # [H]
             else:
-                dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True)             # [2H, H]
+                dw = gemm(dwf, w_in.contiguous(), trans_a=False, trans_b=True, a_amax=fa[3],
+                          b_amax=fa[1])                                                    # [2H, H]
                 dw.add_(torch.outer(dbf, b_in))
-                dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False)                       # [H, K_in]
-                db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False).view(-1)  # [H]
+                dw_in = gemm(wcat, dwf, trans_a=True, trans_b=False, a_amax=fa[0], b_amax=fa[3])  # [H, K_in]
+                db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False, a_amax=fa[0],
+                             b_amax=fa[4]).view(-1)                                        # [H]
             return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
                     None, None, None, None, None, dw_in, db_in, None)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
@@ -827,7 +846,8 @@ def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
 def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
                seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None,
-               w_in: torch.Tensor = None, b_in: torch.Tensor = None, wprep=None, count_batch: bool = True):
+               w_in: torch.Tensor = None, b_in: torch.Tensor = None, wprep=None, count_batch: bool = True,
+               fold_amax: torch.Tensor = None):
     """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
     x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
     spares the GEMM a pass over x_prev; return_amax: also return max|x_next|.
@@ -854,11 +874,13 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
         cfg = LayerConfig(reduce, True, use_batch_stats, float(momentum or 0.0) if bn_module.track_running_stats
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
+        cfg.famax = fold_amax if w_in is not None else None
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
                                 bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in,
                                 wprep)
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
+        cfg.famax = fold_amax if w_in is not None else None
         out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
                                 w_in, b_in, wprep)
     return out if return_amax else out[0]
