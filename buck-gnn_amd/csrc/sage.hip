@@ -119,6 +119,84 @@ __global__ __launch_bounds__(256) void k_bn_finalize(const float* __restrict__ p
     }
 }
 
+// One-launch reduction of [n_slots, 2, H] partial slots (round 3; replaces k_slots_stage1 + the
+// final kernel, one launch fewer per reduction): a block owns 8 channels, its 256 threads are
+// 8 channels x 32 slot phases; each thread sums its slots ph, ph + 32, ... of both halves in f64
+// (eight loads in flight), then a fixed f64 tree over the 32 phases. MODE 0: out0 / out1 (=, or +=
+// with accumulate); MODE 1: the BatchNorm finalize of k_bn_finalize on (sum, sum of squares).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_reduce_slots(const float* __restrict__ part, int n_slots, int H,
+                                                      float* __restrict__ out0, float* __restrict__ out1,
+                                                      int accumulate, int64_t count, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float eps, float momentum,
+                                                      float* __restrict__ rmean, float* __restrict__ rvar,
+                                                      float* __restrict__ mean, float* __restrict__ invstd,
+                                                      float* __restrict__ scale, float* __restrict__ shift) {
+    constexpr int CPB = 8, NPH = 256 / CPB;   // channels per block, slot phases
+    __shared__ double red[2][NPH][CPB];
+    const int cl = threadIdx.x % CPB, ph = threadIdx.x / CPB;
+    const int c = blockIdx.x * CPB + cl;
+    const int64_t W = 2 * (int64_t)H;
+    double s0 = 0.0, s1 = 0.0;
+    if (c < H) {
+        int sl = ph;
+        for (; sl + 7 * NPH < n_slots; sl += 8 * NPH) {
+            float a[8], b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                a[u] = part[(int64_t)(sl + u * NPH) * W + c];
+                b[u] = part[(int64_t)(sl + u * NPH) * W + H + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s0 += (double)a[u];
+                s1 += (double)b[u];
+            }
+        }
+        for (; sl < n_slots; sl += NPH) {
+            s0 += (double)part[(int64_t)sl * W + c];
+            s1 += (double)part[(int64_t)sl * W + H + c];
+        }
+    }
+    red[0][ph][cl] = s0;
+    red[1][ph][cl] = s1;
+    __syncthreads();
+    for (int o = NPH / 2; o > 0; o >>= 1) {
+        if (ph < o) {
+            red[0][ph][cl] += red[0][ph + o][cl];
+            red[1][ph][cl] += red[1][ph + o][cl];
+        }
+        __syncthreads();
+    }
+    if (ph != 0 || c >= H) return;
+    s0 = red[0][0][cl];
+    s1 = red[1][0][cl];
+    if constexpr (MODE == 0) {
+        if (out0) out0[c] = accumulate ? out0[c] + (float)s0 : (float)s0;
+        if (out1) out1[c] = accumulate ? out1[c] + (float)s1 : (float)s1;
+    } else {
+        const double n = (double)count;
+        const double mu = s0 / n;
+        double var = s1 / n - mu * mu;
+        if (var < 0.0) var = 0.0;
+        const double is = 1.0 / sqrt(var + (double)eps);
+        const float g = gamma ? gamma[c] : 1.f;
+        const float b = beta ? beta[c] : 0.f;
+        mean[c] = (float)mu;
+        invstd[c] = (float)is;
+        scale[c] = (float)((double)g * is);
+        shift[c] = (float)((double)b - mu * (double)g * is);
+        if (rmean && rvar && momentum > 0.f) {
+            const double unb = count > 1 ? var * n / (n - 1.0) : var;
+            rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mu);
+            rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+        }
+    }
+}
+
+// one-launch reductions (k_reduce_slots) instead of stage 1 + final kernel (A/B switch)
+static int g_one_pass_reduce = 1;
+
 __global__ void k_bn_eval(int H, const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                           const float* __restrict__ rmean, const float* __restrict__ rvar,
                           float* __restrict__ scale, float* __restrict__ shift) {
@@ -581,6 +659,13 @@ extern "C" int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32
                                     int32_t accumulate, void* stream) {
     BGNN_REQUIRE(partial && H > 0 && n_slots >= 0, "reduce_partials: bad args");
     hipStream_t s = as_stream(stream);
+    if (g_one_pass_reduce) {
+        hipLaunchKernelGGL(k_reduce_slots<0>, dim3((H + 7) / 8), dim3(256), 0, s, partial, n_slots, H, out0, out1,
+                           accumulate, (int64_t)0, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, nullptr);
+        BGNN_CHECK_LAUNCH();
+        return BGNN_OK;
+    }
     const int stride = slots_stage1(const_cast<float*>(partial), n_slots, H, s);
     BGNN_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_reduce_partials, dim3((H + 63) / 64), dim3(256), 0, s, partial, n_slots, stride, H, out0,
@@ -595,6 +680,13 @@ extern "C" int bgnn_bn_finalize(const float* bn_partial, int32_t n_slots, int32_
                                 float* shift, void* stream) {
     BGNN_REQUIRE(bn_partial && H > 0 && count > 0 && mean && invstd && scale && shift, "bn_finalize: bad args");
     hipStream_t s = as_stream(stream);
+    if (g_one_pass_reduce) {
+        hipLaunchKernelGGL(k_reduce_slots<1>, dim3((H + 7) / 8), dim3(256), 0, s, bn_partial, n_slots, H, nullptr,
+                           nullptr, 0, count, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd,
+                           scale, shift);
+        BGNN_CHECK_LAUNCH();
+        return BGNN_OK;
+    }
     const int stride = slots_stage1(const_cast<float*>(bn_partial), n_slots, H, s);
     BGNN_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_bn_finalize, dim3((H + 63) / 64), dim3(256), 0, s, bn_partial, n_slots, stride, H, count,
