@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void k_small_linear_fwd(const float* __restric
 // backward of y = act(x W^T + bias), g = gy masked by y > 0 when act is a ReLU (y != NULL):
 //   dW[n, k] = sum_b g[b, n] x[b, k]     (threads 0 .. N K / 4: one float4 of k each, loop over b)
 //   db[n]    = sum_b g[b, n]             (the k4 == 0 thread of each n)
-//   dx[b, k] = sum_n g[b, n] W[n, k]     (one wave per (b, 64 float4 of k), lanes over k, loop over n)
+//   dx[b, k] = sum_n g[b, n] W[n, k]     (one wave per float4 of dx, lanes split n)
 __global__ __launch_bounds__(256) void k_small_linear_bwd_w(const float* __restrict__ gy, const float* __restrict__ y,
                                                             const float* __restrict__ x, int64_t B, int K, int N,
                                                             float* __restrict__ dW, float* __restrict__ db) {
@@ -358,13 +358,16 @@ __global__ __launch_bounds__(256) void k_small_linear_bwd_w(const float* __restr
 __global__ __launch_bounds__(256) void k_small_linear_bwd_x(const float* __restrict__ gy, const float* __restrict__ y,
                                                             const float* __restrict__ W, int64_t B, int K, int N,
                                                             float* __restrict__ dx) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // one wave per float4 of dx: lanes split N, a fixed shuffle tree sums them (a thread looping
+    // over all N rows of W ran latency-bound at ~20 us for the 512-wide layer)
+    const int lane = threadIdx.x & 63;
+    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int K4 = K / 4;
-    if (t >= B * K4) return;
-    const int64_t b = t / K4;
-    const int k4 = (int)(t % K4);
+    if (o >= B * K4) return;
+    const int64_t b = o / K4;
+    const int k4 = (int)(o % K4);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int n = 0; n < N; ++n) {
+    for (int n = lane; n < N; n += 64) {
         float g = gy[b * N + n];
         if (y && !(y[b * N + n] > 0.f)) g = 0.f;
         const float4 w = reinterpret_cast<const float4*>(W + (int64_t)n * K)[k4];
@@ -373,7 +376,13 @@ __global__ __launch_bounds__(256) void k_small_linear_bwd_x(const float* __restr
         acc.z = fmaf(g, w.z, acc.z);
         acc.w = fmaf(g, w.w, acc.w);
     }
-    reinterpret_cast<float4*>(dx + b * K)[k4] = acc;
+    for (int off = 32; off > 0; off >>= 1) {
+        acc.x += __shfl_xor(acc.x, off, 64);
+        acc.y += __shfl_xor(acc.y, off, 64);
+        acc.z += __shfl_xor(acc.z, off, 64);
+        acc.w += __shfl_xor(acc.w, off, 64);
+    }
+    if (lane == 0) reinterpret_cast<float4*>(dx + b * K)[k4] = acc;
 }
 
 }  // namespace
@@ -460,8 +469,8 @@ extern "C" int bgnn_small_linear_bwd(const float* gy, const float* y, const floa
                        db);
     BGNN_CHECK_LAUNCH();
     if (dx && B > 0) {
-        const int64_t tx = B * (K / 4);
-        hipLaunchKernelGGL(k_small_linear_bwd_x, dim3((unsigned)((tx + 255) / 256)), dim3(256), 0, s, gy, y, W, B, K, N,
+        const int64_t waves = B * (K / 4);
+        hipLaunchKernelGGL(k_small_linear_bwd_x, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, gy, y, W, B, K, N,
                            dx);
         BGNN_CHECK_LAUNCH();
     }
