@@ -98,6 +98,8 @@ def parse():
                          "EA_GNN diverges in the reference too, tests/test_gpu_ea_train.py)")
     ap.add_argument("--bf16", action="store_true",
                     help="EA_GNN only: bf16 GEMM operands with f32 accumulation (BASELINE configs[4])")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="bgnn_set_tuning(KNOB, VALUE) before the run (A/B profiling; include/bgnn.h BGNN_TUNE_*)")
     return ap.parse_args()
 
 
@@ -131,6 +133,9 @@ def main():
     import bgnn
     from bgnn import _lib, fused, synthetic
 
+    for kv in args.tune:
+        k, v = kv.split("=")
+        _lib.call("bgnn_set_tuning", int(k), int(v))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

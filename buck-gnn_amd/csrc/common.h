@@ -92,6 +92,8 @@ int gemm_tail();
 // non-temporal output stores of the row-wise SAGE kernels (sage.hip)
 void set_rows_nt(int on);
 int rows_nt();
+void set_rows_rev(int on);
+int rows_rev();
 
 // 16-byte store, non-temporal (streamed once: no write-allocate in L2 / Infinity Cache)
 __device__ __forceinline__ void store4(float* p, float a, float b, float c, float d, bool nt) {

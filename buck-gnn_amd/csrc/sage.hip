@@ -228,9 +228,23 @@ __global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o
                                                     const float* __restrict__ shift,
                                                     const float4* __restrict__ xprev, int skip, uint32_t thr,
                                                     float inv_keep, uint64_t seed, int64_t n4, int H4,
-                                                    float4* __restrict__ xn, uint32_t* __restrict__ amax, int nt) {
+                                                    float4* __restrict__ xn, uint32_t* __restrict__ amax, int nt,
+                                                    int rev) {
     uint32_t m = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    // rev = 1 (grid a multiple of 8): block b sweeps the eighth (b & 7) of the rows from its last
+    // element down, so each eighth starts on the rows the aggregation (which sweeps the same
+    // eighths upward, one per XCD) wrote last and are still in the Infinity Cache. Element-wise:
+    // the result does not depend on the order.
+    int64_t lo = 0, hi = n4, i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    if (rev) {
+        const int64_t nr = n4 / H4, x = blockIdx.x & 7;
+        lo = (nr * x / 8) * H4;
+        hi = (nr * (x + 1) / 8) * H4;
+        i0 = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x;
+        st = (int64_t)(gridDim.x >> 3) * blockDim.x;
+    }
+    for (int64_t q = i0; q < hi - lo; q += st) {
+        const int64_t i = rev ? hi - 1 - q : q;
         const int c = (int)(i % H4) * 4;
         float4 v = o[i];
         float y[4] = {v.x, v.y, v.z, v.w};
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
     int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
     float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax, int nt,
-    const int32_t* __restrict__ w_rowptr, int w_mode) {
+    const int32_t* __restrict__ w_rowptr, int w_mode, int rev) {
     const int lane = threadIdx.x & 63;
     uint32_t tmax = 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -387,13 +401,21 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
             on[v] = reinterpret_cast<const float4*>(o)[i4];
         }
     };
-    if (r0 + wave < r1) fetch(r0 + wave);
-    for (int64_t r = r0 + wave; r < r1; r += 4) {
+    // rev = 1: the block's rows are walked from its last row down (wave w takes r1-1-w, r1-5-w, ...),
+    // so the first rows read are the ones bgnn_sage_bwd_stats read last over the same block ranges
+    // and that are still in the Infinity Cache. Only the summation order of the dh partials changes.
+    const int64_t nr = r1 - r0 - wave;
+    const int64_t cnt = nr > 0 ? (nr + 3) / 4 : 0;
+    const int64_t rfirst = rev ? r1 - 1 - wave : r0 + wave;
+    const int64_t rstep = rev ? -4 : 4;
+    if (cnt > 0) fetch(rfirst);
+    for (int64_t j = 0; j < cnt; ++j) {
+        const int64_t r = rfirst + j * rstep;
         float ov[NV][4], dov[NV][4], g1v[NV][4];
         float4 gc[NV], oc[NV];
 #pragma unroll
         for (int v = 0; v < NV; ++v) { gc[v] = gn[v]; oc[v] = on[v]; }
-        if (r + 4 < r1) fetch(r + 4);
+        if (j + 1 < cnt) fetch(r + rstep);
         float dot = 0.f;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
@@ -480,6 +502,9 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static int g_rows_nt = 0;
 void set_rows_nt(int on) { g_rows_nt = on ? 1 : 0; }
 int rows_nt() { return g_rows_nt; }
+static int g_rows_rev = 0;
+void set_rows_rev(int on) { g_rows_rev = on & 15; }
+int rows_rev() { return g_rows_rev; }
 
 }  // namespace bgnn
 
@@ -720,11 +745,13 @@ extern "C" int bgnn_sage_apply(const float* o, const float* scale, const float* 
     const int64_t n4 = n_rows * (H / 4);
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
+    const int rev = (rows_rev() & 2) ? 1 : 0;
+    if (rev) blocks = (blocks + 7) / 8 * 8;
     const uint32_t thr = dropout_threshold(p);
     const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
     hipLaunchKernelGGL(k_sage_apply, dim3((unsigned)blocks), dim3(256), 0, s, (const float4*)o, scale, shift,
                        (const float4*)x_prev, skip, thr, inv_keep, seed, n4, H / 4, (float4*)x_next,
-                       reinterpret_cast<uint32_t*>(amax), rows_nt());
+                       reinterpret_cast<uint32_t*>(amax), rows_nt(), rev);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
@@ -773,11 +800,11 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
     if (H > 256)
         hipLaunchKernelGGL(k_sage_bwd_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode);
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode, rows_rev() & 1);
     else
         hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
                            gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode);
+                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode, rows_rev() & 1);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
@@ -799,12 +826,12 @@ extern "C" int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm,
         hipLaunchKernelGGL((k_sage_bwd_rows<2, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
                            rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
-                           0);
+                           0, rows_rev() & 1);
     else
         hipLaunchKernelGGL((k_sage_bwd_rows<1, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
                            rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
-                           0);
+                           0, rows_rev() & 1);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

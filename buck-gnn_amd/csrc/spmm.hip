@@ -61,6 +61,7 @@ struct SegArgs {
     const int32_t* grow;    // first row of each group (NULL = g * group_rows)
     int64_t n_groups;
     int32_t group_rows;
+    int32_t rev;            // row-group kernel: each eighth's groups swept from its last one down
 };
 
 // fold a lane's running max |out| into *amax: wave max, then one atomic per wave
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(256) void k_seg_combine(SegArgs A) {
 // neighbour, deg <= chunk <= 64) issued one row ahead; up to U neighbours are
 // gathered in a single batch, so a light row costs about one memory round trip.
 struct Sweep {
-    int64_t lo, first;
+    int64_t lo, hi, first;
     int W, T;
 };
 
@@ -534,6 +535,7 @@ __device__ __forceinline__ Sweep sweep_rows(int64_t n_rows, int wave) {
     const int64_t lo = n_rows * x / kNumXcd, hi = n_rows * (x + 1) / kNumXcd;
     s.W = 4 * (G >> 3);
     s.lo = lo;
+    s.hi = hi;
     s.first = lo + i * 4 + wave;
     s.T = s.first < hi ? (int)((hi - s.first + s.W - 1) / s.W) : 0;
     return s;
@@ -736,7 +738,8 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
         // and key count
         int32_t hr = 0, hn = 0, hb = 0, hc = 0;
         if (lane < ng) {
-            const int64_t gl = sw.first + (int64_t)sw.W * (t0 + lane);
+            int64_t gl = sw.first + (int64_t)sw.W * (t0 + lane);
+            if (A.rev) gl = sw.lo + sw.hi - 1 - gl;   // mirrored inside the eighth [lo, hi)
             if (A.grow) {
                 hr = A.grow[gl];
                 hn = A.grow[gl + 1] - hr;
@@ -1139,6 +1142,10 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     }
     A.rows_per_block = rpb;
     A.nt = g_seg_nt;
+    // BGNN_TUNE_ROWS_REV bit 2 (SAGE epilogue) / bit 3 (plain): sweep each eighth downward, so it
+    // starts on the rows the producing GEMM (which walks its tiles upward, one eighth per XCD)
+    // wrote last
+    A.rev = (rows_rev() >> (EPI == EPI_SAGE ? 2 : 3)) & 1;
     if (blocks_out) *blocks_out = blocks;
     A.light_slots = (int32_t)blocks;
     if (A.n_rows > 0) {
@@ -1325,6 +1332,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_GROUP_U: return g_grp_u;
         case BGNN_TUNE_GROUP_ZR_EARLY: return g_grp_ze;
         case BGNN_TUNE_SEG_COLSLICE: return g_seg_cs;
+        case BGNN_TUNE_ROWS_REV: return rows_rev();
         default: return -1;
     }
 }
@@ -1350,6 +1358,7 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             g_grp_blocks = value;
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
+        case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
         case BGNN_TUNE_GEMM_TAIL: set_gemm_tail(value ? 1 : 0); return BGNN_OK;
         case BGNN_TUNE_GROUP_U:
             BGNN_REQUIRE(value == 8 || value == 16, "set_tuning: group U must be 8 or 16");

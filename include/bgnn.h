@@ -83,6 +83,16 @@ const char* bgnn_last_error_string(void);
                                     H = 256 / 512: 1 = every XCD reduces one 128-column slice of
                                     its row region (a graph's slice of rows fits that XCD's L2),
                                     0 = whole rows                                           */
+#define BGNN_TUNE_ROWS_REV 13       /* bit 0: sage_bwd_rows / l2norm_bwd walk each block's rows from
+                                    the last one down, so they start on the rows sage_bwd_stats
+                                    read last (still in the Infinity Cache); bit 1: sage_apply
+                                    sweeps each eighth of the rows from its end, where the
+                                    aggregation wrote last; bits 2 / 3: the row-group
+                                    aggregation (SAGE / plain epilogue) sweeps each eighth
+                                    downward, starting on the rows the producing GEMM wrote
+                                    last. Bits 0 and 2 are the only knob settings that change
+                                    rounding (the order of the dh bias partials / of the
+                                    BatchNorm statistics sums; deterministic either way)      */
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);

@@ -94,6 +94,53 @@ def test_fused_layer_gemm_modes(dev, mode, aggr, red):
         _lib.call("bgnn_set_tuning", 5, 2)
 
 
+def _layer_grads(dev, H, rev):
+    from bgnn import _lib
+    b = S.make_batch(9, 3, super_node=True)
+    torch.manual_seed(3)
+    x = torch.randn(b.num_nodes, H)
+    p = make_params(H, 7)
+    graph = Graph.build(b.edge_index.to(dev), b.num_nodes, chunk=16)
+    d = {k: v.to(dev).requires_grad_(k not in ("rm", "rv")) for k, v in p.items()}
+    xd = x.to(dev).requires_grad_(True)
+    cfg = fused.LayerConfig(0, True, True, 0.1, 1e-5, True, 0.1, 123)
+    _lib.call("bgnn_set_tuning", 13, rev)
+    try:
+        out, amax = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"],
+                                         d["rm"].detach().clone(), d["rv"].detach().clone(), graph, cfg)
+        out.backward(torch.randn(out.shape, generator=torch.Generator().manual_seed(5)).to(dev))
+    finally:
+        _lib.call("bgnn_set_tuning", 13, 0)
+    return {"out": out.detach(), "amax": amax, "x": xd.grad,
+            **{k: d[k].grad for k in ("w_l", "b_l", "w_r", "gamma", "beta")}}
+
+
+@pytest.mark.parametrize("rev", [1, 2, 4, 8, 15])
+@pytest.mark.parametrize("H", [64, 512])
+def test_rows_rev_walk(dev, H, rev):
+    """BGNN_TUNE_ROWS_REV changes only the order rows are visited in. Bits 1 (sage_apply sweeps
+    each eighth of the rows from its end) and 3 (the transpose aggregation sweeps each eighth
+    downward) leave every result bit-identical; bit 0 (sage_bwd_rows walks each block's rows from
+    the last one down) changes only the order of the bias-gradient partial sums: dh, and so every
+    other gradient, is bit-identical, b_l agrees to f32 rounding; bit 2 (the SAGE aggregation
+    sweeps each eighth downward) changes the summation order of the BatchNorm statistics, so
+    everything agrees to f32 rounding. The layer still matches the oracle."""
+    a, r = _layer_grads(dev, H, 0), _layer_grads(dev, H, rev)
+    keys = ("out", "amax", "x", "w_l", "w_r", "gamma", "beta", "b_l")
+    exact = () if rev & 4 else keys[:-1] if rev & 1 else keys
+    for k in keys:
+        if k in exact:
+            assert torch.equal(a[k], r[k]), k
+        else:
+            torch.testing.assert_close(r[k], a[k], rtol=1e-4, atol=1e-5, msg=k)
+    from bgnn import _lib
+    _lib.call("bgnn_set_tuning", 13, rev)
+    try:
+        test_fused_layer_matches_oracle(dev, "sum", 0, True, True, True, H)
+    finally:
+        _lib.call("bgnn_set_tuning", 13, 0)
+
+
 def test_dropout_mask_fraction_and_backward_consistency(dev):
     H = 512
     b = S.make_batch(12, 2)
@@ -143,7 +190,7 @@ def test_dgrad_dropadd_bit_identical(dev, monkeypatch, n, drop):
         d = {k: v.to(dev).requires_grad_(k not in ("rm", "rv")) for k, v in p.items()}
         xd = x.to(dev).requires_grad_(True)
         cfg = fused.LayerConfig(0, True, True, 0.1, 1e-5, True, drop, 4242)
-        out, _ = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"],
+        out, amax = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"],
                                          d["rm"].detach().clone(), d["rv"].detach().clone(), graph, cfg)
         out.backward(up)
         res[flag] = [xd.grad] + [d[k].grad for k in ("w_l", "b_l", "w_r", "gamma", "beta")]
@@ -168,7 +215,7 @@ def test_dgrad_dropadd_small(dev, monkeypatch):
         d = {k: v.to(dev).requires_grad_(k not in ("rm", "rv")) for k, v in p.items()}
         xd = x.to(dev).requires_grad_(True)
         cfg = fused.LayerConfig(0, True, True, 0.1, 1e-5, True, 0.2, 99)
-        out, _ = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"],
+        out, amax = fused.SageLayerFn.apply(xd, None, d["w_l"], d["b_l"], d["w_r"], d["gamma"], d["beta"],
                                          d["rm"].detach().clone(), d["rv"].detach().clone(), graph, cfg)
         out.backward(up)
         res[flag] = xd.grad
