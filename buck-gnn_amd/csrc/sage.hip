@@ -502,7 +502,7 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static int g_rows_nt = 0;
 void set_rows_nt(int on) { g_rows_nt = on ? 1 : 0; }
 int rows_nt() { return g_rows_nt; }
-static int g_rows_rev = 0;
+static int g_rows_rev = 1;   // bit 0 on: bwd_rows 107.5 -> 92.9 us in the cfg2 step (profiles/r03_ab_rows_rev.txt)
 void set_rows_rev(int on) { g_rows_rev = on & 15; }
 int rows_rev() { return g_rows_rev; }
 
