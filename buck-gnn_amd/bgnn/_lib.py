@@ -67,6 +67,8 @@ SIGNATURES = {
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
                               c_p, c_p, c_p]),
+    "bgnn_spmm_bwd_add": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
+                                  c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_sage_fwd_slots": (c_i32, [ctypes.POINTER(CsrStruct)]),
     "bgnn_group_plan": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "bgnn_store_gather_groups": (c_i32, [c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64] + [c_p] * 14),

@@ -5,7 +5,8 @@ fused HIP layers (bgnn.fused) instead of per-op modules.
 Variants and where their loop is defined in the reference:
     GraphSage_addAggr / _sumAggr / _meanAggr      :430-458 -> fused (BN, ReLU, skip, dropout)
     GraphSage_addAggr_Shared (TRAIN_FINAL default)  :338-352 -> fused (no BN)
-    GraphSage_maxAggr                               :459-471 -> per-op (bgnn SAGEConv max + torch BN)
+    GraphSage_maxAggr                               :459-471 -> fused, aggregate-first (max aggregation,
+                                                       [agg | x] GEMM, same BN / ReLU / skip / dropout kernels)
     EA_GNN / EA_GNN_Shared                          :326-336,375-387 -> per-op (GraphNetBlock on bgnn scatter_mean)
     GraphSAGE_SAG                                   :190-217,493-511 -> fused SAGE layers (skip added
                                                        after dropout), SAGPooling on bgnn kernels
@@ -229,7 +230,7 @@ class BuckGNN(nn.Module):
         return self.use_fused and x.is_cuda and self.hidden_channels % 4 == 0 and self.hidden_channels <= 512
 
     def _sage_fused(self, x: Tensor, aggr: str) -> bool:
-        return self._fused_ok(x) and aggr in ("add", "sum", "mean")
+        return self._fused_ok(x) and aggr in ("add", "sum", "mean", "max")
 
     def _foldable_encoder(self, x: Tensor) -> bool:
         """The node encoder's last Linear can be folded into the first fused SAGE layer (which
@@ -246,7 +247,7 @@ class BuckGNN(nn.Module):
         p = self.dropout.p
         if self._sage_fused(x, aggr):
             graph = graph_for(edge_index, x.size(0))
-            red = 1 if aggr == "mean" else 0
+            red = {"mean": 1, "max": 2}.get(aggr, 0)
             amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
             # per-layer operand maxima and the folded layer's weight-product maxima, one fill
             scratch = torch.zeros(3 * L + 5, dtype=torch.float32, device=x.device)
@@ -343,7 +344,7 @@ class BuckGNN(nn.Module):
         # (GraphSAGE_SAG folds into sage_layers_1[0]: not when that list is empty, num_layers == 1)
         if (name in _SAGE_VARIANTS or name == "GraphSage_addAggr_Shared"
                 or (name == "GraphSAGE_SAG" and len(self.sage_layers_1) >= 1)) \
-                and self._sage_fused(x, sage) and self._foldable_encoder(x):
+                and self._sage_fused(x, sage) and sage != "max" and self._foldable_encoder(x):
             x_in = self.node_encoder[-1]
             x, x_amax = mlp(self.node_encoder[:-1], x, return_amax=True)
         elif self._fused_ok(x) and x.size(0) >= 1024 and FUSED_ENCODER:

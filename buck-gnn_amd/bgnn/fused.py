@@ -98,11 +98,36 @@ class Planes:
         return self.t.permute(1, 0, 2).reshape(self.size(0), self.size(1))
 
 
+class Pair:
+    """The row-wise concatenation [a | b] of two [rows, blk] fp32 matrices with the same row
+    stride, read in place as one GEMM A operand (the plane-split addressing of the bgnn GEMM:
+    plane 1 lives (b - a) elements after plane 0). The aggregate-first max-aggregation layer
+    multiplies [AGG x | x] by [W_l | W_r]^T this way without building the concatenation."""
+    __slots__ = ("a", "b")
+
+    def __init__(self, a: torch.Tensor, b: torch.Tensor):
+        if (a.dim() != 2 or a.shape != b.shape or a.stride() != b.stride() or a.stride(1) != 1
+                or a.dtype != torch.float32 or b.dtype != torch.float32 or a.device != b.device):
+            raise ValueError("Pair: need two fp32 [rows, blk] matrices of one shape and row stride")
+        self.a, self.b = a, b
+
+    def size(self, d):
+        return self.a.size(0) if d == 0 else 2 * self.a.size(1)
+
+    def dense(self) -> torch.Tensor:
+        return torch.cat([self.a, self.b], 1)
+
+
 def _operand(x):
-    """(ptr, ld, blk, pstride) of a dense tensor or Planes operand."""
+    """(ptr, ld, blk, pstride) of a dense tensor, Planes or Pair operand."""
     if isinstance(x, Planes):
         P, R, blk = x.t.shape
         return x.t.data_ptr(), blk, (blk if P > 1 else 0), R * blk
+    if isinstance(x, Pair):
+        diff = x.b.data_ptr() - x.a.data_ptr()
+        if diff % 4:
+            raise ValueError("Pair: the two halves must be 4-byte aligned relative to each other")
+        return x.a.data_ptr(), x.a.stride(0), x.a.size(1), diff // 4
     if x.stride(1) != 1:
         raise ValueError("gemm: operands must have unit column stride")
     return x.data_ptr(), x.stride(0), 0, 0
@@ -140,7 +165,7 @@ def gemm(a, b: torch.Tensor, trans_a: bool, trans_b: bool, out=None, beta: float
     if out.size(0) != M or out.size(1) != N:
         raise ValueError(f"gemm: out is {out.size(0)}x{out.size(1)}, expected {M}x{N}")
     if GEMM_BACKEND == "torch":
-        ad = a.dense() if isinstance(a, Planes) else a
+        ad = a.dense() if isinstance(a, (Planes, Pair)) else a
         od = out.dense() if isinstance(out, Planes) else out
         ra = ad.t() if trans_a else ad
         rb = b.t() if trans_b else b
@@ -563,6 +588,57 @@ class LayerConfig:
         self.famax = None
 
 
+def _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean, running_var, cfg: LayerConfig, next_amax):
+    """The layer glue after the normalised SAGE output o (Models/BuckGNN.py:436-444): BatchNorm
+    finalize (train: batch statistics from the aggregation's partial sums, running stats updated;
+    eval: running stats), then x_next = drop(relu(o * scale + shift) + skip * x_prev) with
+    max|x_next| folded into next_amax. Returns (x_next, (scale, shift, mean, invstd)) (None
+    coefficients without BN)."""
+    N, H = o.shape
+    dev = o.device
+    s = _stream()
+    scale = shift = mean = invstd = None
+    if cfg.bn:
+        scale = torch.empty(H, dtype=torch.float32, device=dev)
+        shift = torch.empty(H, dtype=torch.float32, device=dev)
+        mean = torch.empty(H, dtype=torch.float32, device=dev)
+        invstd = torch.empty(H, dtype=torch.float32, device=dev)
+        if cfg.training:
+            _lib.call("bgnn_bn_finalize", bn_part.data_ptr(), slots, H, N, _ptr(gamma), _ptr(beta), cfg.eps,
+                      cfg.momentum, _ptr(running_mean), _ptr(running_var), mean.data_ptr(), invstd.data_ptr(),
+                      scale.data_ptr(), shift.data_ptr(), s)
+        else:
+            _lib.call("bgnn_bn_eval_coeffs", H, _ptr(gamma), _ptr(beta), cfg.eps, running_mean.data_ptr(),
+                      running_var.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
+            mean.copy_(running_mean)
+            invstd.copy_(torch.rsqrt(running_var + cfg.eps))
+    x_next = torch.empty(N, H, dtype=torch.float32, device=dev)
+    _lib.call("bgnn_sage_apply", o.data_ptr(), _ptr(scale), _ptr(shift), x_prev.data_ptr(), int(cfg.skip),
+              float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), s)
+    return x_next, (scale, shift, mean, invstd)
+
+
+def _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg: LayerConfig):
+    """BatchNorm backward statistics of the layer glue (bgnn_sage_bwd_stats + one slot reduce):
+    (dgamma, dbeta, sum_g2, sum_g2xhat) -- all None without BN; eval mode uses zero sums."""
+    if not cfg.bn:
+        return None, None, None, None
+    N, H = o.shape
+    dev = o.device
+    s = _stream()
+    rs = _lib.query("bgnn_rows_slots", N)
+    part2 = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
+    _lib.call("bgnn_sage_bwd_stats", g.data_ptr(), o.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+              mean.data_ptr(), invstd.data_ptr(), float(cfg.p), cfg.seed, N, H, part2.data_ptr(), s)
+    sums = torch.empty(2, H, dtype=torch.float32, device=dev)
+    _lib.call("bgnn_reduce_partials", part2.data_ptr(), rs, H, sums[0].data_ptr(), sums[1].data_ptr(), 0, s)
+    dbeta, dgamma = sums[0], sums[1]
+    if cfg.training:
+        return dgamma, dbeta, sums[0], sums[1]
+    z = torch.zeros(H, dtype=torch.float32, device=dev)
+    return dgamma, dbeta, z, z
+
+
 class SageLayerFn(torch.autograd.Function):
     """Outputs (x_next, max|x_next|): the second output (non-differentiable) is the f16x3 GEMM
     operand scale of the next layer, folded in by bgnn_sage_apply at no extra pass."""
@@ -634,24 +710,8 @@ class SageLayerFn(torch.autograd.Function):
             _lib.call("bgnn_sage_fwd", graph.fwd.ref(), zl.data_ptr(), ldz, zr.data_ptr(), ldz, b_l.data_ptr(), H,
                       cfg.reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part), s)
         del z, zl, zr
-        scale = shift = mean = invstd = None
-        if cfg.bn:
-            scale = torch.empty(H, dtype=torch.float32, device=dev)
-            shift = torch.empty(H, dtype=torch.float32, device=dev)
-            mean = torch.empty(H, dtype=torch.float32, device=dev)
-            invstd = torch.empty(H, dtype=torch.float32, device=dev)
-            if cfg.training:
-                _lib.call("bgnn_bn_finalize", bn_part.data_ptr(), slots, H, N, _ptr(gamma), _ptr(beta), cfg.eps,
-                          cfg.momentum, _ptr(running_mean), _ptr(running_var), mean.data_ptr(), invstd.data_ptr(),
-                          scale.data_ptr(), shift.data_ptr(), s)
-            else:
-                _lib.call("bgnn_bn_eval_coeffs", H, _ptr(gamma), _ptr(beta), cfg.eps, running_mean.data_ptr(),
-                          running_var.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
-                mean.copy_(running_mean)
-                invstd.copy_(torch.rsqrt(running_var + cfg.eps))
-        x_next = torch.empty(N, H, dtype=torch.float32, device=dev)
-        _lib.call("bgnn_sage_apply", o.data_ptr(), _ptr(scale), _ptr(shift), x_prev.data_ptr(), int(cfg.skip),
-                  float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), s)
+        x_next, (scale, shift, mean, invstd) = _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean,
+                                                         running_var, cfg, next_amax)
         ctx.graph = graph
         ctx.cfg = cfg
         ctx.folded = folded
@@ -680,20 +740,7 @@ class SageLayerFn(torch.autograd.Function):
         dev = o.device
         s = _stream()
         bn = cfg.bn
-        dgamma = dbeta = None
-        sum_g2 = sum_g2xhat = None
-        if bn:
-            rs = _lib.query("bgnn_rows_slots", N)
-            part2 = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
-            _lib.call("bgnn_sage_bwd_stats", g.data_ptr(), o.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-                      mean.data_ptr(), invstd.data_ptr(), float(cfg.p), cfg.seed, N, H, part2.data_ptr(), s)
-            sums = torch.empty(2, H, dtype=torch.float32, device=dev)
-            _lib.call("bgnn_reduce_partials", part2.data_ptr(), rs, H, sums[0].data_ptr(), sums[1].data_ptr(), 0, s)
-            dbeta, dgamma = sums[0], sums[1]
-            if cfg.training:
-                sum_g2, sum_g2xhat = sums[0], sums[1]
-            else:
-                sum_g2 = sum_g2xhat = torch.zeros(H, dtype=torch.float32, device=dev)
+        dgamma, dbeta, sum_g2, sum_g2xhat = _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg)
         if planes:   # dz = [dz_l ; dh] as two dense [N, H] planes
             dzt = torch.empty(2, N, H, dtype=torch.float32, device=dev)
             dz, dzl, dh, lddz = Planes(dzt), dzt[0], dzt[1], H
@@ -782,33 +829,192 @@ class SageLayerFn(torch.autograd.Function):
                 None, None, None, None, None, None, None, None)
 
 
-_WPACK = {}   # (weight pointers, shape, device) -> persistent ([L, 2H, H], its transpose) pack buffers
+def _max_transform(x, w_l, w_r, graph: Graph, x_amax, w_amax, name: str):
+    """Aggregate-first SAGEConv(aggr='max') transform (max is not linear, so the transform-first
+    algebra of the sum / mean layers does not apply):
+        agg = max_{j->i} x_j                 bgnn_spmm_fwd(MAX) with the per-element CSR argmax
+        y   = [agg | x] [W_l | W_r]^T        one f16x3 GEMM, K = 2 C_in, [agg | x] read in place
+    max|[agg | x]| = max|x| (every agg element is an x element or 0), so x's maximum scales A.
+    Returns (y, agg, arg)."""
+    from .ops import spmm_fwd
+    N, C = x.shape
+    agg, arg = spmm_fwd(graph.fwd, x, 2, N, want_arg=True)
+    wk = torch.cat([w_l, w_r], 1)                                    # [H, 2C]
+    a = Pair(agg, x) if C % 32 == 0 else torch.cat([agg, x], 1)
+    with _timed(name):
+        y = gemm(a, wk, trans_a=False, trans_b=True, a_amax=x_amax, b_amax=w_amax)
+    return y, agg, arg
+
+
+def _max_rows_fwd(y, b_l, H: int):
+    """o = normalize(y + b_l), its row norms and the BatchNorm partial sums of o: bgnn_sage_fwd
+    over a CSR without entries (graph.empty_csr), i.e. the SAGE row epilogue alone (the same
+    arithmetic as the fused sum / mean layers' epilogue)."""
+    from .graph import empty_csr
+    N = y.size(0)
+    dev = y.device
+    csr = empty_csr(N, dev)
+    bias = b_l if b_l is not None else torch.zeros(H, dtype=torch.float32, device=dev)
+    o = torch.empty(N, H, dtype=torch.float32, device=dev)
+    nrm = torch.empty(N, dtype=torch.float32, device=dev)
+    slots = _lib.query("bgnn_sage_fwd_slots", csr.ref())
+    bn_part = torch.empty(slots, 2, H, dtype=torch.float32, device=dev)
+    _lib.call("bgnn_sage_fwd", csr.ref(), y.data_ptr(), y.stride(0), y.data_ptr(), y.stride(0), bias.data_ptr(), H,
+              0, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), None, _stream())
+    return o, nrm, bn_part, slots
+
+
+def _max_backward(dh, dz_amax, wcat_t, x, agg, arg, graph: Graph, x_amax, w_amax, addend_beta_src,
+                  need_dx: bool, p: float = 0.0, seed: int = 0):
+    """Backward of y = [agg | x] [W_l | W_r]^T with agg = max-aggregate(x), given dh = dL/dy:
+        dagg = dh W_l, then dx = A_max^T dagg + (dh W_r [+ drop(g)])   (bgnn_spmm_bwd_add: the
+             gradient of each (target, column) goes to its argmax edge's source, CSR-first on ties)
+        dW_l = dh^T agg,  dW_r = dh^T x
+    wcat_t = [W_l ; W_r]^T ([C, 2H]); addend_beta_src: the skip connection's incoming gradient g
+    (added through its dropout mask in the dW_r product's epilogue) or None."""
+    N, H = dh.shape
+    dev = dh.device
+    dx = None
+    if need_dx:
+        wl_t, wr_t = wcat_t[:, :H], wcat_t[:, H:]                    # W_l^T, W_r^T: [C, H], ld 2H
+        with _timed("gemm_dgrad"):
+            dagg = gemm(dh, wl_t, trans_a=False, trans_b=True, a_amax=dz_amax, b_amax=w_amax)
+            if addend_beta_src is not None and GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) == 2:
+                t = torch.empty(N, wcat_t.size(0), dtype=torch.float32, device=dev)
+                ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", N, t.size(1), H, 0, 1, 0)
+                ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
+                _lib.call("bgnn_gemm_f32_dropadd", 0, 1, N, t.size(1), H, dh.data_ptr(), dh.stride(0),
+                          wr_t.data_ptr(), wr_t.stride(0), t.data_ptr(), t.stride(0), dz_amax.data_ptr(),
+                          w_amax.data_ptr(), addend_beta_src.data_ptr(), addend_beta_src.stride(0), float(p), seed,
+                          _ptr(ws), ws_bytes, _stream())
+            else:
+                t = gemm(dh, wr_t, trans_a=False, trans_b=True, a_amax=dz_amax, b_amax=w_amax)
+                if addend_beta_src is not None:   # (torch GEMM backend / other GEMM modes: an explicit add)
+                    t.add_(_dropped(addend_beta_src, p, seed))
+        dx = torch.empty(N, x.size(1), dtype=torch.float32, device=dev)
+        bw = graph.bwd
+        part = torch.empty(bw.plan.n_chunks * x.size(1), dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
+        with _timed("spmm_bwd"):
+            _lib.call("bgnn_spmm_bwd_add", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
+                      dagg.data_ptr(), dagg.stride(0), x.size(1), 2, arg.data_ptr(), t.data_ptr(), t.stride(0),
+                      dx.data_ptr(), dx.stride(0), _ptr(part), None, _stream())
+    with _timed("gemm_wgrad"):
+        dw_l = gemm(dh, agg, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
+        dw_r = gemm(dh, x, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
+    return dx, dw_l, dw_r
+
+
+def _dropped(g, p: float, seed: int):
+    """drop(g) with the layer's counter-based mask (bgnn_add_dropout with a zero addend): the skip
+    gradient for the GEMM modes without the drop-add epilogue."""
+    out = torch.empty_like(g)
+    _lib.call("bgnn_add_dropout", g.data_ptr(), None, g.numel(), float(p), seed, out.data_ptr(), _stream())
+    return out
+
+
+class SageMaxLayerFn(torch.autograd.Function):
+    """The fused layer of GraphSage_maxAggr (Models/BuckGNN.py:165-180,459-471): SAGEConv(aggr='max',
+    normalize=True) -> BatchNorm -> ReLU -> skip -> Dropout, aggregate-first (_max_transform), then
+    the same row epilogue and glue kernels as the sum / mean layers. Outputs (x_next, max|x_next|)."""
+
+    @staticmethod
+    def forward(ctx, x_prev, x_amax, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
+                cfg: LayerConfig, amax=None, wprep=None):
+        dev = x_prev.device
+        x_prev = x_prev.contiguous()
+        H = w_l.size(0)
+        if amax is None:
+            amax = torch.zeros(3, dtype=torch.float32, device=dev)
+        w_amax, next_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
+        if wprep is not None:   # (prepare_weights has folded max|[W_l;W_r]| into the slot)
+            wcat_t = wprep[1] if wprep[1] is not None else wprep[0].t().contiguous()
+        else:
+            wcat_t = torch.cat([w_l, w_r], 0).t().contiguous()
+            absmax(wcat_t, w_amax, accumulate=True)
+        if x_amax is None:
+            x_amax = absmax(x_prev)
+        y, agg, arg = _max_transform(x_prev, w_l, w_r, graph, x_amax, w_amax, "gemm_fwd_max")
+        with _timed("sage_fwd"):
+            o, nrm, bn_part, slots = _max_rows_fwd(y, b_l, H)
+        del y
+        x_next, (scale, shift, mean, invstd) = _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean,
+                                                         running_var, cfg, next_amax)
+        ctx.graph = graph
+        ctx.cfg = cfg
+        ctx.set_materialize_grads(False)
+        e = torch.empty(0, device=dev)
+        ctx.save_for_backward(x_prev, agg, arg, o, nrm, wcat_t, gamma if gamma is not None else e,
+                              scale if scale is not None else e, shift if shift is not None else e,
+                              mean if mean is not None else e, invstd if invstd is not None else e,
+                              x_amax, w_amax, dz_amax)
+        ctx.mark_non_differentiable(next_amax)
+        return x_next, next_amax
+
+    @staticmethod
+    def backward(ctx, g, _g_amax):
+        if g is None:
+            return (None,) * 13
+        (x_prev, agg, arg, o, nrm, wcat_t, gamma, scale, shift, mean, invstd, x_amax, w_amax,
+         dz_amax) = ctx.saved_tensors
+        cfg: LayerConfig = ctx.cfg
+        g = g.contiguous()
+        N, H = o.shape
+        dev = o.device
+        s = _stream()
+        bn = cfg.bn
+        dgamma, dbeta, sum_g2, sum_g2xhat = _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg)
+        dh = torch.empty(N, H, dtype=torch.float32, device=dev)
+        rs = _lib.query("bgnn_rows_slots", N)
+        part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), o.data_ptr(), nrm.data_ptr(),
+                  _ptr(scale) if bn else None, _ptr(shift) if bn else None,
+                  _ptr(gamma) if (bn and gamma.numel()) else None,
+                  _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
+                  float(cfg.p), cfg.seed, 0, N, H, dh.data_ptr(), H, None, part_db.data_ptr(), dz_amax.data_ptr(),
+                  None, 0, s)
+        db = torch.empty(H, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
+        dx, dw_l, dw_r = _max_backward(dh, dz_amax, wcat_t, x_prev, agg, arg, ctx.graph, x_amax, w_amax,
+                                       g if cfg.skip else None, ctx.needs_input_grad[0], cfg.p, cfg.seed)
+        has_affine = bn and gamma.numel() > 0
+        return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
+                None, None, None, None, None, None)
+
+
+_WPACK = {}   # (weight pointers, shape, device) -> ([L, 2H, H] pack, its transpose, weight versions)
 
 
 def _weight_pack(pairs, L: int, H: int):
-    """Persistent [L, 2H, H] / [L, H, 2H] buffers for one layer loop's [W_l;W_r] (and transpose),
-    refilled every step by copies: a fresh torch.cat of the 2L weights each step blocked the host
-    ~0.4 ms (tools/host_profile.py). Reuse is safe on one stream: step t's backward, which reads
-    the pack, is enqueued before step t+1's refill."""
+    """[L, 2H, H] / [L, H, 2H] buffers holding one layer loop's [W_l;W_r] (and transpose), refilled
+    only when a weight changed (its autograd version moved, e.g. an optimizer step). A pack that
+    is refilled is a NEW pair of buffers, never the one a live autograd graph may have saved, so a
+    second forward before the first backward (two micro-batches, an eval forward in between)
+    keeps the first graph's operands intact. (A fresh torch.cat of the 2L weights each step
+    blocked the host ~0.4 ms, tools/host_profile.py; this is one multi-tensor copy.)"""
     dev = pairs[0][0].device
     key = (tuple((a.data_ptr(), b.data_ptr()) for a, b in pairs), L, H, dev, DGRAD_WT)
-    buf = _WPACK.get(key)
-    if buf is None:
-        if len(_WPACK) > 16:
-            _WPACK.clear()
-        W = torch.empty(L, 2 * H, H, dtype=torch.float32, device=dev)
-        Wt = torch.empty(L, H, 2 * H, dtype=torch.float32, device=dev) if DGRAD_WT else None
-        buf = _WPACK[key] = (W, Wt)
-    return buf
+    vers = tuple(t._version for pr in pairs for t in pr)
+    ent = _WPACK.get(key)
+    if ent is not None and ent[2] == vers:
+        return ent[0], ent[1]
+    if ent is None and len(_WPACK) > 16:
+        _WPACK.clear()
+    W = torch.empty(L, 2 * H, H, dtype=torch.float32, device=dev)
+    Wt = torch.empty(L, H, 2 * H, dtype=torch.float32, device=dev) if DGRAD_WT else None
+    torch._foreach_copy_([W[i, k * H:(k + 1) * H] for i in range(L) for k in (0, 1)], [t for pr in pairs for t in pr])
+    if Wt is not None:
+        Wt.copy_(W.transpose(1, 2))
+    _WPACK[key] = (W, Wt, vers)
+    return W, Wt
 
 
 def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
     """[W_l;W_r] and its transpose for every layer of a loop in a few launches (one multi-tensor
-    copy into a persistent pack, one transpose, one max|W| launch per run of layers that take it)
-    instead of three launches per layer. pairs: [(w_l, w_r)] per layer; amax_bufs: the loop's
-    zeroed [L, 3] operand-max slots, whose slot 0 receives max|[W_l;W_r]| for the layers where
-    fill_amax[i] (a folded layer scales by max|Wf| instead).
-    Returns [(wcat, wcat_t)] per layer (views of two [L, ...] buffers)."""
+    copy into a pack that is reused while the weights are unchanged, one transpose, one max|W|
+    launch per run of layers that take it) instead of three launches per layer. pairs:
+    [(w_l, w_r)] per layer; amax_bufs: the loop's zeroed [L, 3] operand-max slots, whose slot 0
+    receives max|[W_l;W_r]| for the layers where fill_amax[i] (a folded layer scales by max|Wf|
+    instead). Returns [(wcat, wcat_t)] per layer (views of two [L, ...] buffers)."""
     L = len(pairs)
     H = pairs[0][0].size(0)
     with torch.no_grad():   # operands only: the layers return the weight gradients themselves
@@ -816,10 +1022,6 @@ def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
                                     and b.is_contiguous() and a.shape == (H, H) and b.shape == (H, H)
                                     for a, b in pairs):
             W, Wt = _weight_pack(pairs, L, H)
-            torch._foreach_copy_([W[i, k * H:(k + 1) * H] for i in range(L) for k in (0, 1)],
-                                 [t for pr in pairs for t in pr])
-            if Wt is not None:
-                Wt.copy_(W.transpose(1, 2))
         else:
             W = torch.cat([t for pr in pairs for t in pr], 0).view(L, 2 * H, H)
             Wt = W.transpose(1, 2).contiguous() if DGRAD_WT else None
@@ -860,8 +1062,10 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
         raise ValueError(f"sage_layer: x has {x_prev.size(1)} features, the layer {H}")
     if H % 4 or H > 512:
         raise ValueError(f"sage_layer: fused path needs H % 4 == 0 and H <= 512 (got {H})")
-    if reduce not in (0, 1):
-        raise ValueError("sage_layer: fused path supports sum/mean aggregation only")
+    if reduce not in (0, 1, 2):
+        raise ValueError("sage_layer: reduce must be 0 (sum), 1 (mean) or 2 (max)")
+    if reduce == 2 and w_in is not None:
+        raise ValueError("sage_layer: max aggregation needs its input rows (no folded input transform)")
     if bn_module is not None:
         use_batch_stats = training or not bn_module.track_running_stats
         momentum = bn_module.momentum
@@ -875,19 +1079,27 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
         cfg.famax = fold_amax if w_in is not None else None
-        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
-                                bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in,
-                                wprep)
+        if reduce == 2:
+            out = SageMaxLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
+                                       bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, wprep)
+        else:
+            out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
+                                    bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in,
+                                    wprep)
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
         cfg.famax = fold_amax if w_in is not None else None
-        out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
-                                w_in, b_in, wprep)
+        if reduce == 2:
+            out = SageMaxLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
+                                       wprep)
+        else:
+            out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
+                                    w_in, b_in, wprep)
     return out if return_amax else out[0]
 
 
 class SageConvFn(torch.autograd.Function):
-    """One SAGEConv(normalize=True, aggr in {add, sum, mean}) module on the hand-written path:
+    """One SAGEConv(normalize=True, aggr in {add, sum, mean, max}) module on the hand-written path:
     the per-module form of SageLayerFn without the layer glue, for the PyG call surface
     (bgnn.nn.SAGEConv, i.e. the reference's unchanged Models/BuckGNN.py:434 under the shim,
     whose BatchNorm / ReLU / skip / Dropout stay torch modules).
@@ -896,7 +1108,8 @@ class SageConvFn(torch.autograd.Function):
         o = normalize(AGG z_l + z_r + b)  bgnn_sage_fwd (aggregation + bias + L2 normalize)
 
     backward: bgnn_l2norm_bwd (dh, bias-gradient partials, max|dh|), the transpose aggregation
-    dz_l = A^T dh (bgnn_spmm_bwd) and the dgrad / wgrad GEMMs on [dz_l | dh]."""
+    dz_l = A^T dh (bgnn_spmm_bwd) and the dgrad / wgrad GEMMs on [dz_l | dh].
+    aggr='max' runs aggregate-first (_max_transform / _max_rows_fwd / _max_backward)."""
 
     @staticmethod
     def forward(ctx, x, w_l, b_l, w_r, graph: Graph, reduce: int):
@@ -905,10 +1118,19 @@ class SageConvFn(torch.autograd.Function):
         N = x.size(0)
         H = w_l.size(0)
         wcat = torch.cat([w_l, w_r], 0).contiguous()            # [2H, C_in]
-        amax = torch.zeros(3, dtype=torch.float32, device=dev)   # max|W|, max|x|, max|dz|
-        w_amax, x_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
+        amax = torch.zeros(2, dtype=torch.float32, device=dev)   # max|W|, max|x|
+        w_amax, x_amax = amax[0:1], amax[1:2]
         absmax(wcat, w_amax, accumulate=True)
         absmax(x, x_amax, accumulate=True)
+        ctx.graph = graph
+        ctx.reduce = reduce
+        ctx.has_bias = b_l is not None
+        if reduce == 2:   # aggregate-first (max is not linear): SageMaxLayerFn's transform + row epilogue
+            y, agg, arg = _max_transform(x, w_l, w_r, graph, x_amax, w_amax, "conv_gemm_fwd")
+            with _timed("conv_sage_fwd"):
+                o, nrm, _, _ = _max_rows_fwd(y, b_l, H)
+            ctx.save_for_backward(x, o, nrm, wcat, x_amax, w_amax, agg, arg)
+            return o
         with _timed("conv_gemm_fwd"):
             z = gemm(x, wcat, trans_a=False, trans_b=True, a_amax=x_amax, b_amax=w_amax)   # [N, 2H]
         bias = b_l if b_l is not None else torch.zeros(H, dtype=torch.float32, device=dev)
@@ -922,31 +1144,35 @@ class SageConvFn(torch.autograd.Function):
             _lib.call("bgnn_sage_fwd", graph.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H,
                       bias.data_ptr(), H, reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part),
                       _stream())
-        ctx.graph = graph
-        ctx.reduce = reduce
-        ctx.has_bias = b_l is not None
-        ctx.save_for_backward(x, o, nrm, wcat, x_amax, w_amax, dz_amax)
+        ctx.save_for_backward(x, o, nrm, wcat, x_amax, w_amax)
         return o
 
     @staticmethod
     def backward(ctx, g):
-        x, o, nrm, wcat, x_amax, w_amax, dz_amax = ctx.saved_tensors
+        x, o, nrm, wcat, x_amax, w_amax = ctx.saved_tensors[:6]
         graph: Graph = ctx.graph
         g = g.contiguous()
         N, H = o.shape
         dev = o.device
         s = _stream()
-        dz = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)   # [dz_l | dh]
-        dh = dz[:, H:]
+        mx = ctx.reduce == 2
+        # max aggregation: dh alone ([N, H]); sum / mean: dz = [dz_l | dh] for the K = 2H GEMMs
+        dz = torch.empty(N, H if mx else 2 * H, dtype=torch.float32, device=dev)
+        dh = dz if mx else dz[:, H:]
         rs = _lib.query("bgnn_rows_slots", N)
         part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
-        dz_amax.zero_()
-        _lib.call("bgnn_l2norm_bwd", g.data_ptr(), o.data_ptr(), nrm.data_ptr(), N, H, dh.data_ptr(), 2 * H,
+        dz_amax = torch.zeros(1, dtype=torch.float32, device=dev)   # max|dz| (fresh: re-entrant backward)
+        _lib.call("bgnn_l2norm_bwd", g.data_ptr(), o.data_ptr(), nrm.data_ptr(), N, H, dh.data_ptr(), dh.stride(0),
                   part_db.data_ptr(), dz_amax.data_ptr(), s)
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = torch.empty(H, dtype=torch.float32, device=dev)
             _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
+        if mx:
+            agg, arg = ctx.saved_tensors[6:]
+            dx, dw_l, dw_r = _max_backward(dh, dz_amax, wcat.t().contiguous(), x, agg, arg, graph, x_amax, w_amax,
+                                           None, ctx.needs_input_grad[0])
+            return dx, dw_l, db, dw_r, None, None
         bw = graph.bwd
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("conv_spmm_bwd"):
@@ -966,6 +1192,6 @@ class SageConvFn(torch.autograd.Function):
 
 def sage_conv(x: torch.Tensor, w_l: torch.Tensor, b_l, w_r: torch.Tensor, graph: Graph, reduce: int):
     """normalize(lin_l(AGG x) + lin_r(x)) of one SAGEConv module on the hand-written path
-    (SageConvFn); reduce 0 = sum/add, 1 = mean."""
+    (SageConvFn); reduce 0 = sum/add, 1 = mean, 2 = max (aggregate-first)."""
     require_cuda(x, w_l, w_r, what="sage_conv")
     return SageConvFn.apply(x, w_l, b_l, w_r, graph, reduce)

@@ -270,6 +270,24 @@ class _Cache:
 
 _graph_cache = _Cache()
 _index_cache = _Cache()
+_empty_csrs = {}
+
+
+def empty_csr(n_rows: int, device) -> Csr:
+    """A CSR of n_rows rows without entries (cached per size and device). bgnn_sage_fwd over it
+    is the SAGE row epilogue alone -- o_i = normalize(z_r[i] + b), its norm and the BatchNorm
+    partial sums -- which the aggregate-first max-aggregation layer (bgnn.fused) applies to its
+    GEMM output."""
+    key = (int(n_rows), str(device))
+    c = _empty_csrs.get(key)
+    if c is None:
+        if len(_empty_csrs) > 8:
+            _empty_csrs.clear()
+        dev = torch.device(device)
+        z = torch.zeros(1, dtype=torch.int32, device=dev)
+        plan = Plan(z, torch.zeros(2, dtype=torch.int32, device=dev), z, 0, 0, DEFAULT_CHUNK)
+        c = _empty_csrs[key] = Csr(torch.zeros(n_rows + 1, dtype=torch.int32, device=dev), z, n_rows, 0, plan)
+    return c
 
 
 def graph_for(edge_index: torch.Tensor, num_nodes: int, chunk: int = DEFAULT_CHUNK) -> Graph:

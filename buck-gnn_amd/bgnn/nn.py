@@ -93,7 +93,7 @@ class SAGEConv(nn.Module):
             # L2 normalize, with its own backward (bgnn.fused.SageConvFn)
             from .fused import sage_conv
             return sage_conv(x_src, self.lin_l.weight, self.lin_l.bias, self.lin_r.weight, graph,
-                             1 if self.aggr == "mean" else 0)
+                             {"mean": 1, "max": 2}.get(self.aggr, 0))
         if self.aggr in ("add", "sum", "mean") and 2 * self.out_channels <= self.in_channels[0]:
             # narrow output (e.g. SAGPooling's 1-channel scorer): transform first, then aggregate
             # the narrow rows -- lin_l(AGG x) = AGG(x W_l^T) + b_l, since sum / mean are linear
@@ -109,12 +109,12 @@ class SAGEConv(nn.Module):
         return out
 
     def _fast(self, x_src: Tensor, x_dst: Tensor) -> bool:
-        """Whether this call runs on bgnn.fused.SageConvFn: normalize=True, sum/mean
+        """Whether this call runs on bgnn.fused.SageConvFn: normalize=True, sum/mean/max
         aggregation, root weight, no projection, fp32 CUDA input, out_channels a multiple of
         4 up to 512 and not narrower than half the input (the narrow scorer of SAGPooling
         aggregates its 1-wide transform instead)."""
         return (FAST_SAGECONV and self.normalize and self.root_weight and not self.project
-                and self.aggr in ("add", "sum", "mean") and x_src is x_dst and x_src.is_cuda
+                and self.aggr in ("add", "sum", "mean", "max") and x_src is x_dst and x_src.is_cuda
                 and x_src.dtype == torch.float32 and x_src.dim() == 2
                 and self.out_channels % 4 == 0 and 4 <= self.out_channels <= 512
                 and 2 * self.out_channels > self.in_channels[0] and self.in_channels[0] % 4 == 0

@@ -149,6 +149,7 @@ class GradAllReduce:
         while self._next < len(self._buckets) and self._ready[self._next] == len(self._buckets[self._next][0]):
             params, flat, views = self._buckets[self._next]
             torch._foreach_copy_(views, [q.grad for q in params])
+            flat[-len(params):].fill_(1.0)   # every parameter of the bucket has a gradient on this rank
             self._works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
             self._next += 1
 
@@ -169,11 +170,13 @@ class GradAllReduce:
         self._seen = []
         if self.world > 1:
             dev = params[0].device if params else torch.device("cpu")
+            # the group's rank 0 as a global rank (broadcast's src is global)
+            src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
             n = torch.tensor([len(order)], dtype=torch.long, device=dev)
-            dist.broadcast(n, 0, group=self.group)
+            dist.broadcast(n, src, group=self.group)
             ref = torch.tensor(order if dist.get_rank(self.group) == 0 else [0] * int(n.item()),
                                dtype=torch.long, device=dev)
-            dist.broadcast(ref, 0, group=self.group)
+            dist.broadcast(ref, src, group=self.group)
             ref = ref.tolist()
             ok = torch.tensor([int(sorted(ref) == sorted(order))], dtype=torch.long, device=dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
@@ -194,7 +197,11 @@ class GradAllReduce:
         self._buckets = []
         self.layout = [[index[id(p)] for p in b] for b in buckets]   # parameter indices per bucket
         for b, bparams in enumerate(buckets):
-            flat = torch.empty(sum(p.numel() for p in bparams), dtype=bparams[0].dtype, device=bparams[0].device)
+            # [gradients | one "had a gradient" flag per parameter]: the flags are summed with the
+            # gradients, so after the all-reduce a parameter some rank used is told apart from one
+            # no rank used (which keeps grad None, as under DDP: Adam then skips it)
+            flat = torch.empty(sum(p.numel() for p in bparams) + len(bparams), dtype=bparams[0].dtype,
+                               device=bparams[0].device)
             views, off = [], 0
             for p in bparams:
                 views.append(flat[off:off + p.numel()].view_as(p))
@@ -204,16 +211,18 @@ class GradAllReduce:
         self._ready = [0] * len(self._buckets)
 
     def _launch_rest(self) -> None:
-        """Launch the buckets whose gradients did not all arrive this step, with zeros for the
-        missing ones (DDP's semantics for a parameter unused on one rank), so every rank still
-        issues the same collective sequence."""
+        """Launch the buckets whose gradients did not all arrive this step, with zeros (and a zero
+        flag) for the missing ones, so every rank still issues the same collective sequence."""
         while self._next < len(self._buckets):
             params, flat, views = self._buckets[self._next]
-            for p, v in zip(params, views):
+            flags = flat[-len(params):]
+            for i, (p, v) in enumerate(zip(params, views)):
                 if p.grad is None:
                     v.zero_()
+                    flags[i].fill_(0.0)
                 else:
                     v.copy_(p.grad)
+                    flags[i].fill_(1.0)
             self._works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
             self._next += 1
 
@@ -228,10 +237,18 @@ class GradAllReduce:
             inv = 1.0 / self.world
             for params, flat, views in self._buckets:
                 flat.mul_(inv)
-                for p in params:
-                    if p.grad is None:   # (unused on this rank this step: takes the others' average)
-                        p.grad = torch.zeros_like(p)
-                torch._foreach_copy_([p.grad for p in params], views)
+                if any(p.grad is None for p in params):
+                    # unused on this rank this step: it takes the others' average (DDP), unless no
+                    # rank used it -- then it keeps no gradient (one host read, this path only)
+                    used = flat[-len(params):].tolist()
+                    keep = [i for i, p in enumerate(params) if p.grad is not None or used[i] > 0]
+                    for i in keep:
+                        if params[i].grad is None:
+                            params[i].grad = torch.zeros_like(params[i])
+                    if keep:
+                        torch._foreach_copy_([params[i].grad for i in keep], [views[i] for i in keep])
+                else:
+                    torch._foreach_copy_([p.grad for p in params], views)
             extra = self._extra
             self._extra = []
             self._works, self._next = [], 0

@@ -212,7 +212,9 @@ __global__ __launch_bounds__(256) void k_rel_error_loss(const float* __restrict_
         const float d = fabsf(q) + eps;
         const float diff = p - q;
         acc += (double)(fabsf(diff) / d);
-        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+        // sign(diff), NaN propagated (torch's abs backward: sgn(NaN) = NaN), so a diverging
+        // prediction does not get a silent zero gradient
+        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : (diff == 0.f ? 0.f : diff));
         if (dpred) dpred[i] = sg * scale / d * inv_n;
     }
     red[t] = acc;

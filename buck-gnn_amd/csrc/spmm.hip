@@ -54,6 +54,8 @@ struct SegArgs {
     int32_t light_slots;
     int32_t nt;         // stream-once data (z_r rows, output rows) with non-temporal hints
     uint32_t* amax;     // plain epilogue: max |out| folded in (f32 bits, atomic max; NULL = off)
+    const float* add;   // plain epilogue: out[r] += add[r] (NULL = off; bgnn_spmm_bwd_add)
+    int64_t ld_add;
     // row-group plan (bgnn_group_plan): NULL = none
     const int32_t* gsrc;
     const uint8_t* gmask;
@@ -239,8 +241,14 @@ __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& 
             float t = acc.a[v][k];
             if constexpr (OP == OP_MAX) t = (deg > 0) ? t : 0.f;
             o.f[k] = t * sc;
-            tmax = max(tmax, __float_as_uint(o.f[k]) & 0x7fffffffu);
         }
+        if (A.add) {
+            const Vec<VEC> ad = ld<VEC>(A.add + r * A.ld_add + cpos[v]);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) o.f[k] += ad.f[k];
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) tmax = max(tmax, __float_as_uint(o.f[k]) & 0x7fffffffu);
         if constexpr (VEC == 4) {
             if (A.nt) st_nt(A.out + r * A.ldo + cpos[v], o);
             else st<VEC>(A.out + r * A.ldo + cpos[v], o);
@@ -1282,10 +1290,24 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
     }
 }
 
+extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                                 const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                                 const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
+                                 float* amax, void* stream);
+
 extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                              const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
                              float* gx, int64_t ldgx, float* partial, float* amax, void* stream) {
+    return bgnn_spmm_bwd_add(csr_t, perm_t, fwd_rowptr, g, ldg, H, reduce, arg, nullptr, 0, gx, ldgx, partial, amax,
+                             stream);
+}
+
+extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                                 const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                                 const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
+                                 float* amax, void* stream) {
     BGNN_REQUIRE(csr_t && csr_t->rowptr, "spmm_bwd: null csr");
+    BGNN_REQUIRE(!addend || ld_add >= H, "spmm_bwd: bad ld_add");
     BGNN_REQUIRE(H > 0 && ldg >= H && ldgx >= H, "spmm_bwd: bad H/ld");
     BGNN_REQUIRE(csr_t->n_chunks == 0 || partial, "spmm_bwd: partial scratch required");
     SegArgs A = args_from_csr(csr_t);
@@ -1297,8 +1319,11 @@ extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, con
     A.perm_t = perm_t;
     A.arg_in = arg;
     A.amax = reinterpret_cast<uint32_t*>(amax);
+    A.add = addend;
+    A.ld_add = ld_add;
     const bool al = aligned16(g) && aligned16(gx) && ldg % 4 == 0 && ldgx % 4 == 0 &&
-                    (!partial || aligned16(partial)) && (!arg || aligned16(arg));
+                    (!partial || aligned16(partial)) && (!arg || aligned16(arg)) &&
+                    (!addend || (aligned16(addend) && ld_add % 4 == 0));
     const Geometry geo = pick_geometry(H, al);
     hipStream_t s = as_stream(stream);
     switch (reduce) {

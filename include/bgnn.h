@@ -197,6 +197,14 @@ int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H,
 int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                   const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
                   float* gx, int64_t ldgx, float* partial, float* amax, void* stream);
+/* bgnn_spmm_bwd with an addend: gx[j] = (A^T g)[j] + addend[j] (addend [rows, H], ld ld_add),
+ * added after the reduction, in the same pass. The max-aggregation SAGEConv backward
+ * (aggregate-first form) adds the lin_r input gradient dh W_r (+ the skip gradient) to the
+ * scattered lin_l gradient this way (bgnn/fused.py). */
+int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                      const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                      const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
+                      float* amax, void* stream);
 
 /* ------------------------------------------------------------------------
  * Fused SAGE layer (Models/BuckGNN.py:430-444, transform-first order):

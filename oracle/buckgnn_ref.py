@@ -109,13 +109,15 @@ def graphnet_block(sd: Dict[str, Tensor], pre: str, x: Tensor, edge_index: Tenso
 
 
 def ea_forward(sd: Dict[str, Tensor], x: Tensor, edge_index: Tensor, edge_attr: Tensor, batch: Optional[Tensor],
-               training: bool, dropout: float = 0.0, num_layers: int = 6) -> Tensor:
-    """EA_GNN forward (Models/BuckGNN.py:323,375-387,515-516) with mean pooling."""
+               training: bool, dropout: float = 0.0, num_layers: int = 6, shared: bool = False) -> Tensor:
+    """EA_GNN forward (Models/BuckGNN.py:323,375-387,515-516) with mean pooling; shared=True:
+    EA_GNN_Shared (:326-336), one GraphNetBlock (`shared_gn_block`) applied num_layers times
+    with the same skip / dropout pattern."""
     x = _mlp(sd, "node_encoder", x)
     e = _mlp(sd, "edge_encoder", edge_attr)
     for i in range(num_layers):
         x_prev, e_prev = x, e
-        x, e = graphnet_block(sd, f"gn_blocks.{i}", x, edge_index, e)
+        x, e = graphnet_block(sd, "shared_gn_block" if shared else f"gn_blocks.{i}", x, edge_index, e)
         if 0 < i < num_layers - 1:
             x, e = x + x_prev, e + e_prev
         x, e = F.dropout(x, dropout, training), F.dropout(e, dropout, training)

@@ -16,9 +16,49 @@ from torch import Tensor, nn
 
 
 # ----------------------------------------------------------------------------- scatter
+class _ScatterMaxFirst(torch.autograd.Function):
+    """Segment max along dim 0 whose gradient goes to the FIRST position (in src order) that
+    attains the maximum of its (segment, column): torch_scatter's scatter_max convention
+    (its CPU kernel keeps the first strict '>' winner as `arg`; the backward scatters the whole
+    output gradient to `arg`). Empty segments give 0 and pass no gradient.
+
+    Tie convention (SURVEY §7 "Max aggregation tie-breaking"): PyG's `utils.scatter(reduce='max')`
+    calls torch_scatter when it is installed and the input is a CUDA tensor that requires grad
+    (one winner per tie; on CUDA the winner among ties is unspecified), and
+    `Tensor.scatter_reduce_('amax')` otherwise (the gradient split evenly over the ties). The
+    reference imports torch_scatter (Models/BuckGNN.py:6) and trained on CUDA, so the one-winner
+    form is the reference's; the first occurrence is its deterministic instance, the one
+    bgnn's kernels implement (csrc/spmm.hip: strict '>' in CSR = edge_index order)."""
+
+    @staticmethod
+    def forward(ctx, src, index, dim_size):
+        idx = index.view(-1, *([1] * (src.dim() - 1))).expand_as(src)
+        out = src.new_zeros((dim_size,) + tuple(src.shape[1:])).scatter_reduce_(0, idx, src, reduce="amax",
+                                                                                 include_self=False)
+        n = src.size(0)
+        pos = torch.arange(n, device=src.device).view(-1, *([1] * (src.dim() - 1))).expand_as(src)
+        hit = src == out.index_select(0, index)
+        first = torch.full(out.shape, n, dtype=torch.long, device=src.device)
+        first.scatter_reduce_(0, idx, torch.where(hit, pos, torch.full_like(pos, n)), reduce="amin",
+                              include_self=True)
+        ctx.save_for_backward(first)
+        ctx.n = n
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (first,) = ctx.saved_tensors
+        n = ctx.n
+        valid = first < n
+        gs = g.new_zeros((n + 1,) + tuple(g.shape[1:]))   # row n absorbs the empty segments
+        gs.scatter_(0, torch.where(valid, first, torch.full_like(first, n)), torch.where(valid, g, torch.zeros_like(g)))
+        return gs[:n], None, None
+
+
 def scatter(src: Tensor, index: Tensor, dim_size: int, reduce: str) -> Tensor:
     """Segment reduce along dim 0 (torch_scatter / PyG utils.scatter semantics):
-    sum, mean (sum / max(count, 1)), max (empty segments -> 0)."""
+    sum, mean (sum / max(count, 1)), max (empty segments -> 0; gradient to the first maximum,
+    _ScatterMaxFirst)."""
     out_shape = (dim_size,) + tuple(src.shape[1:])
     if reduce in ("sum", "add"):
         return src.new_zeros(out_shape).index_add_(0, index, src)
@@ -28,8 +68,7 @@ def scatter(src: Tensor, index: Tensor, dim_size: int, reduce: str) -> Tensor:
             0, index, torch.ones(index.numel(), dtype=src.dtype, device=src.device))
         return s / cnt.clamp_min(1).view(-1, *([1] * (src.dim() - 1)))
     if reduce == "max":
-        idx = index.view(-1, *([1] * (src.dim() - 1))).expand_as(src)
-        return src.new_zeros(out_shape).scatter_reduce_(0, idx, src, reduce="amax", include_self=False)
+        return _ScatterMaxFirst.apply(src, index, dim_size)
     raise ValueError(reduce)
 
 

@@ -48,6 +48,11 @@ CASES = [
     ("shared_h512", "GraphSage_addAggr_Shared", 512, "mean", [(6, False, 12)], False),
     ("add_h256", "GraphSage_addAggr", 256, "mean", [(5, False, 13), (5, True, 14)], False),
     ("ea_gnn_h64", "EA_GNN", 64, "mean", [(4, False, 15), (5, False, 16)], False),
+    # round 4: EA_GNN_Shared (Models/BuckGNN.py:103-104,326-336; a TRAIN_FINAL.py:66,81 choice) and
+    # max aggregation at the production size (aggregate-first hand-written path, super-node
+    # heavy rows of the max kernel)
+    ("ea_gnn_shared_h64", "EA_GNN_Shared", 64, "mean", [(4, False, 40), (5, False, 41)], True),
+    ("max_h512_n1k", "GraphSage_maxAggr", 512, "mean", [(23, False, 42), (23, True, 43)], False),
     # SAGPooling variants (Models/BuckGNN.py:190-244,354-373,493-511)
     ("sag_h64", "GraphSAGE_SAG", 64, "mean", [(5, False, 17), (6, False, 18), (4, False, 19)], True),
     ("sag_super_h64", "GraphSAGE_SAG", 64, "mean", [(5, True, 20), (4, True, 21)], True),

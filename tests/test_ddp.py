@@ -127,3 +127,64 @@ def test_grad_allreduce_overlapped_buckets_gloo_world2():
 
 
 PORT = _free_port()
+
+
+class Optional_(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.layers = torch.nn.ModuleList([torch.nn.Linear(16, 16) for _ in range(3)])
+        self.opt = torch.nn.Linear(16, 16)
+
+    def forward(self, x, use_opt: bool):
+        for l in self.layers:
+            x = torch.relu(l(x))
+        return self.opt(x) if use_opt else x
+
+
+def _worker_unused(rank, world, port, q):
+    """Hook-launched buckets when a module is skipped after the recording step: by one rank (it
+    takes the other rank's gradient / world, like DDP) and by every rank (it keeps grad None, so
+    the optimizer skips it)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bgnn
+
+    torch.manual_seed(0)
+    m = Optional_()
+    ar = bgnn.GradAllReduce(m, bucket_mb=0.001)
+    res = []
+    for step, use in enumerate([(True, True), (True, False), (False, False)]):
+        torch.manual_seed(100 * step + rank)
+        m.zero_grad(set_to_none=True)
+        m(torch.randn(8, 16), use[rank]).pow(2).sum().backward()
+        own = None if m.opt.weight.grad is None else m.opt.weight.grad.clone()
+        ar()
+        res.append((own, None if m.opt.weight.grad is None else m.opt.weight.grad.clone(),
+                    m.layers[0].weight.grad.clone()))
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_unused_after_recording_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_unused, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0, r1 = res[0], res[1]
+    # step 1: rank 1 skipped `opt`: both ranks hold rank 0's gradient / 2
+    own0 = r0[1][0]
+    assert r1[1][0] is None
+    torch.testing.assert_close(r0[1][1], own0 / 2)
+    torch.testing.assert_close(r1[1][1], own0 / 2)
+    # step 2: no rank used it: no gradient anywhere; the used layers are still averaged
+    assert r0[2][1] is None and r1[2][1] is None
+    torch.testing.assert_close(r0[2][2], r1[2][2])

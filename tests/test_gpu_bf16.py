@@ -249,3 +249,19 @@ def test_rel_error_loss_kernel_matches_torch(dev):
     torch.testing.assert_close(got, ref, rtol=1e-6, atol=0)
     torch.testing.assert_close(ggot, 3.0 * gref, rtol=1e-6, atol=0)
     assert T._fused_loss(crit, norm, p2, y.view(-1)) is None   # broadcasting shapes: torch path
+
+
+def test_rel_error_loss_kernel_propagates_nan(dev):
+    """A NaN prediction gives a NaN loss AND a NaN gradient in that position (torch's abs
+    backward propagates it), not a silent zero; the other positions keep their gradients."""
+    from bgnn import train as T
+    pred = torch.tensor([0.3, float("nan"), -0.7, 1.1], device=dev, requires_grad=True)
+    y = torch.tensor([0.5, 0.4, -0.2, 1.0], device=dev)
+    crit, norm = T.RelativeErrorLoss(), T.EigenvalueScaler(center=0.5, scale=2.0)
+    got = T._fused_loss(crit, norm, pred, y)
+    (g,) = torch.autograd.grad(got, pred)
+    ref = crit(norm.denormalize_eigenvalue(pred), norm.denormalize_eigenvalue(y))
+    (gref,) = torch.autograd.grad(ref, pred)
+    assert torch.isnan(got) and torch.isnan(ref)
+    assert torch.isnan(g[1]) and torch.isnan(gref[1])
+    torch.testing.assert_close(g[[0, 2, 3]], gref[[0, 2, 3]], rtol=1e-6, atol=0)

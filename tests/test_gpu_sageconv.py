@@ -33,7 +33,7 @@ def _run(dev, aggr, H, Cin, super_node, bias=True, seed=0):
     return conv, ref, out, ro, xd, xr
 
 
-@pytest.mark.parametrize("aggr", ["add", "sum", "mean"])
+@pytest.mark.parametrize("aggr", ["add", "sum", "mean", "max"])
 @pytest.mark.parametrize("H,Cin", [(64, 64), (512, 512), (512, 128)])
 @pytest.mark.parametrize("super_node", [False, True])
 def test_sageconv_module_fast_path_matches_oracle(dev, monkeypatch, aggr, H, Cin, super_node):

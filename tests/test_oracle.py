@@ -35,6 +35,24 @@ def test_kat_sum_mean_max_on_path_graph():
     assert torch.equal(P.sage_aggregate(x, ei, "add"), s)
 
 
+def test_kat_max_ties_first_occurrence_gets_gradient():
+    """Tie convention of max aggregation (oracle/pyg_ref._ScatterMaxFirst): the first edge in
+    edge_index order that attains the maximum of its (target, column) takes the whole gradient
+    (torch_scatter's argmax form; ReLU zeros tie in practice). Targets: 0 <- {1, 2, 3},
+    1 <- {2, 0}; node 2 has no in-edges."""
+    x = torch.tensor([[0.0, 5.0], [0.0, 1.0], [0.0, 5.0], [-1.0, 5.0]], requires_grad=True)
+    ei = torch.tensor([[1, 2, 3, 2, 0], [0, 0, 0, 1, 1]])
+    out = P.sage_aggregate(x, ei, "max")
+    assert torch.equal(out.detach(), torch.tensor([[0.0, 5.0], [0.0, 5.0], [0.0, 0.0], [0.0, 0.0]]))
+    g = torch.tensor([[1.0, 10.0], [100.0, 1000.0], [7.0, 7.0], [9.0, 9.0]])
+    out.backward(g)
+    # target 0: column 0 ties at 0 between sources 1 and 2 -> source 1 (first edge); column 1
+    # ties at 5 between sources 2 and 3 -> source 2. Target 1: both columns tie between sources
+    # 2 and 0 -> source 2 (the first edge, although node 0 has the lower index)
+    exp = torch.tensor([[0.0, 0.0], [1.0, 0.0], [100.0, 10.0 + 1000.0], [0.0, 0.0]])
+    assert torch.equal(x.grad, exp)
+
+
 def test_kat_duplicate_edges_count_twice_and_self_loops():
     x = torch.tensor([[1.0], [10.0]])
     ei = torch.tensor([[1, 1, 0], [0, 0, 0]])   # 1->0 twice, self loop 0->0
@@ -145,7 +163,8 @@ def test_ea_oracle_matches_reference_golden(path):
     """oracle.buckgnn_ref.ea_forward (EA_GNN, Models/BuckGNN.py:375-387,528-566) against the
     golden vectors of the reference's own EA_GNN: prediction, loss, every gradient."""
     z, meta = load_case(path)
-    assert meta["model_name"] == "EA_GNN"
+    assert meta["model_name"] in ("EA_GNN", "EA_GNN_Shared")
+    shared = meta["model_name"] == "EA_GNN_Shared"
     sd = oracle_state(meta, reference_shapes(meta))
     x = torch.from_numpy(z["x"])
     ei = torch.from_numpy(z["edge_index"])
@@ -153,7 +172,7 @@ def test_ea_oracle_matches_reference_golden(path):
     batch = torch.from_numpy(z["batch"])
     y = torch.from_numpy(z["y"])
     step = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
-    pred = R.ea_forward(step, x, ei, ea, batch, True, 0.0, meta["num_layers"])
+    pred = R.ea_forward(step, x, ei, ea, batch, True, 0.0, meta["num_layers"], shared)
     loss = R.relative_error_loss(pred, y)
     loss.backward()
     np.testing.assert_allclose(pred.detach().numpy().reshape(-1), z["pred_train"], rtol=2e-5, atol=2e-5)
@@ -168,7 +187,7 @@ def test_ea_oracle_matches_reference_golden(path):
             n += 1
     assert n > 0
     with torch.no_grad():
-        pe = R.ea_forward(step, x, ei, ea, batch, False, 0.0, meta["num_layers"])
+        pe = R.ea_forward(step, x, ei, ea, batch, False, 0.0, meta["num_layers"], shared)
     np.testing.assert_allclose(pe.numpy().reshape(-1), z["pred_eval"], rtol=2e-5, atol=2e-5)
 
 
