@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lock = threading.Lock()
 _lib = None
@@ -99,9 +99,6 @@ SIGNATURES = {
     "bgnn_gemm_b16_variant": (c_i32, [c_i32]),
     "bgnn_add_dropout_bf16": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p, c_p]),
     "bgnn_segment_sum_bf16": (c_i32, [c_p, c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p]),
-    "bgnn_split_f16x2": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p]),
-    "bgnn_gemm_p16": (c_i32, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_p, c_i64, c_p,
-                              c_i32, c_p, c_p, c_i64, c_f32, c_u64, c_i32, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
     "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
     "bgnn_gemm_f32_planes": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,

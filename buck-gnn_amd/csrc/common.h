@@ -82,13 +82,6 @@ static inline uint32_t dropout_threshold(float p) {
 // GEMM kernel family (gemm.hip): 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (f32-accurate split products)
 void set_gemm_mode(int mode);
 int gemm_mode();
-// f16x3 operand staging: -1 = register-staged (gemm_x6.hip) always, v >= 0 = LDS-DMA kernel
-// variant v (gemm_h3g.hip) where the shape allows
-void set_gemm_staging(int v);
-int gemm_staging();
-// tail split of tall f16x3 GEMMs whose last 256x256 tile round is under-filled (gemm.hip)
-void set_gemm_tail(int on);
-int gemm_tail();
 // non-temporal output stores of the row-wise SAGE kernels (sage.hip)
 void set_rows_nt(int on);
 int rows_nt();

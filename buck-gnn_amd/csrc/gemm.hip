@@ -311,18 +311,14 @@ constexpr GemmCfg kCfgs[] = {
 constexpr int kNumCfgs = 9;
 static int g_gemm_cfg = -1;   // -1 = automatic
 static int g_gemm_abl = 0;    // ablation (measurement only)
-static int g_gemm_mode = 2;   // 0 = f32 MFMA kernel, 1 = bf16x6, 2 = f16x3 (gemm_x6.hip, default:
-                              // half the MFMAs of bf16x6, error below the f32 MFMA's; tools/tune_gemm.py)
-
-static int g_gemm_staging = -1;   // f16x3 staging: -1 register-staged, else gemm_h3g.hip variant
+static int g_gemm_mode = 2;   // 0 = f32 MFMA kernel (gemm.hip), 2 = f16x3 (gemm_x6.hip, default: error
+                              // below the f32 MFMA's at 3 f16 MFMAs per product; tools/tune_gemm.py)
 
 void set_gemm_mode(int mode) { g_gemm_mode = mode; }
 int gemm_mode() { return g_gemm_mode; }
-void set_gemm_staging(int v) { g_gemm_staging = v; }
-int gemm_staging() { return g_gemm_staging; }
 
 
-// bf16x6 / f16x3 tile choice (tools/tune_gemm.py)
+// f16x3 / bf16-operand tile choice (tools/tune_gemm.py)
 // f16x3 (MI355X, tools/gemm_one.py under rocprofv3, cfg2 SAGE shapes): fwd 80656x1024x512
 // 256x256 tiles 293 us (256x128: 341); dgrad 80656x512x1024 128x256 311 us (256x128: 329,
 // 256x256: 323, under-filled last wave); wgrad 1024x512x80656 256x256 + split-K 302 us
@@ -397,52 +393,11 @@ extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
 // Launch plan of one GEMM call: kernel family, tile config and split-K factor.
 struct Plan {
     int x6;            // 1 = split-precision kernel (gemm_x6.hip), 0 = f32 MFMA
-    int prec;          // split kernel: 0 = bf16x6, 1 = f16x3
+    int prec;          // split kernel: 1 = f16x3, 2 = bf16 operands
     int cfg;           // index into kX6Cfgs / kCfgs
     int bm, bn, bk;    // tile
     int split;
-    // tail split (f16x3 tall products whose last round of 256x256 tiles would run under-filled):
-    // rows [0, rows_a) as whole rounds of 256x256 tiles, rows [rows_a, M) as 256x256 tiles with
-    // split-K tail_split (+ slab reduce). rows_a = M: off.
-    int64_t rows_a;
-    int tail_split;
 };
-
-constexpr int kNumCUs = 256;              // MI355X: one 256x256 f16x3 workgroup per CU (128 KB LDS)
-// tail split (A/B knob BGNN_TUNE_GEMM_TAIL), off by default: measured in the cfg2 train step
-// (tools/ab_step.py, MI355X) 9.96 ms/step with it against 9.89 ms with the 128x256 dgrad tiles
-static int g_gemm_tail = 0;
-namespace bgnn {
-void set_gemm_tail(int on) { g_gemm_tail = on; }
-int gemm_tail() { return g_gemm_tail; }
-}  // namespace bgnn
-
-// dgrad 80656x512x1024 runs 128x256 tiles (1,262 tiles = 4.93 rounds) because 256x256 tiles
-// leave the third round half empty (632 tiles = 2.47 rounds), yet a 256x256 tile does twice the
-// MFMA work per operand byte. Tail split: two full rounds of 256x256 tiles over the first
-// 65,536 rows, and the remaining 120 tiles as 240 half-K pieces (one round) + a slab reduce.
-// Measured slower than the 128x256 tiles in the train step (see g_gemm_tail): kept as a knob.
-static void plan_tail(Plan& p, int64_t M, int64_t N, int64_t K, int ta, int64_t a_blk, int64_t c_blk) {
-    p.rows_a = M;
-    p.tail_split = 1;
-    if (!g_gemm_tail || g_gemm_cfg >= 0 || !p.x6 || p.prec != 1 || p.cfg != 2 || p.split != 1 || ta != 0 ||
-        a_blk != 0 || c_blk != 0 || K < 512 || K % 64 != 0)
-        return;
-    const int64_t tcols = (N + 255) / 256;
-    const int64_t trows = (M + 255) / 256;
-    const int64_t tiles = trows * tcols;
-    const int64_t full = tiles / kNumCUs;                  // whole rounds
-    const int64_t rem = tiles - full * kNumCUs;
-    if (full < 1 || rem == 0 || 4 * rem > 3 * kNumCUs) return;   // last round >= 3/4 full: keep
-    const int64_t rows_a = (full * kNumCUs / tcols) * 256;
-    if (rows_a <= 0 || rows_a >= M) return;
-    const int64_t tail_tiles = ((M - rows_a + 255) / 256) * tcols;
-    if (2 * tail_tiles > kNumCUs) return;                  // the halved tail must fit one round
-    p.cfg = 4;
-    p.bm = 256; p.bn = 256;
-    p.rows_a = rows_a;
-    p.tail_split = 2;
-}
 
 static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk,
                       int precision = 0) {
@@ -454,23 +409,19 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         if (a_blk != 0 || c_blk != 0) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves, kX6Cfgs[p.cfg].blocks_per_cu});
-        p.rows_a = M;
-        p.tail_split = 1;
         return p;
     }
     auto planes_ok = [&](int bm, int bn, int bk) {
         return (a_blk == 0 || a_blk % (ta ? bm : bk) == 0) && (c_blk == 0 || c_blk % bn == 0);
     };
-    if (g_gemm_mode >= 1) {
+    if (g_gemm_mode == 2) {
         p.x6 = 1;
-        p.prec = g_gemm_mode == 2 ? 1 : 0;
+        p.prec = 1;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
-        if (p.prec == 0 && p.cfg > 2) p.cfg = 1;   // 256x256 tiles exceed the LDS with three pieces
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves,
                                                  kX6Cfgs[p.cfg].blocks_per_cu});
-        plan_tail(p, M, N, K, ta, a_blk, c_blk);
         return p;
     } else {
         p.cfg = pick_cfg(M, N, K, ta, tb);
@@ -481,15 +432,7 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.bm = c.bm; p.bn = c.bn; p.bk = c.bk;
         p.split = choose_split(M, N, K, c);
     }
-    p.rows_a = M;
-    p.tail_split = 1;
     return p;
-}
-
-// the LDS-DMA staged f16x3 kernel for tall K-contiguous products (fwd / dgrad of the SAGE
-// layers, the EA_GNN edge MLPs) when the staging knob selects it and the shape qualifies
-static bool use_h3g(const Plan& p, int ta, int tb, const GemmArgs& g) {
-    return g_gemm_staging >= 0 && p.x6 && p.prec == 1 && g.M >= 4096 && g.N >= 256 && h3g_ok(g, ta, tb);
 }
 
 // workspace: [256 B operand-max head (f16x3)] [split-K slabs]
@@ -497,7 +440,6 @@ constexpr size_t kAmaxHead = 256;
 
 static size_t ws_need(const Plan& p, int64_t M, int64_t N) {
     const size_t head = (p.x6 && p.prec == 1) ? kAmaxHead : 0;
-    if (p.rows_a < M) return head + (size_t)p.tail_split * (size_t)(M - p.rows_a) * (size_t)N * sizeof(float);
     return head + (p.split > 1 ? (size_t)p.split * (size_t)M * (size_t)N * sizeof(float) : 0);
 }
 
@@ -643,15 +585,11 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
     }
     float* slabs = ws ? reinterpret_cast<float*>(static_cast<char*>(ws) + head) : nullptr;
     const size_t slab_bytes = ws_bytes > head ? ws_bytes - head : 0;
-    const int64_t Mt = M - pl.rows_a;   // tail rows (tail split), 0 = none
-    if (Mt > 0 && (slabs == nullptr || slab_bytes < (size_t)pl.tail_split * Mt * N * sizeof(float))) {
-        return fail(BGNN_E_WS, "gemm: workspace too small for the tail split (need bgnn_gemm_ws_bytes_ex())");
-    }
-    int split = Mt > 0 ? 1 : pl.split;
+    int split = pl.split;
     if (split > 1 && (slabs == nullptr || slab_bytes < (size_t)split * M * N * sizeof(float))) split = 1;
     if (st & 4) split = 1;   // (a bf16 C has no f32 slab reduce)
-    if (bs.src) {   // the masked beta source lives in the split kernels' epilogue: no split-K, no tail
-        BGNN_REQUIRE(pl.x6 && pl.prec == 1 && Mt == 0, "gemm_dropadd: needs the f16x3 kernels without a tail split");
+    if (bs.src) {   // the masked beta source lives in the split kernels' epilogue: no split-K
+        BGNN_REQUIRE(pl.x6 && pl.prec == 1, "gemm_dropadd: needs the f16x3 kernels");
         split = 1;
     }
     if ((st & 3) == 3 && alpha == 1.f && beta == 0.f) {   // bf16-stored A and B: the LDS-DMA bf16 kernel, all rows
@@ -664,7 +602,7 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
             return BGNN_OK;
         }
     }
-    const int64_t Ma = pl.rows_a;
+    const int64_t Ma = M;
     GemmArgs g{A, B, C, slabs, Ma, N, K, lda, ldb, ldc, alpha, beta, 0, split, bias, relu,
                a_blk, a_pstride, c_blk, c_pstride, a_amax, b_amax, nullptr};
     g.st = st;
@@ -676,15 +614,14 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
         g.dkeep = g.dthr ? 1.f / (1.f - bs.p) : 1.f;
     }
     // max |C| for the next GEMM's operand scale: in the split kernels' epilogue, else one pass
-    const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1 && Mt == 0;
+    const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1;
     if (c_amax_fused) g.c_amax = c_amax;
     int64_t kc = (K + split - 1) / split;
     kc = (kc + pl.bk - 1) / pl.bk * pl.bk;
     g.kchunk = kc > 0 ? kc : pl.bk;
     const int64_t tiles_a = ((Ma + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
     dim3 grid((unsigned)tiles_a, split);
-    if (!bs.src && use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, Ma, N), s, g);
-    else if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, bs.src ? 8 : g_gemm_abl, grid, s, g);
+    if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, bs.src ? 8 : g_gemm_abl, grid, s, g);
     else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
     else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
     else if (ta == 1 && tb == 0) launch_cfg<1, 0>(pl.cfg, grid, s, g);
@@ -692,21 +629,6 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
     BGNN_CHECK_LAUNCH();
     if (split > 1) {
         const int rc = launch_splitk_reduce(slabs, split, M, N, alpha, beta, C, ldc, bias, relu, c_blk, c_pstride, s);
-        if (rc != BGNN_OK) return rc;
-    }
-    if (Mt > 0) {   // tail rows: 256x256 tiles, split-K over tail_split slabs, then the slab reduce (f16x3 only)
-        GemmArgs t = g;
-        t.A = A + Ma * lda;
-        t.C = C + Ma * ldc;
-        t.M = Mt;
-        t.split = pl.tail_split;
-        t.c_amax = nullptr;
-        int64_t tk = (K + t.split - 1) / t.split;
-        t.kchunk = (tk + pl.bk - 1) / pl.bk * pl.bk;
-        const int64_t tiles_t = ((Mt + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
-        launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles_t, t.split), s, t);
-        BGNN_CHECK_LAUNCH();
-        const int rc = launch_splitk_reduce(slabs, t.split, Mt, N, alpha, beta, t.C, ldc, bias, relu, 0, 0, s);
         if (rc != BGNN_OK) return rc;
     }
     if (c_amax != nullptr && !c_amax_fused) {
@@ -758,10 +680,7 @@ static int gather_add_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t
     BGNN_REQUIRE(ldc >= N || M == 0, "gemm_gather_add: bad ldc");
     if (M == 0 || N == 0) return BGNN_OK;
     Plan pl = make_plan(M, N, K, ta, tb, 0, 0, precision);
-    BGNN_REQUIRE(pl.x6, "gemm_gather_add: needs the split GEMM family (BGNN_TUNE_GEMM_MODE 1 or 2)");
-    if (pl.rows_a < M) {   // no split-K here (the gathered epilogue): the plain 128x256 tiles
-        pl.cfg = 2; pl.bm = 128; pl.bn = 256; pl.rows_a = M; pl.tail_split = 1;
-    }
+    BGNN_REQUIRE(pl.x6, "gemm_gather_add: needs the split GEMM family (BGNN_TUNE_GEMM_MODE 2)");
     const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
     BGNN_REQUIRE(tiles < (int64_t(1) << 31), "gemm_gather_add: too many tiles");
     hipStream_t s = as_stream(stream);
@@ -785,7 +704,6 @@ static int gather_add_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t
     g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;
     if (g.kchunk == 0) g.kchunk = pl.bk;
     if (b16_ok(g, ta, tb)) launch_b16(s, g);   // bf16-stored A and B: the LDS-DMA bf16 kernel
-    else if (use_h3g(pl, ta, tb, g)) launch_h3g(g_gemm_staging, h3g_tiles(g_gemm_staging, M, N), s, g);
     else launch_x6(pl.prec, ta, tb, pl.cfg, 0, dim3((unsigned)tiles, 1), s, g);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;

@@ -70,7 +70,7 @@ __device__ __forceinline__ const float* plane_base(const float* P, int64_t x0, i
     return P + plane * (pstride - blk);
 }
 
-// f32-accurate GEMMs on 16-bit MFMAs (gemm_x6.hip): prec 0 = bf16x6, 1 = f16x3; launches the
+// GEMMs on 16-bit MFMAs (gemm_x6.hip): prec 1 = f16x3 (f32-accurate), 2 = bf16 operands; launches the
 // main kernel of tile config `cfg` (index into kX6Cfgs) on grid (tiles, split); abl != 0
 // selects a timing ablation.
 struct X6Cfg {
@@ -79,13 +79,6 @@ struct X6Cfg {
 extern const X6Cfg kX6Cfgs[];
 extern const int kNumX6Cfgs;
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
-// f16x3 with LDS-DMA staging (gemm_h3g.hip): h3g_ok = the shape and operands qualify (ta 0,
-// tb 1, dense 16-B aligned A and B, K % 32 == 0, no split-K, scales supplied); launches
-// variant `variant` on the grid of h3g_tiles(variant, M, N) output tiles
-bool h3g_ok(const GemmArgs& g, int ta, int tb);
-int64_t h3g_tiles(int variant, int64_t M, int64_t N);
-void launch_h3g(int variant, int64_t tiles, hipStream_t s, const GemmArgs& g);
-constexpr int kNumH3gVariants = 2;
 // bf16-operand GEMM on bf16-STORED A and B (gemm_b16.hip): b16_ok = the call qualifies (ta 0,
 // tb 1, storage bits 0 and 1, K % 64 == 0, dense 16-B aligned rows, no split-K / drop-add);
 // launch_b16 covers all M rows (no tail split; tile / persistent form picked per call)

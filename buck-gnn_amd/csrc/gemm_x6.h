@@ -1,6 +1,5 @@
-// Split-precision GEMM tile helpers shared by gemm_x6.hip (register-staged kernels) and
-// gemm_h3g.hip (LDS-DMA staged f16x3 kernel): operand piece splits, the f16x3 operand
-// scale and the LDS-staged C epilogue.
+// Split-precision GEMM tile helpers of gemm_x6.hip (and the bf16 C stores gemm_b16.hip shares):
+// operand piece splits, the f16x3 operand scale and the LDS-staged C epilogue.
 #pragma once
 #include "common.h"
 #include "gemm_common.h"
@@ -17,17 +16,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16(float x, float y) {
     const f32x2 v = {x, y};
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
-}
-
-// exact three-way split of (x, y) into packed bf16 pieces
-__device__ __forceinline__ void split2(float x, float y, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
-    p0 = pack_bf16(x, y);
-    x -= __uint_as_float(p0 << 16);
-    y -= __uint_as_float(p0 & 0xffff0000u);
-    p1 = pack_bf16(x, y);
-    x -= __uint_as_float(p1 << 16);
-    y -= __uint_as_float(p1 & 0xffff0000u);
-    p2 = pack_bf16(x, y);
 }
 
 // two f32 -> packed f16x2 (round to nearest even; v_cvt_pk_f16_f32)

@@ -14,25 +14,14 @@
 // Elements below 2^-39 max|A| (f16 subnormal range after scaling) lose relative precision;
 // their absolute error stays below 2^-39 max|A| |b|.
 //
-// PREC 0 = bf16x6:
-//
-// Every f32 operand element is split exactly into three bf16 pieces by round-to-nearest:
-//   a0 = bf16(a), a1 = bf16(a - a0), a2 = bf16(a - a0 - a1),  a = a0 + a1 + a2
-// (|a1| <= 2^-8 |a|, |a2| <= 2^-16 |a|; each residual is exact in f32). The product is
-//   a.b = a0.b0 + (a0.b1 + a1.b0) + (a0.b2 + a1.b1 + a2.b0) + O(2^-23 |a||b|)
-// i.e. six bf16 MFMAs per f32 product, every bf16 x bf16 product exact in f32 and all
-// accumulation in the f32 MFMA accumulator. The three dropped terms are at most
-// 2^-23 |a||b| together, the size of one f32 rounding of the product, so the result sits in
-// the same error class as the f32 MFMA kernel (measured against fp64 in
-// tests/test_gpu_gemm.py), at 6 x 32 = 192 MFMA cycles per 32x32x16 block instead of
-// 8 x 64 = 512 for the f32 MFMA.
-//
 // Tiling: BM x BN output tile per workgroup, waves WM x WN, each wave (BM/WM) x (BN/WN) in
 // 32x32 MFMA tiles; K in BK = 32 slices, double-buffered in LDS. Global operands are read as
 // f32 (float4 when K-contiguous, coalesced dwords along M/N when transposed), split in
-// registers and stored as three bf16 row images [R][32] per operand (K contiguous, 64-B
-// rows, 16-B chunks XOR-swizzled by (row >> 2) & 3 so a 16-lane ds_read_b128 group hits 16
-// distinct bank quads). Each MFMA operand is one ds_read_b128 per piece per lane.
+// registers and stored as 16-bit row images [R][32] per piece (K contiguous, 64-B rows, 16-B
+// chunks XOR-swizzled by (row >> 2) & 3 so a 16-lane ds_read_b128 group hits 16 distinct
+// bank quads). Each MFMA operand is one ds_read_b128 per piece per lane. (A bf16x6 family --
+// three exact bf16 pieces, six products -- was measured and dropped in round 2: f16x3 halves
+// its MFMAs at a lower error.)
 #include <type_traits>
 
 #include "common.h"
@@ -129,7 +118,7 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
             S[pos] = q0;
             continue;
         }
-        if constexpr (PREC == 1) {
+        {
             uint4 q0, q1;
             if constexpr (ABL == 1) {
                 q0.x = pack_f16(v[u][0], v[u][1]); q0.y = pack_f16(v[u][2], v[u][3]);
@@ -143,22 +132,7 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
             }
             S[pos] = q0;
             S[R * 4 + pos] = q1;
-            continue;
         }
-        uint4 q0, q1, q2;
-        if constexpr (ABL == 1) {
-            q0.x = pack_bf16(v[u][0], v[u][1]); q0.y = pack_bf16(v[u][2], v[u][3]);
-            q0.z = pack_bf16(v[u][4], v[u][5]); q0.w = pack_bf16(v[u][6], v[u][7]);
-            q1 = q0; q2 = q0;
-        } else {
-            split2(v[u][0], v[u][1], q0.x, q1.x, q2.x);
-            split2(v[u][2], v[u][3], q0.y, q1.y, q2.y);
-            split2(v[u][4], v[u][5], q0.z, q1.z, q2.z);
-            split2(v[u][6], v[u][7], q0.w, q1.w, q2.w);
-        }
-        S[pos] = q0;
-        S[R * 4 + pos] = q1;
-        S[2 * R * 4 + pos] = q2;
     }
 }
 
@@ -227,7 +201,7 @@ __device__ __forceinline__ void kq_store(uint4* __restrict__ S, const float (&v)
 
 
 
-// the six leading piece products of one 16-deep k-step, small terms first
+// the leading piece products of one 16-deep k-step, small terms first
 template <int TM, int TN, int PREC, int NP>
 __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa)[TM][NP],
                                        const uint4 (&fb)[TN][NP]) {
@@ -240,22 +214,10 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[i][0]), as_bf16x8(fb[j][0]), t, 0, 0, 0);
                 continue;
             }
-            if constexpr (PREC == 1) {   // f16x3: the two cross terms, then the leading product
-                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][0]), t, 0, 0, 0);
-                acc[i][j] = t;
-                continue;
-            }
-            bf16x8 a[3], b[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) { a[p] = as_bf16x8(fa[i][p < NP ? p : 0]); b[p] = as_bf16x8(fb[j][p < NP ? p : 0]); }
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], t, 0, 0, 0);
+            // f16x3: the two cross terms, then the leading product
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][0]), t, 0, 0, 0);
             acc[i][j] = t;
         }
 }
@@ -264,8 +226,7 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
 // ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored in
 // every piece slot), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA +
 // barriers), 4 = MFMA + barriers only, 5 = everything but the C stores, 6 = cached C stores,
-// 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands,
-// 9 / 10 = s_setprio(1) around the MFMA block forced on / off (scheduling only; results unchanged).
+// 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands.
 // ABL >= 16: not an ablation but the bf16 STORAGE flags ST = ABL - 16 of the bf16-operand family
 // (PREC 2): bit 0 = A, bit 1 = B, bit 2 = C stored as bf16 (EA_GNN's per-edge activations).
 template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL_ = 0>
@@ -274,8 +235,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int ABL = ABL_ >= 16 ? 0 : ABL_;
     constexpr bool A16 = (ST & 1) != 0, B16 = (ST & 2) != 0, C16 = (ST & 4) != 0;
     static_assert(ST == 0 || PREC == 2, "bf16 storage is for the bf16-operand family only");
+    static_assert(PREC == 1 || PREC == 2, "f16x3 (1) or bf16 operands (2)");
     constexpr int NT = 64 * WM * WN;
-    constexpr int NP = PREC == 1 ? 2 : (PREC == 2 ? 1 : 3);   // pieces per operand
+    constexpr int NP = PREC == 1 ? 2 : 1;   // pieces per operand
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
@@ -339,11 +301,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
     constexpr bool kStage = ABL != 3 && ABL != 4, kLoad = kStage && ABL != 2;
-    // ABL 9: the MFMA block at s_setprio 1 (guide T5). Measured and not adopted: in an
-    // interleaved A/B (tools/prio_ab.py, cold cache) it lost on every SAGE shape -- fwd 317 ->
-    // 341 us, dgrad 324 -> 359, wgrad 303 -> 406 (a one-off sequential run had suggested a fwd
-    // gain). ABL 10 = the default (no priority change), kept for the A/B.
-    constexpr bool kPrio = ABL == 9;
+    // (s_setprio(1) around the MFMA block, guide T5, measured in round 3 and dropped: fwd 317 ->
+    // 341 us, dgrad 324 -> 359, wgrad 303 -> 406 in an interleaved A/B, profiles/r03_*)
     // the main loop is instantiated twice (interior tiles without guards, edge tiles with
     // them) and selected once, so the hot loop carries no per-slice bounds branches
     auto mainloop = [&](auto full_tag) {
@@ -401,9 +360,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             if (kt + 1 + PF < nk && kLoad) load_ab(kb + (kt + 1 + PF) * X6_BK, r);
             // keep the staging (split VALU, LDS writes, global loads) out of the MFMA block
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);
             mma_slice(cur, kt);
-            if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
             __syncthreads();
         };
         if (nk > 0) {
@@ -473,14 +430,10 @@ static void launch_x6_t(int cfg, int abl, dim3 grid, hipStream_t s, const GemmAr
             case 4: launch_x6_a<PREC, TA, TB, 4>(cfg, grid, s, g); break;
             case 5: launch_x6_a<PREC, TA, TB, 5>(cfg, grid, s, g); break;
             case 6: launch_x6_a<PREC, TA, TB, 6>(cfg, grid, s, g); break;
-            case 9: launch_x6_a<PREC, TA, TB, 9>(cfg, grid, s, g); break;
-            case 10: launch_x6_a<PREC, TA, TB, 10>(cfg, grid, s, g); break;
             default: launch_x6_a<PREC, TA, TB, 7>(cfg, grid, s, g); break;
         }
-    } else if constexpr (TA == 1 && TB == 0) {   // wgrad: ablations 7 (dword k-major staging), 9, 10 (priority)
+    } else if constexpr (TA == 1 && TB == 0) {   // wgrad: ablation 7 (dword k-major staging)
         if (abl == 7) launch_x6_a<PREC, TA, TB, 7>(cfg, grid, s, g);
-        else if (abl == 9) launch_x6_a<PREC, TA, TB, 9>(cfg, grid, s, g);
-        else if (abl == 10) launch_x6_a<PREC, TA, TB, 10>(cfg, grid, s, g);
         else launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);
     } else {
         launch_x6_a<PREC, TA, TB, 0>(cfg, grid, s, g);
@@ -511,8 +464,7 @@ static void launch_prec(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if (prec == 2 && g.st != 0) launch_x6_bf16_storage(ta, tb, cfg, g.st, grid, s, g);
     else if (prec == 2) launch_prec<2>(ta, tb, cfg, 0, grid, s, g);
-    else if (prec == 1) launch_prec<1>(ta, tb, cfg, abl, grid, s, g);
-    else launch_prec<0>(ta, tb, cfg > 2 ? 1 : cfg, abl, grid, s, g);
+    else launch_prec<1>(ta, tb, cfg, abl, grid, s, g);
 }
 
 // max |x| over a strided (optionally plane-split) matrix, folded into *out by an unsigned

@@ -715,9 +715,9 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
 // per row and column: VALU, hidden under the loads). Groups are swept per XCD like rows in
 // k_seg_sweep. Per row, the entries are summed in plan order (deterministic; for the group's
 // first row it is CSR order), so results match the sweep kernel to rounding, not bitwise.
-// ZE (SAGE epilogue): issue the group's z_r row loads before its gathers (they complete under
-// them) instead of after (one more round trip per group, fewer VGPRs held).
-template <int NV, int OP, int EPI, int R, int U, int ZE = 0>
+// (Measured in round 2 and dropped: issuing the group's z_r loads before its gathers, 160 -> 188
+// us, and 16 source rows per gather batch, 160 -> 168 us; profiles/r02_tune_agg_knobs.txt.)
+template <int NV, int OP, int EPI, int R, int U>
 __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -781,16 +781,6 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                 sl_n = lane < c ? A.gsrc[b + lane] : 0;
                 ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
             }
-            constexpr bool kZE = EPI == EPI_SAGE && ZE != 0;
-            Vec<4> zre[kZE ? R : 1][NV];
-            if constexpr (kZE) {
-#pragma unroll
-                for (int t = 0; t < R; ++t) {
-                    const int64_t r = r0 + (t < rows ? t : 0);
-#pragma unroll
-                    for (int v = 0; v < NV; ++v) zre[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
-                }
-            }
             float a[R][NV][4];
 #pragma unroll
             for (int t = 0; t < R; ++t)
@@ -849,10 +839,7 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                 for (int t = 0; t < R; ++t) {
                     const int64_t r = r0 + (t < rows ? t : 0);
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        if constexpr (kZE) zr[t][v] = zre[kZE ? t : 0][v];
-                        else zr[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
-                    }
+                    for (int v = 0; v < NV; ++v) zr[t][v] = ld_nt(A.zr + r * A.ldzr + (cok[v] ? cpos[v] : 0));
                 }
 #pragma unroll
                 for (int t = 0; t < R; ++t) {
@@ -925,136 +912,6 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// Column-slice row-group kernel (plain epilogue: the transpose aggregation dz_l = A^T dh;
-// SUM / MEAN / MEANT, H = 128 S with S = 2 or 4 slices, groups of R rows).
-//
-// Why: a 71x71 mesh graph's [5041, 512] f32 rows are 10 MB, and its random virtual edges
-// (GraphCreate.py / VirtualEdgeCreate.py) gather from anywhere in the graph, so with whole
-// rows an XCD's 4 MB L2 misses on most of them. Here XCD x reduces only column slice
-// c = x mod S (128 columns = 512 B per row) over row region x / S of 8 / S: a graph's slice
-// of rows is 2.5 MB at H = 512 and stays in that XCD's L2 while the sweep front crosses
-// the graph. Lane l owns columns 128 c + 2 l, 2 l + 1 (one 8-B load per source row and
-// lane, 512 B per wave load). Per row and column the entries are summed in plan order with
-// the same roundings as k_seg_group, so the result is bit-identical to it.
-template <int OP, int S, int R, int U>
-__global__ __launch_bounds__(256) void k_seg_group_cs(SegArgs A) {
-    static_assert(S == 2 || S == 4, "column slices: 2 or 4");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr int NREG = kNumXcd / S;
-    const int x = blockIdx.x & 7, ib = blockIdx.x >> 3;
-    const int cs = x % S, reg = x / S;
-    const int64_t lo = A.n_groups * reg / NREG, hi = A.n_groups * (reg + 1) / NREG;
-    const int W = 4 * ((int)gridDim.x >> 3);
-    const int64_t first = lo + ib * 4 + wave;
-    const int T = first < hi ? (int)((hi - first + W - 1) / W) : 0;
-    const int col = cs * 128 + 2 * lane;
-    const int32_t chunk = A.chunk;
-    uint32_t tmax = 0;
-
-    for (int t0 = 0; t0 < T; t0 += 64) {
-        const int ng = min(64, T - t0);
-        int32_t hr = 0, hn = 0, hb = 0, hc = 0;
-        if (lane < ng) {
-            const int64_t gl = first + (int64_t)W * (t0 + lane);
-            if (A.grow) {
-                hr = A.grow[gl];
-                hn = A.grow[gl + 1] - hr;
-            } else {
-                hr = (int32_t)(gl * R);
-                hn = (int32_t)min((int64_t)R, A.n_rows - hr);
-            }
-            hb = A.rowptr[hr];
-            hc = A.gcnt[gl];
-        }
-        int32_t rp_n, sl_n;
-        uint32_t ml_n;
-        {
-            const int64_t r0 = __builtin_amdgcn_readlane(hr, 0);
-            rp_n = lane <= R ? A.rowptr[min(r0 + lane, A.n_rows)] : 0;
-            const int32_t b = __builtin_amdgcn_readlane(hb, 0), c = __builtin_amdgcn_readlane(hc, 0);
-            sl_n = lane < c ? A.gsrc[b + lane] : 0;
-            ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
-        }
-        for (int k = 0; k < ng; ++k) {
-            const int64_t r0 = __builtin_amdgcn_readlane(hr, k);
-            const int rows = __builtin_amdgcn_readlane(hn, k);
-            const int32_t base = __builtin_amdgcn_readlane(hb, k), cnt = __builtin_amdgcn_readlane(hc, k);
-            const int32_t rp = rp_n, sl0 = sl_n;
-            const uint32_t ml0 = ml_n;
-            if (k + 1 < ng) {
-                const int64_t r1 = __builtin_amdgcn_readlane(hr, k + 1);
-                rp_n = lane <= R ? A.rowptr[min(r1 + lane, A.n_rows)] : 0;
-                const int32_t b = __builtin_amdgcn_readlane(hb, k + 1), c = __builtin_amdgcn_readlane(hc, k + 1);
-                sl_n = lane < c ? A.gsrc[b + lane] : 0;
-                ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
-            }
-            float a[R][2];
-#pragma unroll
-            for (int t = 0; t < R; ++t) a[t][0] = a[t][1] = 0.f;
-            for (int32_t eb = 0; eb < cnt; eb += 64) {
-                const int n = min(64, cnt - eb);
-                int32_t sl = sl0;
-                uint32_t ml = ml0;
-                if (eb > 0) {
-                    sl = lane < n ? A.gsrc[base + eb + lane] : 0;
-                    ml = lane < n ? (uint32_t)A.gmask[base + eb + lane] : 0u;
-                }
-                for (int u0 = 0; u0 < n; u0 += U) {
-                    int32_t j[U];
-                    uint32_t m[U];
-                    float w[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const bool ok = u0 + u < n;
-                        const int kk = ok ? u0 + u : u0;
-                        j[u] = __builtin_amdgcn_readlane(sl, kk);
-                        m[u] = ok ? (uint32_t)__builtin_amdgcn_readlane((int)ml, kk) : 0u;
-                        w[u] = 1.f;
-                        if constexpr (OP == OP_MEANT) {
-                            const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
-                            w[u] = inv_deg(d);
-                        }
-                    }
-                    float2 val[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        val[u] = *reinterpret_cast<const float2*>(A.x + (int64_t)j[u] * A.ldx + col);
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const float x0 = (OP == OP_MEANT) ? __fmul_rn(val[u].x, w[u]) : val[u].x;
-                        const float x1 = (OP == OP_MEANT) ? __fmul_rn(val[u].y, w[u]) : val[u].y;
-#pragma unroll
-                        for (int t = 0; t < R; ++t) {
-                            const bool on = (m[u] >> t) & 1u;
-                            a[t][0] += on ? x0 : 0.f;
-                            a[t][1] += on ? x1 : 0.f;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < R; ++t) {
-                const int64_t r = r0 + t;
-                const int32_t rb = __builtin_amdgcn_readlane(rp, t);
-                const int32_t deg = __builtin_amdgcn_readlane(rp, t + 1) - rb;
-                if (t >= rows || deg > chunk) continue;   // heavy row: chunk + combine
-                const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
-                f32x2_t o;
-                o[0] = a[t][0] * sc;
-                o[1] = a[t][1] * sc;
-                tmax = max(tmax, __float_as_uint(o[0]) & 0x7fffffffu);
-                tmax = max(tmax, __float_as_uint(o[1]) & 0x7fffffffu);
-                f32x2_t* dst = reinterpret_cast<f32x2_t*>(A.out + r * A.ldo + col);
-                if (A.nt) __builtin_nontemporal_store(o, dst);
-                else *dst = o;
-            }
-        }
-    }
-    amax_flush_wave(A.amax, tmax);
-}
-
-// ---------------------------------------------------------------------------
 constexpr int kMaxLightBlocks = 1024;
 
 // Tuning knobs (process-wide; defaults are the production choice; see bgnn_set_tuning).
@@ -1063,10 +920,6 @@ static int g_seg_kernel = 0;     // 0 = auto (row-group kernel where planned, el
 static int g_grp_blocks = 1024;  // row-group kernel grid (4 blocks of 4 waves per CU)
 static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
 static int g_seg_nt = 1;         // non-temporal hints on stream-once data (default on: +8 % fwd)
-static int g_grp_u = 8;          // source rows per gather batch in the row-group kernel (8 or 16)
-static int g_grp_ze = 0;         // row-group SAGE epilogue: z_r loads before the gathers (0/1)
-static int g_seg_cs = 0;         // row-group plain epilogue: per-XCD column slices (0 = off, 1 = U 16,
-                                 // 2 = U 8)
 static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto = 12:
                                  // mesh rows have 8 neighbours + ~1 virtual edge, one batch)
 
@@ -1158,30 +1011,10 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     A.light_slots = (int32_t)blocks;
     if (A.n_rows > 0) {
         if constexpr (VEC == 4 && LPR == 64 && (OP == OP_SUM || OP == OP_MEAN || OP == OP_MEANT)) {
-            const bool cs = group && EPI == EPI_PLAIN && OP != OP_MAX && g_seg_cs && A.group_rows == 4 &&
-                            (A.H == 512 || A.H == 256) && A.ldx % 2 == 0 && A.ldo % 2 == 0;
-            if (cs) {
+            if (group) {
                 const dim3 gr((unsigned)blocks);
-                if (A.H == 512) {
-                    if (g_seg_cs == 2) hipLaunchKernelGGL((k_seg_group_cs<OP, 4, 4, 8>), gr, dim3(256), 0, s, A);
-                    else hipLaunchKernelGGL((k_seg_group_cs<OP, 4, 4, 16>), gr, dim3(256), 0, s, A);
-                } else {
-                    if (g_seg_cs == 2) hipLaunchKernelGGL((k_seg_group_cs<OP, 2, 4, 8>), gr, dim3(256), 0, s, A);
-                    else hipLaunchKernelGGL((k_seg_group_cs<OP, 2, 4, 16>), gr, dim3(256), 0, s, A);
-                }
-                BGNN_CHECK_LAUNCH();
-            } else if (group) {
-                const dim3 gr((unsigned)blocks);
-                constexpr int ZE = EPI == EPI_SAGE ? 1 : 0;   // (plain epilogue: no z_r variant)
-                const bool ze = ZE && g_grp_ze;
                 if (A.group_rows == 8)
                     hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 8>), gr, dim3(256), 0, s, A);
-                else if (g_grp_u == 16 && ze)
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 16, ZE>), gr, dim3(256), 0, s, A);
-                else if (g_grp_u == 16)
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 16>), gr, dim3(256), 0, s, A);
-                else if (ze)
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8, ZE>), gr, dim3(256), 0, s, A);
                 else
                     hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8>), gr, dim3(256), 0, s, A);
                 BGNN_CHECK_LAUNCH();
@@ -1352,11 +1185,6 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_GEMM_MODE: return gemm_mode();
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
-        case BGNN_TUNE_GEMM_STAGING: return gemm_staging();
-        case BGNN_TUNE_GEMM_TAIL: return gemm_tail();
-        case BGNN_TUNE_GROUP_U: return g_grp_u;
-        case BGNN_TUNE_GROUP_ZR_EARLY: return g_grp_ze;
-        case BGNN_TUNE_SEG_COLSLICE: return g_seg_cs;
         case BGNN_TUNE_ROWS_REV: return rows_rev();
         default: return -1;
     }
@@ -1384,25 +1212,9 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
-        case BGNN_TUNE_GEMM_TAIL: set_gemm_tail(value ? 1 : 0); return BGNN_OK;
-        case BGNN_TUNE_GROUP_U:
-            BGNN_REQUIRE(value == 8 || value == 16, "set_tuning: group U must be 8 or 16");
-            g_grp_u = value;
-            return BGNN_OK;
-        case BGNN_TUNE_GROUP_ZR_EARLY: g_grp_ze = value ? 1 : 0; return BGNN_OK;
-        case BGNN_TUNE_SEG_COLSLICE:
-            BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: column slices must be 0 (off), 1 (U 16) or 2 (U 8)");
-            g_seg_cs = value;
-            return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
-            BGNN_REQUIRE(value >= 0 && value <= 2, "set_tuning: gemm mode must be 0 (f32), 1 (bf16x6) or 2 (f16x3)");
+            BGNN_REQUIRE(value == 0 || value == 2, "set_tuning: gemm mode must be 0 (f32 MFMA) or 2 (f16x3)");
             set_gemm_mode(value);
-            return BGNN_OK;
-        case BGNN_TUNE_GEMM_STAGING:
-            BGNN_REQUIRE((value >= -1 && value < kNumH3gVariants) || (value > 10 && value < 15) || value == 24,
-                         "set_tuning: gemm staging must be -1 (registers) or an LDS-DMA variant 0..%d",
-                         kNumH3gVariants - 1);
-            set_gemm_staging(value);
             return BGNN_OK;
         default: return fail(BGNN_E_ARG, "set_tuning: unknown knob %d", knob);
     }

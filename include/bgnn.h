@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 8
+#define BGNN_ABI_VERSION 9
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -66,23 +66,11 @@ const char* bgnn_last_error_string(void);
 #define BGNN_TUNE_SEG_BLOCKS 2   /* sweep grid in blocks (default 1024)                   */
 #define BGNN_TUNE_SEG_U 3        /* neighbours per gather batch: 0 = auto (12), 8, 12, 16  */
 #define BGNN_TUNE_SEG_NT 4       /* non-temporal hints on stream-once rows (default 1)       */
-#define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 1 = bf16x6, 2 = f16x3 (default) */
+#define BGNN_TUNE_GEMM_MODE 5    /* GEMM kernel: 0 = f32 MFMA, 2 = f16x3 (default)           */
 #define BGNN_TUNE_ROWS_NT 6      /* non-temporal stores in sage_apply / sage_bwd_rows (0/1)   */
 #define BGNN_TUNE_GROUP_BLOCKS 7 /* row-group kernel grid in blocks (default 1024)            */
-#define BGNN_TUNE_GEMM_STAGING 8 /* f16x3 operand staging: -1 = registers (gemm_x6), 0..1 =
-                                    LDS-DMA kernel variant (gemm_h3g) for tall K-contiguous
-                                    products                                                 */
-#define BGNN_TUNE_GEMM_TAIL 9     /* tall f16x3 GEMMs whose last round of 256x256 tiles would be
-                                    under-filled (the SAGE dgrad): whole rounds of 256x256 tiles +
-                                    the remaining rows as split-K halves (1 = on; 0 = the 128x256
-                                    tiles, default: measured faster in the train step)       */
-#define BGNN_TUNE_GROUP_U 10      /* row-group kernel: source rows per gather batch, 8 or 16    */
-#define BGNN_TUNE_GROUP_ZR_EARLY 11 /* row-group SAGE epilogue: z_r loads issued before the gathers
-                                    (1) or after them (0)                                    */
-#define BGNN_TUNE_SEG_COLSLICE 12   /* row-group kernel, plain epilogue (transpose aggregation),
-                                    H = 256 / 512: 1 = every XCD reduces one 128-column slice of
-                                    its row region (a graph's slice of rows fits that XCD's L2),
-                                    0 = whole rows                                           */
+/* (ABI 9 retired knobs 8-12 -- LDS-DMA GEMM staging, the GEMM tail split, 16-row gather
+ * batches, early z_r loads, per-XCD column slices: measured, not adopted; profiles/r0[23]_*) */
 #define BGNN_TUNE_ROWS_REV 13       /* bit 0: sage_bwd_rows / l2norm_bwd walk each block's rows from
                                     the last one down, so they start on the rows sage_bwd_stats
                                     read last (still in the Infinity Cache); bit 1: sage_apply
@@ -334,34 +322,15 @@ int bgnn_add_dropped_bf16(const void* a, const void* b, int64_t n, float p, uint
 int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
                           int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream);
 
-/* Pre-split f16x3 operands (ABI 5). An f32 matrix x [rows, cols] (ld ldx) as its two f16 pieces,
- * the split the f16x3 GEMM does internally: with s = 2^k from *amax (max|x|, or any bound within
- * a modest factor above it: max|x| s lands in [2^14, 2^15) for the exact max), hi = f16(x s),
- * lo = f16(x s - hi), stored k8-interleaved: row r = [cols/8][hi 8 | lo 8] f16 (row stride ldp
- * >= 2 cols elements). cols % 8 == 0. */
-int bgnn_split_f16x2(const float* x, int64_t rows, int64_t cols, int64_t ldx, const float* amax,
-                     uint16_t* pieces, int64_t ldp, void* stream);
-/* C[M,N] = alpha * A B^T (+ beta C or the drop-add source, + bias, ReLU, max|C| into c_amax)
- * with A [M,K] and B [N,K] given as k8-interleaved f16 pieces (bgnn_split_f16x2's layout; lda /
- * ldb elements per row, >= 2K, multiples of 8) and the maxima their pieces were scaled by.
- * Bit-identical to bgnn_gemm_f32_scaled(f16x3) on the f32 operands. bsrc != NULL: the drop-add
- * epilogue of bgnn_gemm_f32_dropadd (beta must be 1). K % 32 == 0. variant: 0 (default), 1, 2
- * (tile / slice-depth choices, measurement only), 12-14 timing ablations. */
-int bgnn_gemm_p16(int64_t M, int64_t N, int64_t K, const uint16_t* a, int64_t lda, const float* a_amax,
-                  const uint16_t* b, int64_t ldb, const float* b_amax, float alpha, float beta, float* C,
-                  int64_t ldc, const float* bias, int32_t relu, float* c_amax, const float* bsrc,
-                  int64_t ld_bsrc, float p, uint64_t seed, int32_t variant, void* stream);
-
 /* ------------------------------------------------------------------------
  * fp32 GEMM (f32 operands, f32 result, f32 accumulation):
  *   C[M,N] = alpha * op(A)[M,K] · op(B)[K,N] + beta * C
- * Three kernel families (BGNN_TUNE_GEMM_MODE):
+ * Two kernel families (BGNN_TUNE_GEMM_MODE):
  *   2 (default) f16x3: each operand is scaled by a power of two from its max |value| and
  *     split into two f16 pieces; three f16 MFMAs per product (a0b0 + a0b1 + a1b0), f32
  *     accumulation, exact unscale (dropped terms <= ~2^-21 |a||b|; measured error vs fp64 at
  *     or below the f32 MFMA's). Needs the workspace of bgnn_gemm_ws_bytes() (the operand
  *     maxima live there unless the caller passes them to bgnn_gemm_f32_scaled).
- *   1 bf16x6: three exact bf16 pieces per operand, six products (dropped <= 2^-23 |a||b|).
  *   0 the f32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 FMA chain).
  * trans_a = 0: A is [M,K] row-major (lda >= K); 1: A is [K,M] row-major (lda >= M).
  * trans_b = 0: B is [K,N] row-major (ldb >= N);  1: B is [N,K] row-major (ldb >= K).

@@ -82,10 +82,10 @@ def test_fused_layer_layouts(dev, monkeypatch, z_planes, dz_planes, H):
     test_fused_layer_matches_oracle(dev, "mean", 1, True, True, True, H)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 2])
 @pytest.mark.parametrize("aggr,red", [("sum", 0), ("mean", 1)])
 def test_fused_layer_gemm_modes(dev, mode, aggr, red):
-    """The layer matches the oracle with every GEMM family (f32 MFMA / bf16x6 / f16x3)."""
+    """The layer matches the oracle with every GEMM family (f32 MFMA / f16x3)."""
     from bgnn import _lib
     _lib.call("bgnn_set_tuning", 5, mode)
     try:

@@ -232,91 +232,29 @@ def test_spmm_bwd_folds_max_abs(dev, kernel, reduce):
         _lib.call("bgnn_set_tuning", 1, old)
 
 
-@pytest.mark.parametrize("knobs", [(16, 0), (8, 1), (16, 1)], ids=["u16", "zr_early", "u16_zr_early"])
+@pytest.mark.parametrize("reduce", [0, 1, 2], ids=["sum", "mean", "max"])
 @pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
-def test_group_kernel_knobs_bit_identical(dev, knobs, graph):
-    """Row-group kernel variants (BGNN_TUNE_GROUP_U: 16 source rows per gather batch;
-    BGNN_TUNE_GROUP_ZR_EARLY: z_r loads before the gathers) change only load scheduling: the
-    fused SAGE forward (o, norms, BN partial sums) and the plain / transpose aggregations are
-    bit-identical to the defaults."""
-    from bgnn import _lib
-    ei, n = _variant_graph(dev, graph)
-    g = Graph.build(ei, n)
-    assert g.fwd.groups is not None
-    H = 512
-    torch.manual_seed(9)
-    z = torch.randn(n, 2 * H, device=dev)
-    bias = torch.randn(H, device=dev)
-    x = torch.randn(n, H, device=dev)
-    gy = torch.randn(n, H, device=dev)
-    slots = _lib.query("bgnn_sage_fwd_slots", g.fwd.ref())
-    s = torch.cuda.current_stream().cuda_stream
-
-    def run():
-        o = torch.empty(n, H, device=dev)
-        nrm = torch.empty(n, device=dev)
-        bnp = torch.empty(slots, 2, H, device=dev)
-        part = torch.empty(max(g.fwd.plan.n_chunks, 1) * H, device=dev)
-        _lib.call("bgnn_sage_fwd", g.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H, bias.data_ptr(), H,
-                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
-        red = {}
-        for r in ("sum", "mean"):
-            xx = x.clone().requires_grad_(True)
-            y = bgnn.aggregate(xx, g, r)
-            y.backward(gy)
-            red[r] = (y.detach(), xx.grad)
-        return o, nrm, bnp, red
-
-    ref = run()
-    try:
-        _lib.call("bgnn_set_tuning", 10, knobs[0])
-        _lib.call("bgnn_set_tuning", 11, knobs[1])
-        got = run()
-    finally:
-        _lib.call("bgnn_set_tuning", 10, 8)
-        _lib.call("bgnn_set_tuning", 11, 0)
-    for a, b in zip(ref[:3], got[:3]):
-        assert torch.equal(a, b)
-    for r in ("sum", "mean"):
-        assert torch.equal(ref[3][r][0], got[3][r][0]) and torch.equal(ref[3][r][1], got[3][r][1]), r
-
-
-@pytest.mark.parametrize("cs", [1, 2], ids=["u16", "u8"])
-@pytest.mark.parametrize("H", [512, 256])
-@pytest.mark.parametrize("graph", ["mesh_super", "random_dense"])
-def test_column_slice_kernel_bit_identical(dev, cs, H, graph):
-    """BGNN_TUNE_SEG_COLSLICE (per-XCD 128-column slices of the row-group kernel, plain epilogue)
-    changes only which XCD reads which columns: the plain aggregations (sum, mean) and their
-    transposes (the training step's bgnn_spmm_bwd, sum and mean) are bit-identical to the
-    whole-row kernel, and the folded max|out| is the same."""
+def test_spmm_bwd_add_equals_spmm_bwd_plus_addend(dev, reduce, graph):
+    """bgnn_spmm_bwd_add (the max-aggregation layer's backward adds dh W_r there) is the transpose
+    aggregation plus the addend, bit for bit, on every kernel path (row groups, sweep, heavy-row
+    chunks + combine), and folds max|gx| of the sum."""
     from bgnn import _lib, ops
     ei, n = _variant_graph(dev, graph)
     g = Graph.build(ei, n)
-    assert g.fwd.groups is not None and g.bwd.groups is not None
-    torch.manual_seed(11)
+    H = 512
+    torch.manual_seed(12)
     x = torch.randn(n, H, device=dev)
     gy = torch.randn(n, H, device=dev)
-
-    def run():
-        red = {}
-        for r in ("sum", "mean"):
-            xx = x.clone().requires_grad_(True)
-            y = bgnn.aggregate(xx, g, r)
-            y.backward(gy)
-            red[r] = (y.detach(), xx.grad)
-        amax = torch.zeros(1, device=dev)
-        gx = ops.spmm_bwd(g.bwd, g.perm_t, g.fwd.rowptr, gy, 0, None, n, amax=amax)
-        return red, gx, amax
-
-    ref = run()
-    old = _lib.query("bgnn_get_tuning", 12)
-    try:
-        _lib.call("bgnn_set_tuning", 12, cs)
-        got = run()
-    finally:
-        _lib.call("bgnn_set_tuning", 12, old)
-    for r in ("sum", "mean"):
-        assert torch.equal(ref[0][r][0], got[0][r][0]), (r, "fwd")
-        assert torch.equal(ref[0][r][1], got[0][r][1]), (r, "bwd")
-    assert torch.equal(ref[1], got[1])
-    assert ref[2].item() == got[2].item() == ref[1].abs().max().item()
+    add = torch.randn(n, H, device=dev)
+    arg = None
+    if reduce == 2:
+        _, arg = ops.spmm_fwd(g.fwd, x, 2, n, want_arg=True)
+    ref = ops.spmm_bwd(g.bwd, g.perm_t, g.fwd.rowptr, gy, reduce, arg, n) + add
+    gx = torch.empty(n, H, device=dev)
+    amax = torch.zeros(1, device=dev)
+    part = torch.empty(max(g.bwd.plan.n_chunks, 1) * H, device=dev)
+    _lib.call("bgnn_spmm_bwd_add", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), gy.data_ptr(), H, H,
+              reduce, None if arg is None else arg.data_ptr(), add.data_ptr(), H, gx.data_ptr(), H, part.data_ptr(),
+              amax.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(gx, ref)
+    assert amax.item() == gx.abs().max().item()

@@ -83,9 +83,9 @@ def test_size_queries_need_no_gpu():
     # f16x3 (default): a 256-B head for the operand maxima, plus split-K slabs where used
     assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 256    # forward: no split-K
     assert _lib.query("bgnn_gemm_ws_bytes", 1024, 512, 80656, 1, 0) > 256     # wgrad: split-K
-    _lib.call("bgnn_set_tuning", 5, 1)
+    _lib.call("bgnn_set_tuning", 5, 0)
     try:
-        assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 0  # bf16x6: no head
+        assert _lib.query("bgnn_gemm_ws_bytes", 80656, 1024, 512, 0, 1) == 0  # f32 MFMA: no head
     finally:
         _lib.call("bgnn_set_tuning", 5, 2)
 

@@ -9,7 +9,6 @@ HIP-event times:
   bwd_fwdcsr    the same gather with the FORWARD CSR (= transpose as a multiset: symmetric graph)
   bwd_dense     transpose CSR, dense dh [N, H] in, dense out
   bwd_nt0       bwd_t with non-temporal hints off
-  bwd_cs16/8    bwd_t with per-XCD 128-column slices (BGNN_TUNE_SEG_COLSLICE 1 / 2: U = 16 / 8)
 
 Usage: python tools/agg_bwd_ab.py [--rounds 15]"""
 import argparse
@@ -79,14 +78,6 @@ def main():
         return w
 
     bwd_t = bwd(g.bwd, dz[:, H:], 2 * H, dz, 2 * H)
-    # bit-identity of the column-slice kernel (dz_l written into dz[:, :H])
-    bwd_t()
-    ref = dz[:, :H].clone()
-    for v in (1, 2):
-        dz[:, :H].zero_()
-        knob(bwd_t, 12, v)()
-        torch.cuda.synchronize()
-        print(f"colslice {v}: bit-identical = {bool(torch.equal(dz[:, :H], ref))}")
     variants = {
         "sage_fwd": sage_fwd,
         "plain_fwd": plain_fwd,
@@ -94,9 +85,6 @@ def main():
         "bwd_fwdcsr": bwd(g.fwd, dz[:, H:], 2 * H, dz, 2 * H),
         "bwd_dense": bwd(g.bwd, dh_dense, H, out_dense, H),
         "bwd_nt0": nt0(bwd_t),
-        "bwd_cs16": knob(bwd_t, 12, 1),
-        "bwd_cs8": knob(bwd_t, 12, 2),
-        "bwd_dense_cs16": knob(bwd(g.bwd, dh_dense, H, out_dense, H), 12, 1),
     }
     junk = torch.empty(1 << 28, device=dev)
     times = {k: [] for k in variants}

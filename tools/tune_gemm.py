@@ -50,7 +50,7 @@ def main():
                     fused.GEMM_BACKEND = "torch"
                 else:
                     fused.GEMM_BACKEND = "hip"
-                    _lib.call("bgnn_set_tuning", 5, {"x": 1, "h": 2}.get(v[0], 0))
+                    _lib.call("bgnn_set_tuning", 5, 2 if v[0] == "h" else 0)
                     _lib.call("bgnn_gemm_set_cfg", int(v.lstrip("xh")))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
