@@ -212,9 +212,10 @@ __global__ __launch_bounds__(256) void k_rel_error_loss(const float* __restrict_
         const float d = fabsf(q) + eps;
         const float diff = p - q;
         acc += (double)(fabsf(diff) / d);
-        // sign(diff), NaN propagated (torch's abs backward: sgn(NaN) = NaN), so a diverging
-        // prediction does not get a silent zero gradient
-        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : (diff == 0.f ? 0.f : diff));
+        // sign(diff) with sign(NaN) = 0: torch's abs backward (grad * sgn(x), sgn(NaN) = 0 on
+        // ROCm and CPU), which the reference's loss differentiates through -- a NaN prediction
+        // shows as a NaN loss, with the same zero gradient as the reference
+        const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
         if (dpred) dpred[i] = sg * scale / d * inv_n;
     }
     red[t] = acc;

@@ -28,6 +28,25 @@ def build(meta, dev, fused_path):
     return m.to(dev)
 
 
+def _fp64_checksums(z, meta):
+    """Gradient checksums of the golden's case from the fp64 oracle (oracle/buckgnn_ref.py, the
+    restatement the golden's reference run used, in double precision)."""
+    from oracle import buckgnn_ref as R
+    from test_oracle import reference_shapes
+    w = make_weights(reference_shapes(meta), meta["weight_seed"])
+    step = {}
+    for k, v in w.items():
+        t = torch.from_numpy(v)
+        t = t.double() if t.is_floating_point() else t.clone()
+        step[k] = t.requires_grad_(t.is_floating_point() and "running" not in k)
+    batch = None if meta["single_graph"] else torch.from_numpy(z["batch"])
+    y = torch.from_numpy(z["y"]).double()
+    pred = R.forward(step, meta["model_name"], torch.from_numpy(z["x"]).double(), torch.from_numpy(z["edge_index"]),
+                     batch, True, meta["pooling"], 0.0)
+    R.relative_error_loss(pred, y[0] if meta["single_graph"] else y).backward()
+    return {"gradsum/" + k: grad_checksum(v.grad.numpy()) for k, v in step.items() if v.grad is not None}
+
+
 @pytest.mark.parametrize("fused_path", [True, False], ids=["fused", "per_op"])
 @pytest.mark.parametrize("path", FILES, ids=os.path.basename)
 def test_model_matches_reference_golden(dev, path, fused_path):
@@ -53,6 +72,7 @@ def test_model_matches_reference_golden(dev, path, fused_path):
     np.testing.assert_allclose(loss.item(), float(z["loss_train"]), **tol)
     np.testing.assert_allclose(captured["pooled"].cpu().numpy(), z["pooled_train"], **tol)
     params = dict(model.named_parameters())
+    exact = _fp64_checksums(z, meta) if meta["model_name"] == "GraphSage_maxAggr" and meta["hidden"] >= 256 else {}
     for k in z.files:
         if k.startswith("grad/"):
             g = params[k[5:]].grad
@@ -64,8 +84,17 @@ def test_model_matches_reference_golden(dev, path, fused_path):
             # [sum, sum |g|, projection]: the signed sums cancel (|sum| can be 1e-3 of sum |g| on
             # the >= 1,024-node fixtures), so their error is bounded relative to the L1 mass sum |g|
             # as well: |d| <= 2e-3 |ref| + 2e-4 + 1e-4 sum |g|
-            np.testing.assert_allclose(grad_checksum(g.cpu().numpy()), z[k], rtol=2e-3,
-                                       atol=2e-4 + 1e-4 * float(z[k][1]), err_msg=k)
+            got = grad_checksum(g.cpu().numpy())
+            tol = 2e-3 * np.abs(z[k]) + 2e-4 + 1e-4 * float(z[k][1])
+            if k in exact:
+                # max aggregation: the gradient follows each (target, channel) argmax, so f32 rounding
+                # that reorders two near-tied neighbours moves a gradient element between sources; the
+                # fp32 reference itself sits that far from its own fp64 evaluation. The bar: as close
+                # to the fp64 answer as the reference is, plus the usual tolerance.
+                ref64 = exact[k]
+                assert (np.abs(got - ref64) <= tol + np.abs(z[k] - ref64)).all(), (k, got, z[k], ref64)
+            else:
+                np.testing.assert_allclose(got, z[k], rtol=2e-3, atol=2e-4 + 1e-4 * float(z[k][1]), err_msg=k)
     sd = model.state_dict()
     for k in z.files:
         if k.startswith("state/"):
@@ -180,5 +209,6 @@ def test_production_path_taken_on_n1k_goldens(dev, monkeypatch, path):
     model.train()
     pred, _ = model(x, torch.from_numpy(z["edge_index"]).to(dev), torch.from_numpy(z["edge_attr"]).to(dev),
                     torch.from_numpy(z["batch"]).to(dev))
-    assert seen == {"mlp2": 1, "fold": 1}, seen
+    # (max aggregation aggregates the encoder output itself: its first layer cannot fold it)
+    assert seen == {"mlp2": 1, "fold": 0 if meta["model_name"] == "GraphSage_maxAggr" else 1}, seen
     np.testing.assert_allclose(pred.detach().cpu().numpy().reshape(-1), z["pred_train"], rtol=1e-4, atol=1e-4)
