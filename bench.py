@@ -75,6 +75,9 @@ def parse():
                          "use_fused=False, i.e. the module graph the PyG shim gives the reference's unchanged "
                          "Models/BuckGNN.py (bgnn.nn.SAGEConv modules on the hand-written GEMM + fused "
                          "aggregation/normalize, torch BatchNorm/ReLU/Dropout and encoder)")
+    ap.add_argument("--bn", default="torch", choices=["torch", "bgnn"],
+                    help="per_op path: the BatchNorm1d modules as torch's (default, the reference's modules "
+                         "unchanged) or bgnn.nn.BatchNorm1d (install_pyg_shim(batchnorm=True), csrc/bn.hip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
@@ -164,6 +167,8 @@ def main():
     state0 = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
     model.use_fused = args.path == "fused"
+    if args.path == "per_op" and args.bn == "bgnn":
+        bgnn.nn.use_bgnn_batchnorm(model)
     model.ea_bf16 = bool(args.bf16)
     is_ea = args.model.startswith("EA_GNN")
     lr = args.lr if args.lr is not None else (1e-3 if is_ea else 1e-2)
@@ -331,7 +336,8 @@ def main():
                         + (" + super node" if args.config == "cfg3" else " + 13.33% random virtual edges")
                         + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam"
                         + ("; per-op modules (PyG-surface SAGEConv on the bgnn GEMM + fused aggregation/normalize, "
-                           "torch BatchNorm/ReLU/Dropout/encoder)" if args.path == "per_op" else "")
+                           + ("bgnn BatchNorm1d, " if args.bn == "bgnn" else "torch BatchNorm, ")
+                           + "torch ReLU/Dropout/encoder)" if args.path == "per_op" else "")
                         + (", bf16 GEMM operands" if args.bf16 and args.model.startswith("EA_GNN") else "") + "; "
                         + {"static": "CSR rebuilt every step" if not args.cache_graph else "CSR cached across steps",
                            "store": f"new shuffled batch every step gathered on the GPU from a resident "
@@ -349,6 +355,7 @@ def main():
             "parallelism": f"dp{world}",
             "gemm": args.gemm,
             "path": args.path,
+            **({"batchnorm": args.bn} if args.path == "per_op" else {}),
         },
         "roofline": dict(gemm_blocks[main_key], family=main_key),
         "roofline_gemm": {

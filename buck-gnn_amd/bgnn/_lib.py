@@ -67,6 +67,11 @@ SIGNATURES = {
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
                               c_p, c_p, c_p]),
+    "bgnn_bn_slots": (c_i32, [c_i64, c_i32]),
+    "bgnn_bn_stats": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
+    "bgnn_bn_apply": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
+    "bgnn_bn_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p]),
+    "bgnn_bn_bwd_dx": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p]),
     "bgnn_spmm_bwd_add": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
                                   c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_sage_fwd_slots": (c_i32, [ctypes.POINTER(CsrStruct)]),

@@ -124,6 +124,113 @@ class SAGEConv(nn.Module):
         return f"{self.__class__.__name__}({self.in_channels[0]}, {self.out_channels}, aggr={self.aggr})"
 
 
+class _BatchNormFn(torch.autograd.Function):
+    """torch.nn.functional.batch_norm over a [N, C] fp32 CUDA activation on libbgnn (csrc/bn.hip):
+    train (batch statistics; running stats updated in place by bgnn_bn_finalize) or eval (running
+    statistics), forward one stats pass + one apply pass, backward one stats pass + one row pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, batch_stats: bool, momentum: float, eps: float):
+        from . import _lib
+        from .graph import _stream
+        x = x.contiguous()
+        N, C = x.shape
+        dev = x.device
+        s = _stream()
+        coef = torch.empty(4, C, dtype=torch.float32, device=dev)   # mean, invstd, scale, shift
+        mean, invstd, scale, shift = coef[0], coef[1], coef[2], coef[3]
+        w = None if weight is None else weight.contiguous()
+        b = None if bias is None else bias.contiguous()
+        if batch_stats:
+            slots = _lib.query("bgnn_bn_slots", N, C)
+            part = torch.empty(slots, 2, C, dtype=torch.float32, device=dev)
+            _lib.call("bgnn_bn_stats", x.data_ptr(), N, C, part.data_ptr(), s)
+            _lib.call("bgnn_bn_finalize", part.data_ptr(), slots, C, N, None if w is None else w.data_ptr(),
+                      None if b is None else b.data_ptr(), float(eps), float(momentum),
+                      None if running_mean is None else running_mean.data_ptr(),
+                      None if running_var is None else running_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                      scale.data_ptr(), shift.data_ptr(), s)
+        else:
+            _lib.call("bgnn_bn_eval_coeffs", C, None if w is None else w.data_ptr(), None if b is None else b.data_ptr(),
+                      float(eps), running_mean.data_ptr(), running_var.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                      s)
+            mean.copy_(running_mean)
+            invstd.copy_(torch.rsqrt(running_var + eps))
+        y = torch.empty_like(x)
+        _lib.call("bgnn_bn_apply", x.data_ptr(), N, C, scale.data_ptr(), shift.data_ptr(), y.data_ptr(), s)
+        ctx.batch_stats = batch_stats
+        ctx.affine = (weight is not None, bias is not None)
+        ctx.save_for_backward(x, coef, w if w is not None else torch.empty(0, device=dev))
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        from .graph import _stream
+        x, coef, w = ctx.saved_tensors
+        g = g.contiguous()
+        N, C = x.shape
+        dev = x.device
+        s = _stream()
+        mean, invstd, scale = coef[0], coef[1], coef[2]
+        slots = _lib.query("bgnn_bn_slots", N, C)
+        part = torch.empty(slots, 2, C, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_bn_bwd_stats", g.data_ptr(), x.data_ptr(), mean.data_ptr(), invstd.data_ptr(), N, C,
+                  part.data_ptr(), s)
+        sums = torch.empty(2, C, dtype=torch.float32, device=dev)   # dbeta, dgamma
+        _lib.call("bgnn_reduce_partials", part.data_ptr(), slots, C, sums[0].data_ptr(), sums[1].data_ptr(), 0, s)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            if ctx.batch_stats:
+                _lib.call("bgnn_bn_bwd_dx", g.data_ptr(), x.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                          w.data_ptr() if w.numel() else None, sums.data_ptr(), N, C, dx.data_ptr(), s)
+            else:   # eval: dx = g * gamma * invstd (the scale of the forward)
+                zero = torch.zeros(C, dtype=torch.float32, device=dev)
+                _lib.call("bgnn_bn_apply", g.data_ptr(), N, C, scale.data_ptr(), zero.data_ptr(), dx.data_ptr(), s)
+        has_w, has_b = ctx.affine
+        return (dx, sums[1] if has_w else None, sums[0] if has_b else None, None, None, None, None, None)
+
+
+class BatchNorm1d(nn.BatchNorm1d):
+    """torch.nn.BatchNorm1d with the same constructor, parameters, buffers and state-dict keys,
+    whose forward over a 2-D fp32 CUDA input runs on libbgnn (_BatchNormFn: csrc/bn.hip) -- the
+    opt-in replacement bgnn.install_pyg_shim(batchnorm=True) installs for the BatchNorm1d modules
+    the reference's unchanged Models/BuckGNN.py builds (torch's channels-last BatchNorm kernels
+    take ~1.7 ms per cfg2 layer on ROCm). Anything else (3-D input, other dtypes,
+    CPU) takes torch's forward. The momentum / num_batches_tracked / running-stats logic is
+    torch's _BatchNorm.forward, restated."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        C = input.size(-1) if input.dim() == 2 else -1
+        if not (input.is_cuda and input.dim() == 2 and input.dtype == torch.float32 and C == self.num_features
+                and C % 4 == 0 and C <= 1024 and 256 % (C // 4) == 0 and input.size(0) > 0
+                and (self.weight is None or self.weight.dtype == torch.float32)):
+            return super().forward(input)
+        eaf = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            if self.momentum is None:   # cumulative moving average (one host read, as torch's)
+                eaf = 1.0 / float(self.num_batches_tracked.item())
+        batch_stats = self.training or (self.running_mean is None and self.running_var is None)
+        if batch_stats and input.size(0) < 2:
+            raise ValueError(f"Expected more than 1 value per channel when training, got input size {tuple(input.shape)}")
+        # (train: the running buffers are updated unless they are not tracked; eval: used)
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        return _BatchNormFn.apply(input, self.weight, self.bias, rm, rv, batch_stats, eaf, self.eps)
+
+
+def use_bgnn_batchnorm(module: nn.Module) -> nn.Module:
+    """Make every torch.nn.BatchNorm1d inside `module` a bgnn.nn.BatchNorm1d in place (the class
+    only: parameters, buffers and state-dict keys are unchanged) and return the module."""
+    torch_bn = torch.nn.modules.batchnorm.BatchNorm1d   # (torch's class even while the shim replaces nn's)
+    for m in module.modules():
+        if type(m) is torch_bn:
+            m.__class__ = BatchNorm1d
+    return module
+
+
 def _num_segments(index: Tensor, size: Optional[int]) -> int:
     if size is not None:
         return int(size)

@@ -20,7 +20,15 @@ def _module(name: str, **attrs) -> types.ModuleType:
     return m
 
 
-def install_pyg_shim(force: bool = False) -> None:
+_TORCH_BN = None   # torch.nn.BatchNorm1d while install_pyg_shim(batchnorm=True) has replaced it
+
+
+def install_pyg_shim(force: bool = False, batchnorm: bool = False) -> None:
+    """batchnorm=True (opt-in): also make torch.nn.BatchNorm1d bgnn.nn.BatchNorm1d (a subclass with
+    the same parameters, buffers and state-dict keys whose 2-D fp32 GPU forward runs on libbgnn),
+    so the BatchNorm1d modules the reference builds (Models/BuckGNN.py:133-217, `nn.BatchNorm1d`
+    looked up when the model is constructed) take the HIP kernels too."""
+    global _TORCH_BN
     existing = sys.modules.get("torch_geometric")
     if existing is not None and not getattr(existing, "__bgnn_shim__", False) and not force:
         raise RuntimeError("a real torch_geometric is already imported; pass force=True to replace it")
@@ -51,9 +59,18 @@ def install_pyg_shim(force: bool = False) -> None:
         "torch_geometric.loader": loader_mod,
         "torch_scatter": scatter,
     })
+    if batchnorm and _TORCH_BN is None:
+        import torch
+        _TORCH_BN = torch.nn.BatchNorm1d
+        torch.nn.BatchNorm1d = N.BatchNorm1d
 
 
 def uninstall_pyg_shim() -> None:
+    global _TORCH_BN
+    if _TORCH_BN is not None:
+        import torch
+        torch.nn.BatchNorm1d = _TORCH_BN
+        _TORCH_BN = None
     for k in ("torch_geometric", "torch_geometric.nn", "torch_geometric.data", "torch_geometric.data.data",
               "torch_geometric.data.storage", "torch_geometric.loader", "torch_scatter"):
         m = sys.modules.get(k)

@@ -506,6 +506,28 @@ int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, int32_t D2, 
 int bgnn_add_dropout(const float* a, const float* b, int64_t n, float p, uint64_t seed, float* out,
                      void* stream);
 
+/* ------------------------------------------------------------------------
+ * ABI 9: BatchNorm1d over a row-major [n_rows, C] fp32 activation (torch.nn.BatchNorm1d, the
+ * modules the reference builds after each SAGEConv, Models/BuckGNN.py:133,148,163,179; used by
+ * bgnn.nn.BatchNorm1d on the per-module path). C % 4 == 0 with C / 4 a power of two <= 256;
+ * 16-byte aligned pointers.
+ *   bgnn_bn_stats:     per-block partials [bgnn_bn_slots(n_rows, C), 2, C] of sum x, sum x^2
+ *                      (finished by bgnn_bn_finalize)
+ *   bgnn_bn_apply:     y = x * scale + shift
+ *   bgnn_bn_bwd_stats: partials of sum g, sum g * (x - mean) * invstd (finished by
+ *                      bgnn_reduce_partials into sums[2, C] = dbeta, dgamma)
+ *   bgnn_bn_bwd_dx:    train-mode input gradient gamma invstd / N (N g - sums[0] - xhat sums[1])
+ *                      (gamma may be NULL: affine=False)
+ * ---------------------------------------------------------------------- */
+int32_t bgnn_bn_slots(int64_t n_rows, int32_t C);
+int bgnn_bn_stats(const float* x, int64_t n_rows, int32_t C, float* partial, void* stream);
+int bgnn_bn_apply(const float* x, int64_t n_rows, int32_t C, const float* scale, const float* shift, float* y,
+                  void* stream);
+int bgnn_bn_bwd_stats(const float* g, const float* x, const float* mean, const float* invstd, int64_t n_rows,
+                      int32_t C, float* partial, void* stream);
+int bgnn_bn_bwd_dx(const float* g, const float* x, const float* mean, const float* invstd, const float* gamma,
+                   const float* sums, int64_t n_rows, int32_t C, float* dx, void* stream);
+
 /* ABI 8: RelativeErrorLoss on denormalised values (Utils/Losses.py:755-761 applied to
  * Normalizer.py:203-215's value * scale + center, TRAIN_FINAL.py:267-270): *loss =
  * mean(|p' - t'| / (|t'| + eps)) with p' = pred * scale + center, t' = y * scale + center over n

@@ -160,3 +160,22 @@ def test_relu_mask_matches_reference_form():
     g, out = torch.randn(64, 33), torch.randn(64, 33)
     out[0, :5] = 0.0
     assert torch.equal(torch.ops.aten.threshold_backward(g, out, 0.0), g * (out > 0))
+
+
+def test_pyg_shim_batchnorm_opt_in_patches_and_restores():
+    """install_pyg_shim(batchnorm=True) makes torch.nn.BatchNorm1d bgnn's subclass (same state-dict
+    keys) for modules built while it is installed; uninstall restores torch's class."""
+    import torch
+    import bgnn
+    from bgnn import nn as bnn
+    orig = torch.nn.BatchNorm1d
+    bgnn.install_pyg_shim(batchnorm=True)
+    try:
+        assert torch.nn.BatchNorm1d is bnn.BatchNorm1d
+        m = torch.nn.BatchNorm1d(8)
+        assert isinstance(m, orig) and set(m.state_dict()) == set(orig(8).state_dict())
+        y = m(torch.randn(4, 8))   # CPU input: torch's own forward
+        assert y.shape == (4, 8)
+    finally:
+        bgnn.uninstall_pyg_shim()
+    assert torch.nn.BatchNorm1d is orig
