@@ -1,0 +1,91 @@
+#!/usr/bin/env python
+"""Interleaved A/B of aggregation-kernel settings (bgnn_set_tuning knobs) on a config's batch as the
+training step runs them: the fused SAGE forward (bgnn_sage_fwd, z interleaved [N, 2H]) and the
+transpose aggregation (bgnn_spmm_bwd, dh = dz[:, H:] -> dz[:, :H]); 1 GiB cache flush between
+launches, median HIP-event times, bit-identity against the first setting.
+    python tools/agg_knob_ab.py [--config cfg2] [--rounds 15] "" "14=1" "15=1280" ..."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+import torch  # noqa: E402
+
+from bgnn import _lib, synthetic  # noqa: E402
+from bgnn.graph import Graph  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=15)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("settings", nargs="*", default=[""])
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    b = synthetic.make_config_batch(args.config)
+    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    N, E, H = b.num_nodes, b.num_edges, 512
+    torch.manual_seed(0)
+    z = torch.randn(N, 2 * H, device=dev)
+    dz = torch.randn(N, 2 * H, device=dev)
+    bias = torch.randn(H, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    slots = _lib.query("bgnn_sage_fwd_slots", g.fwd.ref())
+    o = torch.empty(N, H, device=dev)
+    nrm = torch.empty(N, device=dev)
+    bnp = torch.empty(max(slots, 2048), 2, H, device=dev)
+    part = torch.empty(max(g.fwd.plan.n_chunks, g.bwd.plan.n_chunks, 1) * H, device=dev)
+    flush = torch.empty(1 << 28, device=dev)
+    fwd_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
+    bwd_bytes = 2 * N * H * 4 + 4 * E + 4 * (N + 1)
+
+    def sage_fwd():
+        _lib.call("bgnn_sage_fwd", g.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H, bias.data_ptr(), H,
+                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
+        return o
+
+    def bwd_t():
+        _lib.call("bgnn_spmm_bwd", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), dz[:, H:].data_ptr(),
+                  2 * H, H, 0, None, dz.data_ptr(), 2 * H, part.data_ptr(), None, s)
+        return dz[:, :H]
+
+    def apply(setting, undo=None):
+        for kv in filter(None, setting.split(";")):
+            k, v = (int(t) for t in kv.split("="))
+            if undo is not None:
+                undo.append((k, _lib.query("bgnn_get_tuning", k)))
+            _lib.call("bgnn_set_tuning", k, v)
+
+    kernels = {"sage_fwd": (sage_fwd, fwd_bytes), "spmm_bwd": (bwd_t, bwd_bytes)}
+    times = {(k, st): [] for k in kernels for st in args.settings}
+    ref = {}
+    for rnd in range(args.rounds + 2):
+        for kname, (fn, _) in kernels.items():
+            for st in args.settings:
+                undo = []
+                apply(st, undo)
+                flush.fill_(float(rnd))
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                out = fn()
+                e1.record()
+                torch.cuda.synchronize()
+                for k, v in reversed(undo):
+                    _lib.call("bgnn_set_tuning", k, v)
+                if rnd == 1:
+                    ref[(kname, st)] = out.clone()
+                if rnd >= 2:
+                    times[(kname, st)].append(e0.elapsed_time(e1) * 1e3)
+    for kname, (_, nbytes) in kernels.items():
+        for st in args.settings:
+            ts = sorted(times[(kname, st)])
+            med = ts[len(ts) // 2]
+            same = torch.equal(ref[(kname, st)], ref[(kname, args.settings[0])])
+            print(f"{args.config} {kname:8s} [{st or 'default':>16s}] median {med:7.1f} us  min {ts[0]:7.1f}  "
+                  f"{nbytes / med / 1e6:7.1f} GB/s = {nbytes / med / 1e6 / 8000:.3f} of 8 TB/s  "
+                  f"{'bit-identical' if same else 'DIFFERS'}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
