@@ -20,11 +20,28 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--group-rows", type=int, default=4)
+    ap.add_argument("--reorder", action="store_true", help="strip-pair node order (bgnn.store.cluster_order)")
     ap.add_argument("settings", nargs="*", default=[""])
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    from bgnn import graph as G_
+    G_.GROUP_ROWS = args.group_rows
     b = synthetic.make_config_batch(args.config)
-    g = Graph.build(b.edge_index.to(dev), b.num_nodes)
+    ei = b.edge_index
+    if args.reorder:
+        from bgnn.store import cluster_order
+        import numpy as np
+        src, dst = ei.numpy()
+        inv = np.empty(b.num_nodes, np.int64)
+        ptr = b.ptr.numpy()
+        for k in range(b.num_graphs):   # per graph (graphs are contiguous node ranges)
+            lo, hi = int(ptr[k]), int(ptr[k + 1])
+            m = (dst >= lo) & (dst < hi)
+            perm = cluster_order(src[m] - lo, dst[m] - lo, hi - lo)
+            inv[lo + perm] = lo + np.arange(hi - lo)
+        ei = torch.from_numpy(np.stack([inv[src], inv[dst]]))
+    g = Graph.build(ei.to(dev), b.num_nodes)
     N, E, H = b.num_nodes, b.num_edges, 512
     torch.manual_seed(0)
     z = torch.randn(N, 2 * H, device=dev)
@@ -82,7 +99,7 @@ def main():
             ts = sorted(times[(kname, st)])
             med = ts[len(ts) // 2]
             same = torch.equal(ref[(kname, st)], ref[(kname, args.settings[0])])
-            print(f"{args.config} {kname:8s} [{st or 'default':>16s}] median {med:7.1f} us  min {ts[0]:7.1f}  "
+            print(f"{args.config} R{args.group_rows}{'r' if args.reorder else ''} {kname:8s} [{st or 'default':>16s}] median {med:7.1f} us  min {ts[0]:7.1f}  "
                   f"{nbytes / med / 1e6:7.1f} GB/s = {nbytes / med / 1e6 / 8000:.3f} of 8 TB/s  "
                   f"{'bit-identical' if same else 'DIFFERS'}", flush=True)
 
