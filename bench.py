@@ -78,6 +78,11 @@ def parse():
     ap.add_argument("--bn", default="torch", choices=["torch", "bgnn"],
                     help="per_op path: the BatchNorm1d modules as torch's (default, the reference's modules "
                          "unchanged) or bgnn.nn.BatchNorm1d (install_pyg_shim(batchnorm=True), csrc/bn.hip)")
+    ap.add_argument("--mode", default="train", choices=["train", "infer"],
+                    help="infer: INFERENCE_TIMER.py:151-270's GNN timing -- one mesh replicated --infer-batch "
+                         "times in one batch, eval mode, no_grad forward passes (a separate line, not the "
+                         "BASELINE metric)")
+    ap.add_argument("--infer-batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
@@ -124,10 +129,89 @@ def cpu_baseline(batch, model_state, model_name, steps):
         st(x, ei, b, y)
     dt = time.perf_counter() - t0
     g = batch.num_graphs * steps
-    return {"value": round(g / dt, 4), "unit": "graphs/s", "cores": threads, "kind": "port",
+    return {"value": round(g / dt, 4), "unit": "graphs/s", "cores": threads, "host_cpus": os.cpu_count(),
+            "kind": "port",
             "sample": f"{steps} timed train steps (fwd+bwd+Adam, dropout 0.1) of the oracle on the same "
                       f"{batch.num_graphs}-graph batch ({batch.num_nodes} nodes) after 1 warm-up, "
                       f"torch CPU with {threads} threads; {dt:.1f} s"}
+
+
+def run_infer(args, model, dev, world, rank):
+    """INFERENCE_TIMER.py:151-270 (run_time_analysis, GNN part): one graph deep-copied batch_size
+    times (:207), one DataLoader batch moved to the device once (:221-225), an untimed forward,
+    then total_loop timed forwards under no_grad in eval mode; throughput = batch_size / average
+    forward time (:237). The reference times with time.time() around an asynchronous forward; here
+    every timed region ends in torch.cuda.synchronize()."""
+    import torch
+    import bgnn
+    from bgnn import fused, synthetic
+    c = synthetic.CONFIGS[args.config]
+    one = synthetic.make_mesh_graph(c["n"], 1000 * rank, super_node=c["super_node"])
+    batch = bgnn.Batch.from_data_list([one] * args.infer_batch).to(dev)
+    model.eval()
+
+    def fwd():
+        with torch.no_grad():
+            return model(batch.x, batch.edge_index, batch.edge_attr, batch.batch)
+
+    for _ in range(max(1, args.warmup)):
+        fwd()
+    torch.cuda.synchronize()
+    fused.TIMERS = {}
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pred, _ = fwd()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    timers, fused.TIMERS = fused.TIMERS, None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    N, E, H = batch.num_nodes, batch.num_edges, 512
+    gemm_ev = timers.get("gemm_fwd", [])
+    g_ms = sum(a.elapsed_time(b) for a, b in gemm_ev) / len(gemm_ev) if gemm_ev else float("nan")
+    g_tfs = 2.0 * N * (2 * H) * H / (g_ms * 1e-3) / 1e12
+    agg_ev = timers.get("sage_fwd", [])
+    a_ms = sum(a.elapsed_time(b) for a, b in agg_ev) / len(agg_ev) if agg_ev else float("nan")
+    a_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
+    out = {
+        "metric": "GNN inference throughput (INFERENCE_TIMER.py run_time_analysis)",
+        "value": round(args.infer_batch * world * args.steps / elapsed, 3),
+        "unit": "graphs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.config} mesh ({c['n']}x{c['n']}"
+                               + (" + super node" if c["super_node"] else " + virtual edges")
+                               + f") replicated x{args.infer_batch} in one batch, {args.model} h=512 L=6, eval, "
+                                 f"no_grad forward per step",
+                   "batch": args.infer_batch, "nodes_per_gpu": N, "edges_per_gpu": E, "path": args.path,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "bgnn_gemm_f32 fwd z = x [W_l;W_r]^T (f16x3)", "bound": "mfma",
+                     "achieved": round(g_tfs, 2), "peak": H3_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": round(g_tfs / H3_PEAK_TFS, 4), "traffic": None, "avg_launch_ms": round(g_ms, 5),
+                     "launches": len(gemm_ev)},
+        "roofline_hbm": {"kernel": "bgnn_sage_fwd", "bound": "hbm",
+                         "achieved": round(a_bytes / (a_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(a_bytes / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes": a_bytes, "avg_launch_ms": round(a_ms, 5), "launches": len(agg_ev)},
+        "latency_ms_per_graph": round(elapsed / args.steps / args.infer_batch * 1e3, 5),
+        "pred_checksum": float(pred.double().sum()),
+    }
+    if rank == 0:
+        def clean(o):
+            if isinstance(o, dict):
+                return {k: clean(v) for k, v in o.items()}
+            return None if isinstance(o, float) and o != o else o
+        print(json.dumps(clean(out)), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
 
 
 def main():
@@ -181,6 +265,8 @@ def main():
         opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-8)
     crit = bgnn.RelativeErrorLoss()
     norm = bgnn.EigenvalueScaler(center=1.0, scale=0.5)
+    if args.mode == "infer":
+        return run_infer(args, model, dev, world, rank)
     ar = bgnn.GradAllReduce(model) if world > 1 else None
 
     if args.data == "static":
