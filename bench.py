@@ -93,9 +93,6 @@ def parse():
                          "step; host: the same batches as store collated on the host (PyG DataLoader path of "
                          "the reference) and copied to the GPU inside the step")
     ap.add_argument("--store-graphs", type=int, default=256)
-    ap.add_argument("--reorder", type=int, default=-1, choices=[-1, 0, 1],
-                    help="GraphStore node renumbering for 8-row aggregation groups (bgnn.store.cluster_order): "
-                         "1 on, 0 off, -1 the library default (bgnn.store.REORDER)")
     ap.add_argument("--epochs", type=int, default=0,
                     help="> 0: the training loop's epoch shape (TRAIN_FINAL.py:246-298 over the DataLoader of "
                          ":1298; BASELINE configs[3]): a dataset of --dataset-graphs meshes sharded by rank "
@@ -289,8 +286,7 @@ def main():
         else:
             pool = [synthetic.make_mesh_graph(c["n"], 1000 * rank + g, super_node=c["super_node"])
                     for g in range(args.store_graphs)]
-        store = (bgnn.GraphStore(pool, dev, reorder=None if args.reorder < 0 else bool(args.reorder))
-                 if args.data == "store" else None)
+        store = bgnn.GraphStore(pool, dev) if args.data == "store" else None
         rng = np.random.default_rng(rank)
         order = iter(())
         epoch = -1
@@ -435,8 +431,6 @@ def main():
                            "host": f"new shuffled batch every step collated on the host from {args.store_graphs} "
                                    f"meshes and copied to the GPU (reference DataLoader path)"}[args.data],
             "data_path": args.data,
-            **({"node_order": "cluster_order (8-row groups)" if store.reorder else "dataset order (4-row groups)"}
-               if args.data == "store" else {}),
             **({"epochs": args.epochs, "dataset_graphs": args.dataset_graphs or args.store_graphs * world,
                 "steps_per_epoch": args.steps // args.epochs} if args.epochs > 0 else {}),
             "global_batch": bsz * world,

@@ -43,103 +43,12 @@ def _heavy_counts(rowptr: torch.Tensor, gid: torch.Tensor, G: int, chunk: int):
     return h, c
 
 
-def cluster_order(src: np.ndarray, dst: np.ndarray, n: int, strip: int = 4) -> np.ndarray:
-    """A node order for row groups of 2 * strip rows (graph-local; returns new -> old node ids).
-
-    The row-group aggregation kernels (csrc/spmm.hip k_seg_group) fetch every distinct source
-    row of a group of consecutive target rows once. In the order a mesh is numbered (sorted
-    Nastran ids, GraphCreate.py:150: row-major), consecutive rows are a 1-D strip of the mesh,
-    whose neighbourhoods overlap along one direction only. Here the graph's strips of `strip`
-    consecutive rows are paired greedily, each with the not yet paired strip that shares the most
-    source rows (on a mesh: the strip one mesh row away), and each pair is placed consecutively,
-    so a group of 2 * strip rows is a 2-D patch: cfg2 meshes fetch 4.23 source rows per target row
-    in groups of 8 instead of 4.74 (1-D strips of 8) or 5.47 (strips of 4). Strips left unpaired
-    (and a last partial strip) go to the end. Generic: uses the edge list only."""
-    n = int(n)
-    order = np.argsort(dst, kind="stable")
-    rp = np.zeros(n + 1, np.int64)
-    np.add.at(rp, dst + 1, 1)
-    rp = np.cumsum(rp)
-    s_sorted = src[order]
-    G = (n + strip - 1) // strip
-    keys = [set(s_sorted[rp[g * strip]:rp[min(n, g * strip + strip)]].tolist()) for g in range(G)]
-    full = [min(n, g * strip + strip) - g * strip == strip for g in range(G)]
-    partner = [-1] * G
-    for g in range(G):
-        if partner[g] >= 0 or not full[g]:
-            continue
-        best, bs = -1, 0
-        for c in sorted({k // strip for k in keys[g]}):
-            if c == g or partner[c] >= 0 or not full[c]:
-                continue
-            sh = len(keys[g] & keys[c])
-            if sh > bs:
-                bs, best = sh, c
-        if best >= 0:
-            partner[g], partner[best] = best, g
-    perm, rest, done = [], [], [False] * G
-    for g in range(G):
-        if done[g]:
-            continue
-        done[g] = True
-        rows = list(range(g * strip, min(n, g * strip + strip)))
-        if partner[g] >= 0:
-            p = partner[g]
-            done[p] = True
-            perm += rows + list(range(p * strip, p * strip + strip))
-        else:
-            rest += rows
-    return np.asarray(perm + rest, dtype=np.int64)
-
-
-# GraphStore default: renumber every graph's nodes by cluster_order and aggregate in row groups of 8
-# (the row-group plans of 2-D patches); False keeps the dataset's node order and groups of 4
-REORDER = False
-
-
-def _reordered(d: Data, perm: np.ndarray) -> Data:
-    """d with its nodes renumbered: new node i is old node perm[i] (per-node tensors permuted,
-    edge_index relabelled, edge order and every other attribute unchanged)."""
-    n = d.num_nodes
-    inv = np.empty(n, dtype=np.int64)
-    inv[perm] = np.arange(n)
-    pt, it = torch.from_numpy(perm), torch.from_numpy(inv)
-    out = Data()
-    for k, v in d.items():
-        if k == "edge_index":
-            out[k] = it[v.to(torch.int64)].to(v.dtype)
-        elif isinstance(v, torch.Tensor) and v.dim() > 0 and v.size(0) == n:
-            out[k] = v.index_select(0, pt.to(v.device))
-        else:
-            out[k] = v
-    if "num_nodes" in d.keys():
-        out["num_nodes"] = n
-    return out
-
-
 class GraphStore:
-    """All graphs of a dataset resident on one GPU, with graph-local CSR structures.
+    """All graphs of a dataset resident on one GPU, with graph-local CSR structures."""
 
-    reorder=True renumbers each graph's nodes by cluster_order (new node i = old node
-    node_perm[g][i]; the batches then carry the renumbered graphs -- isomorphic, so graph-level
-    outputs such as the buckling prediction are unchanged up to float summation order) and plans
-    row groups of 8 rows."""
-
-    def __init__(self, graphs: Sequence[Data], device=None, chunk: int = DEFAULT_CHUNK,
-                 reorder: Optional[bool] = None):
+    def __init__(self, graphs: Sequence[Data], device=None, chunk: int = DEFAULT_CHUNK):
         if len(graphs) == 0:
             raise ValueError("GraphStore: empty dataset")
-        self.reorder = REORDER if reorder is None else bool(reorder)
-        self.node_perm = None
-        if self.reorder:
-            self.node_perm = []
-            out = []
-            for d in graphs:
-                ei = d.edge_index.to(torch.int64).cpu().numpy()
-                perm = cluster_order(ei[0], ei[1], d.num_nodes)
-                self.node_perm.append(perm)
-                out.append(_reordered(d, perm))
-            graphs = out
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if dev.type != "cuda":
             raise RuntimeError("GraphStore: the store lives in GPU memory (bgnn has no CPU fallback)")
@@ -203,7 +112,7 @@ class GraphStore:
         heavy = torch.zeros(G, 4, dtype=torch.int64, device=dev)
         # row-group plans (bgnn_group_plan), per graph: groups start at the graph's first node, so
         # a batch's plan is the concatenation of its graphs' plans (bgnn_store_gather_groups)
-        R = (8 if self.reorder else _graph.GROUP_ROWS) if chunk <= 64 else 0
+        R = _graph.GROUP_ROWS if chunk <= 64 else 0
         self.group_rows = R
         if R > 0:
             self.n_groups = (n + R - 1) // R

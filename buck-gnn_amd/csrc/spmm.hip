@@ -717,7 +717,7 @@ __global__ __launch_bounds__(256) void k_seg_sweep(SegArgs A) {
 // first row it is CSR order), so results match the sweep kernel to rounding, not bitwise.
 // (Measured in round 2 and dropped: issuing the group's z_r loads before its gathers, 160 -> 188
 // us, and 16 source rows per gather batch, 160 -> 168 us; profiles/r02_tune_agg_knobs.txt.)
-template <int NV, int OP, int EPI, int R, int U, int BR = 0>
+template <int NV, int OP, int EPI, int R, int U>
 __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -822,25 +822,17 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                     for (int u = 0; u < U; ++u)
 #pragma unroll
                         for (int t = 0; t < R; ++t) {
-                            const bool on = (m[u] >> t) & 1u;
-                            if constexpr (BR) {   // wave-uniform mask bit: add only where the key is used
-                                if (__builtin_amdgcn_readfirstlane((int)on)) {
+                            // the mask bit is wave-uniform (j[u], m[u] come from readlane): add only
+                            // where the key is used, by a scalar branch (measured: spmm_bwd 138.5 ->
+                            // 135.9 us against a per-lane select, profiles/r04_ab_agg_knobs.txt)
+                            if (__builtin_amdgcn_readfirstlane((int)((m[u] >> t) & 1u))) {
 #pragma unroll
-                                    for (int v = 0; v < NV; ++v)
+                                for (int v = 0; v < NV; ++v)
 #pragma unroll
-                                        for (int q = 0; q < 4; ++q)
-                                            a[t][v][q] += (OP == OP_MEANT) ? __fmul_rn(val[u][v].f[q], w[u])
-                                                                           : val[u][v].f[q];
-                                }
-                                continue;
+                                    for (int q = 0; q < 4; ++q)
+                                        a[t][v][q] += (OP == OP_MEANT) ? __fmul_rn(val[u][v].f[q], w[u])
+                                                                       : val[u][v].f[q];
                             }
-#pragma unroll
-                            for (int v = 0; v < NV; ++v)
-#pragma unroll
-                                for (int q = 0; q < 4; ++q) {
-                                    const float x = (OP == OP_MEANT) ? __fmul_rn(val[u][v].f[q], w[u]) : val[u][v].f[q];
-                                    a[t][v][q] += on ? x : 0.f;
-                                }
                         }
                 }
             }
@@ -929,8 +921,6 @@ constexpr int kMaxLightBlocks = 1024;
 static int g_seg_kernel = 0;     // 0 = auto (row-group kernel where planned, else sweep), 1 = blocked,
                                  // 2 = sweep
 static int g_grp_blocks = 1024;  // row-group kernel grid (4 blocks of 4 waves per CU)
-static int g_grp_br = 0;         // EXPERIMENT (knob 14): row-group accumulate by uniform branches
-static int g_grp_blocks_plain = 0;   // EXPERIMENT (knob 15): plain-epilogue row-group grid (0 = g_grp_blocks)
 static int g_seg_blocks = 1024;  // sweep grid (rounded to a multiple of 8)
 static int g_seg_nt = 1;         // non-temporal hints on stream-once data (default on: +8 % fwd)
 static int g_seg_u = 0;          // neighbours per gather batch in the sweep kernel (0 = auto = 12:
@@ -981,9 +971,9 @@ inline int64_t sweep_grid(int64_t n_rows) {
     return blocks < 8 ? 8 : blocks;
 }
 
-inline int64_t group_grid(int64_t G, bool plain = false) {
+inline int64_t group_grid(int64_t G) {
     int64_t want = (G + 3) / 4;                      // at most one group per wave
-    int64_t blocks = (plain && g_grp_blocks_plain) ? g_grp_blocks_plain : g_grp_blocks;
+    int64_t blocks = g_grp_blocks;
     if (want < blocks) blocks = want;
     blocks = (blocks + 7) / 8 * 8;
     return blocks < 8 ? 8 : blocks;
@@ -1007,7 +997,7 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     const bool sweep = (VEC == 4 && LPR == 64 && g_seg_kernel != 1 && A.chunk <= 64);
     int64_t blocks;
     if (group) {
-        blocks = group_grid(A.n_groups, EPI == EPI_PLAIN);
+        blocks = group_grid(A.n_groups);
     } else if (sweep || EPI == EPI_SAGE) {   // SAGE: slot count = bgnn_sage_fwd_slots() for either kernel
         blocks = sweep_grid(A.n_rows);
         rpb = (A.n_rows + blocks - 1) / blocks;
@@ -1028,8 +1018,6 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
                 const dim3 gr((unsigned)blocks);
                 if (A.group_rows == 8)
                     hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 8>), gr, dim3(256), 0, s, A);
-                else if (g_grp_br)
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8, 1>), gr, dim3(256), 0, s, A);
                 else
                     hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8>), gr, dim3(256), 0, s, A);
                 BGNN_CHECK_LAUNCH();
@@ -1201,8 +1189,6 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
         case BGNN_TUNE_ROWS_REV: return rows_rev();
-        case 14: return g_grp_br;
-        case 15: return g_grp_blocks_plain;
         default: return -1;
     }
 }
@@ -1229,8 +1215,6 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
-        case 14: g_grp_br = value ? 1 : 0; return BGNN_OK;
-        case 15: g_grp_blocks_plain = value; return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value == 0 || value == 2, "set_tuning: gemm mode must be 0 (f32 MFMA) or 2 (f16x3)");
             set_gemm_mode(value);

@@ -147,66 +147,3 @@ def test_train_step_on_store_batch_equals_host_batch(dev, super_node):
     for a, b in zip(results[0][1], results[1][1]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()) + 1e-12)
 
-
-def test_cluster_order_is_a_permutation_pairing_strips():
-    from bgnn.store import cluster_order
-    for s in range(3):
-        d = S.make_mesh_graph(24, seed=s, super_node=(s == 2))
-        ei = d.edge_index.numpy()
-        p = cluster_order(ei[0], ei[1], d.num_nodes)
-        assert sorted(p.tolist()) == list(range(d.num_nodes))
-        # paired strips are placed whole: every aligned block of 4 new rows is one old strip
-        full = (d.num_nodes // 4) * 4
-        for b in range(0, full // 8 * 8, 4):
-            blk = p[b:b + 4]
-            assert blk[0] % 4 == 0 and (blk == blk[0] + np.arange(4)).all()
-
-
-def test_store_reorder_batches_are_renumbered_graphs(dev):
-    """reorder=True: every batch is the collation of the renumbered graphs (new node i = old node
-    node_perm[g][i]); row groups of 8 rows start at every graph's first node; the structures equal
-    fresh builds of the collated edge_index; a train step's loss equals the dataset-order one to
-    fp32 summation order (the graphs are isomorphic)."""
-    from bgnn.graph import enqueue_groups
-    from bgnn.store import _reordered
-    gs = dataset()
-    store = bgnn.GraphStore(gs, dev, chunk=16, reorder=True)
-    assert store.reorder and store.group_rows == 8
-    ids = [6, 2, 8, 0, 3]
-    b = store.batch(ids)
-    ref = Batch.from_data_list([_reordered(gs[i], store.node_perm[i]) for i in ids]).to(dev)
-    for k in ("x", "edge_index", "edge_attr", "y", "batch", "ptr"):
-        assert torch.equal(b[k], ref[k]), k
-    for i in ids:   # the renumbering itself: x rows follow node_perm, edges are relabelled
-        p = torch.from_numpy(store.node_perm[i])
-        r = _reordered(gs[i], store.node_perm[i])
-        assert torch.equal(r.x, gs[i].x[p])
-        inv = torch.empty_like(p)
-        inv[p] = torch.arange(len(p))
-        assert torch.equal(r.edge_index, inv[gs[i].edge_index])
-    g = _graph_cache.peek(b.edge_index, (b.num_nodes, 16))
-    r = Graph.build(ref.edge_index, ref.num_nodes, chunk=16)
-    csr_equal(g.fwd, r.fwd)
-    csr_equal(g.bwd, r.bwd)
-    gf = g.fwd.groups
-    assert gf.rows == 8
-    ptr = ref.ptr.cpu().tolist()
-    want = [p + k * 8 for p, q in zip(ptr[:-1], ptr[1:]) for k in range((q - p + 7) // 8)] + [ptr[-1]]
-    assert gf.grow.cpu().tolist() == want
-    for mine, csr in ((g.fwd, r.fwd), (g.bwd, r.bwd)):
-        want_g = enqueue_groups(csr.rowptr, csr.col, r.num_nodes, r.num_edges, 16, 8, gf.grow, gf.n_groups)
-        groups_equal(mine.groups, want_g, csr.rowptr)
-
-    # graph-level outputs are invariant under the renumbering
-    mesh = [S.make_mesh_graph(20, seed=s) for s in range(4)]
-    outs = []
-    for reorder in (False, True):
-        bgnn.clear_caches()
-        torch.manual_seed(0)
-        model = bgnn.BuckGNN(16, 5, hidden_channels=128, num_layers=6, dropout_rate=0.0,
-                             model_name="GraphSage_addAggr").to(dev).eval()
-        st = bgnn.GraphStore(mesh, dev, reorder=reorder)
-        bb = st.batch([0, 1, 2, 3])
-        with torch.no_grad():
-            outs.append(model(bb.x, bb.edge_index, bb.edge_attr, bb.batch).detach().clone())
-    torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-5)

@@ -3,17 +3,68 @@
 training step runs them: the fused SAGE forward (bgnn_sage_fwd, z interleaved [N, 2H]) and the
 transpose aggregation (bgnn_spmm_bwd, dh = dz[:, H:] -> dz[:, :H]); 1 GiB cache flush between
 launches, median HIP-event times, bit-identity against the first setting.
-    python tools/agg_knob_ab.py [--config cfg2] [--rounds 15] "" "14=1" "15=1280" ..."""
+    python tools/agg_knob_ab.py [--config cfg2] [--rounds 15] "" "7=2048" ..."""
 import argparse
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "buck-gnn_amd"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from bgnn import _lib, synthetic  # noqa: E402
 from bgnn.graph import Graph  # noqa: E402
+
+
+def cluster_order(src: np.ndarray, dst: np.ndarray, n: int, strip: int = 4) -> np.ndarray:
+    """(Round-4 experiment, not adopted: R = 8 groups over this order ran slower than R = 4 in
+    dataset order, profiles/r04_ab_agg_knobs.txt.) A node order for row groups of 2 * strip rows (graph-local; returns new -> old node ids).
+
+    The row-group aggregation kernels (csrc/spmm.hip k_seg_group) fetch every distinct source
+    row of a group of consecutive target rows once. In the order a mesh is numbered (sorted
+    Nastran ids, GraphCreate.py:150: row-major), consecutive rows are a 1-D strip of the mesh,
+    whose neighbourhoods overlap along one direction only. Here the graph's strips of `strip`
+    consecutive rows are paired greedily, each with the not yet paired strip that shares the most
+    source rows (on a mesh: the strip one mesh row away), and each pair is placed consecutively,
+    so a group of 2 * strip rows is a 2-D patch: cfg2 meshes fetch 4.23 source rows per target row
+    in groups of 8 instead of 4.74 (1-D strips of 8) or 5.47 (strips of 4). Strips left unpaired
+    (and a last partial strip) go to the end. Generic: uses the edge list only."""
+    n = int(n)
+    order = np.argsort(dst, kind="stable")
+    rp = np.zeros(n + 1, np.int64)
+    np.add.at(rp, dst + 1, 1)
+    rp = np.cumsum(rp)
+    s_sorted = src[order]
+    G = (n + strip - 1) // strip
+    keys = [set(s_sorted[rp[g * strip]:rp[min(n, g * strip + strip)]].tolist()) for g in range(G)]
+    full = [min(n, g * strip + strip) - g * strip == strip for g in range(G)]
+    partner = [-1] * G
+    for g in range(G):
+        if partner[g] >= 0 or not full[g]:
+            continue
+        best, bs = -1, 0
+        for c in sorted({k // strip for k in keys[g]}):
+            if c == g or partner[c] >= 0 or not full[c]:
+                continue
+            sh = len(keys[g] & keys[c])
+            if sh > bs:
+                bs, best = sh, c
+        if best >= 0:
+            partner[g], partner[best] = best, g
+    perm, rest, done = [], [], [False] * G
+    for g in range(G):
+        if done[g]:
+            continue
+        done[g] = True
+        rows = list(range(g * strip, min(n, g * strip + strip)))
+        if partner[g] >= 0:
+            p = partner[g]
+            done[p] = True
+            perm += rows + list(range(p * strip, p * strip + strip))
+        else:
+            rest += rows
+    return np.asarray(perm + rest, dtype=np.int64)
 
 
 def main():
@@ -30,7 +81,6 @@ def main():
     b = synthetic.make_config_batch(args.config)
     ei = b.edge_index
     if args.reorder:
-        from bgnn.store import cluster_order
         import numpy as np
         src, dst = ei.numpy()
         inv = np.empty(b.num_nodes, np.int64)

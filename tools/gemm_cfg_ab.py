@@ -14,7 +14,7 @@ import torch  # noqa: E402
 
 from bgnn import _lib, fused  # noqa: E402
 
-M, H = 80656, 512
+H = 512
 
 
 def main():
@@ -22,7 +22,9 @@ def main():
     ap.add_argument("--cfgs", default="-1,5,6,7")
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--shapes", default="fwd,dgrad,dropadd,wgrad")
+    ap.add_argument("--rows", type=int, default=80656, help="M (node rows; cfg2 = 80656)")
     args = ap.parse_args()
+    M = args.rows
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     x = torch.randn(M, H, device=dev)

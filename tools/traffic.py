@@ -27,6 +27,8 @@ KERNELS = {
     "gemm_wgrad": ("k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0>",),   # wgrad (split-K partial products)
     "sage_fwd": ("k_seg_group<2, 0, 1,", "k_seg_sweep<2, 0, 1,"),   # fused SAGE forward aggregation
     "spmm_bwd": ("k_seg_group<2, 0, 0,", "k_seg_sweep<2, 0, 0,"),   # transpose aggregation
+    "ea_edge_b16": ("k_gemm_b16<",),   # EA_GNN bf16 per-edge Linears (gathered and plain epilogues)
+    "ea_wgrad_b16": ("k_gemm_x6<2, 1, 0, 256, 256, 4, 2, 19>",),   # EA_GNN bf16 per-edge weight gradients
 }
 
 
