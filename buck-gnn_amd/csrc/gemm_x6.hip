@@ -142,11 +142,22 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
 // 8-k units, written as the same [row][32 k] swizzled images as the K-contiguous path (so
 // the MFMA reads are unchanged). Quads of A go to threads [0, BM), of B to [BM, BM + BN).
 // Measured (wgrad 1024x512x80656, 256x256 tiles): 804 -> 300 us against per-lane dword loads.
-template <int R, bool FULL, bool BF = false>
+// KTAIL: rows in range and 16-B aligned, only k may run past kend (the last split-K slab of a
+// K that is no multiple of the slice): float4 loads from row min(k, kend - 1), zeroed past kend.
+template <int R, bool FULL, bool BF = false, bool KTAIL = false>
 __device__ __forceinline__ void kq_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
                                         int64_t kend, bool vec_ok, float (&v)[4][8], int q) {
     const int r4 = q % (R / 4), c = q / (R / 4);
     const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
+    if constexpr (KTAIL && !BF) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool ok = gk + k < kend;
+            const float4 f = *reinterpret_cast<const float4*>(P + (ok ? gk + k : kend - 1) * ld + gr);
+            v[0][k] = ok ? f.x : 0.f; v[1][k] = ok ? f.y : 0.f; v[2][k] = ok ? f.z : 0.f; v[3][k] = ok ? f.w : 0.f;
+        }
+        return;
+    }
     if constexpr (BF) {   // bf16 storage: 4 consecutive rows = one 8-B load per k
         const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
 #pragma unroll
@@ -305,13 +316,16 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // 341 us, dgrad 324 -> 359, wgrad 303 -> 406 in an interleaved A/B, profiles/r03_*)
     // the main loop is instantiated twice (interior tiles without guards, edge tiles with
     // them) and selected once, so the hot loop carries no per-slice bounds branches
-    auto mainloop = [&](auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
+    // MODE 1 = interior tile, 2 = interior rows / columns with a ragged K range (k-major quads
+    // only), 0 = edge tile (element guards)
+    auto mainloop = [&](auto mode_tag) {
+        constexpr int MODE = decltype(mode_tag)::value;
+        constexpr bool FULL = MODE == 1, KT = MODE == 2;
         auto load_ab = [&](int64_t k0, Regs& r) {
             const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
             if constexpr (KQ) {
-                if (t < BM) kq_load<BM, FULL, A16>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
-                else if (t < BM + BN) kq_load<BN, FULL, B16>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+                if (t < BM) kq_load<BM, FULL, A16, KT>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
+                else if (t < BM + BN) kq_load<BN, FULL, B16, KT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
             } else {
                 x6_load<AK, BM, NT, FULL, A16>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
                 x6_load<BKc, BN, NT, FULL, B16>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
@@ -381,8 +395,22 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
         }
     };
-    if (full) mainloop(std::true_type{});
-    else mainloop(std::false_type{});
+    if (full) {
+        mainloop(std::integral_constant<int, 1>{});
+    } else {
+        // the last split-K slab of the weight gradient (K = the node count, rarely a multiple of
+        // 32): interior rows and columns, only k ragged -- the guarded edge loop would set the
+        // whole kernel's time (one round of workgroups: 413 vs 280 us at K = 80,656 vs 80,640)
+        bool ktail = false;
+        if constexpr (KQ && !A16 && !B16)
+            ktail = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && (g.lda % 4 == 0) && (g.ldb % 4 == 0);
+        if constexpr (KQ && !A16 && !B16) {
+            if (ktail) mainloop(std::integral_constant<int, 2>{});
+            else mainloop(std::integral_constant<int, 0>{});
+        } else {
+            mainloop(std::integral_constant<int, 0>{});
+        }
+    }
     // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
     x6_epilogue<TM, TN, ABL, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
