@@ -150,6 +150,14 @@ __device__ __forceinline__ void kq_load(const float* __restrict__ P, int64_t ld,
     const int r4 = q % (R / 4), c = q / (R / 4);
     const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
     if constexpr (KTAIL && !BF) {
+        if (k0 + X6_BK <= kend) {   // (uniform) every slice but the last: the interior loads
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 f = *reinterpret_cast<const float4*>(P + (gk + k) * ld + gr);
+                v[0][k] = f.x; v[1][k] = f.y; v[2][k] = f.z; v[3][k] = f.w;
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const bool ok = gk + k < kend;

@@ -1017,7 +1017,7 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
             if (group) {
                 const dim3 gr((unsigned)blocks);
                 if (A.group_rows == 8)
-                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 8>), gr, dim3(256), 0, s, A);
+                    hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 8, 4>), gr, dim3(256), 0, s, A);
                 else
                     hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 8>), gr, dim3(256), 0, s, A);
                 BGNN_CHECK_LAUNCH();
