@@ -418,15 +418,16 @@ __global__ __launch_bounds__(256) void k_seg_chunk(SegArgs A) {
     }
 }
 
-// Combine heavy rows: one 256-thread block per heavy row (and column tile). For SUM / MEAN the
-// four waves sum four contiguous quarters of the row's chunks and wave 0 adds the quarter sums
-// in order: a fixed summation tree (deterministic, the same for every light-row kernel
-// variant) with 4x the memory parallelism of one wave walking 79 chunks of a super node
-// (cfg3: 44 us -> see DESIGN.md). MAX keeps one wave walking the chunks in order
-// (first-occurrence argmax).
+// Combine heavy rows: one block per heavy row (and column tile). For SUM / MEAN the block's 16
+// waves (1024 threads) sum 16 contiguous runs of the row's chunks and wave 0 adds the 16 run
+// sums in order: a fixed summation tree (deterministic, the same for every light-row kernel
+// variant). A cfg3 super node has 79 chunks, so each wave loads 5 partial rows in one batch:
+// one memory round trip instead of three (4 waves: 17 us per launch; one wave: 44 us). MAX keeps
+// one wave walking the chunks in order (first-occurrence argmax), launched with 256 threads.
+constexpr int kCombineWaves = 16;
 template <int VEC, int NV, int LPR, int OP, int EPI>
-__global__ __launch_bounds__(256) void k_seg_combine(SegArgs A) {
-    constexpr int W = (OP == OP_MAX) ? 1 : 4;
+__global__ __launch_bounds__(1024) void k_seg_combine(SegArgs A) {
+    constexpr int W = (OP == OP_MAX) ? 1 : kCombineWaves;
     constexpr int TW = LPR * VEC * NV;   // columns of one column tile
     __shared__ __attribute__((aligned(16))) float red[W][TW];
     const int lane = threadIdx.x & 63;
@@ -486,7 +487,10 @@ __global__ __launch_bounds__(256) void k_seg_combine(SegArgs A) {
 #pragma unroll
                     for (int q = 0; q < VEC; ++q) {
                         const int i = cpos[v] - cb + q;
-                        acc.a[v][q] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+                        float t = red[0][i];
+#pragma unroll
+                        for (int w = 1; w < W; ++w) t += red[w][i];
+                        acc.a[v][q] = t;
                     }
         }
     }
@@ -1052,7 +1056,8 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
                            A);
         BGNN_CHECK_LAUNCH();
         constexpr int MOP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MEAN ? OP_MEAN : OP_SUM);
-        hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles), dim3(256), 0, s, A);
+        hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles),
+                           dim3(MOP == OP_MAX ? 256 : 64 * kCombineWaves), 0, s, A);
         BGNN_CHECK_LAUNCH();
     }
     return BGNN_OK;
