@@ -48,7 +48,7 @@ FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.m
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md)
 X6_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6   # f32-equivalent ceiling of the 6-product bf16 split GEMM
 H3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 3   # f32-equivalent ceiling of the 3-product f16 split GEMM (f16 = bf16 rate)
-TRAFFIC_FILE = "traffic_r03w.json"   # rocprofv3 PMC passes of this bench (tools/gpu_round.sh)
+TRAFFIC_FILE = "traffic_r04k.json"   # rocprofv3 PMC passes of this bench (tools/gpu_r4p.sh TAG pmc)
 METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"   # BASELINE.json
 
 
@@ -355,7 +355,10 @@ def main():
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
     if os.path.exists(tpath):
         try:
-            traffic = {k: v["bytes_per_launch"] for k, v in json.load(open(tpath))["kernels"].items()}
+            tj = json.load(open(tpath))
+            cfgk = "ea5" if (is_ea and args.bf16 and args.config == "cfg5") else args.config
+            kern = tj.get("configs", {}).get(cfgk, tj["kernels"])
+            traffic = {k: v["bytes_per_launch"] for k, v in kern.items()}
         except (ValueError, OSError, KeyError):
             traffic = {}
     gmode = _lib.query("bgnn_get_tuning", 5) if args.gemm == "hip" else -1
@@ -499,7 +502,9 @@ def main():
             "kernel": "per-edge GraphNetBlock GEMMs (edge_mlp / phi, K = H = 512; gather-add + ReLU epilogues): "
                       + ("k_gemm_x6 bf16 operands" if args.bf16 else "k_gemm_x6 f16x3"),
             "bound": "hbm", "achieved": round(ea_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ea_gbs / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": ea_bytes,
+            "frac": round(ea_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic.get("ea_edge_b16") if (args.bf16 and ea_mod.BF16_STORAGE) else None,
+            "algorithmic_bytes": ea_bytes,
             "avg_launch_ms": round(ea_ms, 5), "launches": n_ea,
             "ms_per_step": round(ea_ms * n_ea / args.steps, 4) if n_ea else float("nan"),
             "mfma": {"achieved": round(ea_tfs, 2), "peak": ea_peak, "unit": "TFLOP/s",
