@@ -220,6 +220,47 @@ __device__ __forceinline__ void kq_store(uint4* __restrict__ S, const float (&v)
 
 
 
+// k-major quads of a bf16-STORED operand kept packed (PREC 2, A and B both bf16: the EA_GNN
+// weight gradient g^T e, K = E): per k one 8-B load of 4 consecutive rows, held as the raw
+// 16-bit pairs (8 VGPRs per quad instead of 32 widened floats), so two register sets fit and
+// the slice pipeline runs at prefetch distance 2. The LDS image is the one kq_store writes
+// (bf16 values are exact, the same bits).
+template <int R, bool FULL>
+__device__ __forceinline__ void kq_load16(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
+                                          int64_t kend, bool vec_ok, uint2 (&f)[8], int q) {
+    const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
+    const int r4 = q % (R / 4), c = q / (R / 4);
+    const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
+            f[k] = *reinterpret_cast<const uint2*>(P16 + (gk + k) * ld + gr);
+        } else {
+            uint32_t e[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) e[i] = (gr + i < Rlim && gk + k < kend) ? P16[(gk + k) * ld + gr + i] : 0u;
+            f[k] = make_uint2(e[0] | (e[1] << 16), e[2] | (e[3] << 16));
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void kq_store16(uint4* __restrict__ S, const uint2 (&f)[8], int q) {
+    const int r4 = q % (R / 4), c = q / (R / 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = (i < 2) ? f[k].x : f[k].y;
+        uint32_t p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            p[j] = (i & 1) ? ((w[2 * j] >> 16) | (w[2 * j + 1] & 0xffff0000u))
+                           : ((w[2 * j] & 0xffffu) | (w[2 * j + 1] << 16));
+        S[x6_pos(4 * r4 + i, c)] = make_uint4(p[0], p[1], p[2], p[3]);
+    }
+}
+
 // the leading piece products of one 16-deep k-step, small terms first
 template <int TM, int TN, int PREC, int NP>
 __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa)[TM][NP],
@@ -311,11 +352,14 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // and kt+3 are in flight (prefetch distance 2; ABL 7 = distance 1 for measurement). The
     // second set fits the VGPR budget only for K-contiguous operands and tiles up to 256x128
     // (measured: fwd 363 -> 334 us, dgrad 384 -> 322 us at 256x128).
-    constexpr int PF = (ABL == 7 || BM * BN > 256 * 128 || (!(AK && BKc) && !KQ)) ? 1 : 2;
+    // both k-major operands stored bf16: the quads stay packed (kq_load16), two sets fit
+    constexpr bool KQ16 = KQ && A16 && B16 && PREC == 2;
+    constexpr int PF = (ABL == 7 || (BM * BN > 256 * 128 && !KQ16) || (!(AK && BKc) && !KQ)) ? 1 : 2;
     // k-major quad staging for the weight gradient (both operands k-major, f16x3)
     struct RegsStd { float a[BM * 4 / NT][8]; float b[BN * 4 / NT][8]; };
     struct RegsKQ { float q[4][8]; };
-    using Regs = std::conditional_t<KQ, RegsKQ, RegsStd>;
+    struct RegsKQ16 { uint2 q[8]; };
+    using Regs = std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ, RegsStd>>;
     Regs rs[2];
     const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
@@ -331,7 +375,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         constexpr bool FULL = MODE == 1, KT = MODE == 2;
         auto load_ab = [&](int64_t k0, Regs& r) {
             const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
-            if constexpr (KQ) {
+            if constexpr (KQ16) {
+                if (t < BM) kq_load16<BM, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
+                else if (t < BM + BN) kq_load16<BN, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+            } else if constexpr (KQ) {
                 if (t < BM) kq_load<BM, FULL, A16, KT>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
                 else if (t < BM + BN) kq_load<BN, FULL, B16, KT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
             } else {
@@ -340,7 +387,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             }
         };
         auto store_ab = [&](int buf, const Regs& r) {
-            if constexpr (KQ) {
+            if constexpr (KQ16) {
+                if (t < BM) kq_store16<BM>(As[buf], r.q, t);
+                else if (t < BM + BN) kq_store16<BN>(Bs[buf], r.q, t - BM);
+            } else if constexpr (KQ) {
                 if (t < BM) kq_store<BM, PREC>(As[buf], r.q, t, sa);
                 else if (t < BM + BN) kq_store<BN, PREC>(Bs[buf], r.q, t - BM, sb);
             } else {
