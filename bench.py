@@ -340,12 +340,18 @@ def main():
         return sum(a.elapsed_time(b) for a, b in ev) / len(ev) if ev else float("nan")
 
     N, E, H = batch.num_nodes, batch.num_edges, 512
-    agg_ms = avg_ms("sage_fwd")
-    agg_bytes = 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
+    is_max = "maxAggr" in args.model
+    if is_max and "gemm_fwd_max" in timers:   # (the aggregate-first transform: same flops, K = 2H)
+        timers.setdefault("gemm_fwd", timers["gemm_fwd_max"])
+    # max aggregation (aggregate-first, bgnn/fused.py::_max_transform): bgnn_spmm_fwd(MAX) reads each
+    # source row once and writes agg and its argmax; the SAGE row epilogue runs separately
+    agg_ms = avg_ms("agg_max" if is_max else "sage_fwd")
+    agg_bytes = (3 * N * H * 4 + 4 * E + 4 * (N + 1)) if is_max else 3 * N * H * 4 + 4 * E + 4 * (N + 1) + 4 * N
     agg_gbs = agg_bytes / (agg_ms * 1e-3) / 1e9
     # transpose aggregation (bgnn_spmm_bwd): SURVEY.md §8d's per-layer aggregation bytes
     bwd_ms = avg_ms("spmm_bwd")
-    bwd_bytes = 2 * N * H * 4 + 4 * E + 4 * (N + 1)
+    # max: bgnn_spmm_bwd_add(MAXT) reads dagg, its argmax and the addend dh W_r, writes dx
+    bwd_bytes = (4 if is_max else 2) * N * H * 4 + 4 * E + 4 * (N + 1)
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     seg_kernel = _lib.query("bgnn_get_tuning", 1)
     from bgnn import graph as _graph
@@ -455,26 +461,28 @@ def main():
                                "tflop_per_step": round(tot_flop / args.steps / 1e12, 4)},
         },
         "roofline_hbm": {
-            "kernel": "bgnn_sage_fwd: " + agg_name.format(e=1)
-                      + ", SAGE epilogue (+chunk/combine for super nodes)",
+            "kernel": ("bgnn_spmm_fwd(MAX) with the per-element argmax (aggregate-first max layer)" if is_max else
+                       "bgnn_sage_fwd: " + agg_name.format(e=1)
+                       + ", SAGE epilogue (+chunk/combine for super nodes)"),
             "bound": "hbm",
             "achieved": round(agg_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(agg_gbs / HBM_PEAK_GBS, 4),
-            "traffic": traffic.get("sage_fwd"),
+            "traffic": None if is_max else traffic.get("sage_fwd"),
             "algorithmic_bytes": agg_bytes,
             "avg_launch_ms": round(agg_ms, 5),
-            "launches": len(timers.get("sage_fwd", [])),
+            "launches": len(timers.get("agg_max" if is_max else "sage_fwd", [])),
         },
         "roofline_agg_bwd": {
-            "kernel": "bgnn_spmm_bwd (transpose aggregation): " + agg_name.format(e=0),
+            "kernel": ("bgnn_spmm_bwd_add(MAXT): argmax scatter of dagg + the dh W_r addend" if is_max else
+                       "bgnn_spmm_bwd (transpose aggregation): " + agg_name.format(e=0)),
             "bound": "hbm",
             "achieved": round(bwd_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
-            "traffic": traffic.get("spmm_bwd"),
+            "traffic": None if is_max else traffic.get("spmm_bwd"),
             "algorithmic_bytes": bwd_bytes,
             "avg_launch_ms": round(bwd_ms, 5),
             "launches": len(timers.get("spmm_bwd", [])),

@@ -838,7 +838,8 @@ def _max_transform(x, w_l, w_r, graph: Graph, x_amax, w_amax, name: str):
     Returns (y, agg, arg)."""
     from .ops import spmm_fwd
     N, C = x.shape
-    agg, arg = spmm_fwd(graph.fwd, x, 2, N, want_arg=True)
+    with _timed("agg_max"):
+        agg, arg = spmm_fwd(graph.fwd, x, 2, N, want_arg=True)
     wk = torch.cat([w_l, w_r], 1)                                    # [H, 2C]
     a = Pair(agg, x) if C % 32 == 0 else torch.cat([agg, x], 1)
     with _timed(name):
