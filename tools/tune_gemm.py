@@ -2,7 +2,7 @@
 """A/B the GEMM kernels and tile configurations (and torch.mm) on the SAGE layer shapes,
 interleaved in one process; median per-launch HIP-event time, TFLOP/s, and the error
 against an fp64 product as max_ij |c - c64|_ij / (|A| |B|)_ij.
-Variants: "3" = f32 MFMA config 3, "x1" = bf16x6 config 1, "h1" = f16x3 config 1,
+Variants: "3" = f32 MFMA config 3, "h1" = f16x3 config 1 (bf16x6 "x" variants removed in ABI 9),
 "torch" = torch.mm; add 100*k to a config for timing ablation k (wrong results)."""
 import argparse
 import os
@@ -24,7 +24,7 @@ SHAPES = {  # name: (M, N, K, trans_a, trans_b)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="3,x1,h0,h1,h2,h3,h4")
+    ap.add_argument("--cfgs", default="3,h0,h1,h2,h3,h4")
     ap.add_argument("--rounds", type=int, default=10)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
