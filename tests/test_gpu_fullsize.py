@@ -6,7 +6,9 @@ batch (16 meshes with super nodes of in-degree 5,041: N = 80,672, E = 792,992), 
 encoder + bgnn_mlp2 head, fused layers, BatchNorm in train mode, dropout 0 (torch's dropout RNG
 cannot be matched). Checked: the 16 predictions and the RelativeErrorLoss within the north
 star's 1e-4, every used parameter's gradient within the golden fixtures' checksum tolerance,
-BatchNorm running statistics, and the set of parameters with gradients."""
+the whole gradient tensors within 1e-3 relative L2 per parameter (with a noise floor for the
+gradients that are exactly 0 in exact arithmetic), BatchNorm running statistics, and the set of
+parameters with gradients."""
 import numpy as np
 import pytest
 import torch
@@ -58,5 +60,18 @@ def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg):
     assert set(got) == set(ref)
     for k in ref:
         np.testing.assert_allclose(grad_checksum(got[k]), grad_checksum(ref[k]), rtol=2e-3, atol=2e-4, err_msg=k)
+    # whole gradient tensors, elementwise in aggregate: per parameter the L2 distance to fp64 within
+    # 1e-3 of the parameter's own gradient norm, plus a floor of 1e-5 of the largest per-element RMS
+    # gradient of the model (biases feeding a BatchNorm have an exact gradient of 0; their float
+    # gradients are rounding noise that a purely relative bound cannot judge)
+    rms = max(np.sqrt(np.mean(r ** 2)) for r in ref.values())
+    worst = []
+    for k in ref:
+        err = float(np.linalg.norm(got[k] - ref[k]))
+        nrm = float(np.linalg.norm(ref[k]))
+        bound = 1e-3 * nrm + 1e-5 * rms * np.sqrt(ref[k].size)
+        worst.append((err / max(bound, 1e-300), k, err, nrm))
+        assert err <= bound, (k, err, nrm, bound)
+    print("largest gradient error / bound:", max(worst)[:2])
     for k, v in state.items():   # running statistics after one train-mode step (momentum 0.1)
         np.testing.assert_allclose(v.numpy(), st[k].detach().numpy(), rtol=1e-5, atol=1e-6, err_msg=k)
