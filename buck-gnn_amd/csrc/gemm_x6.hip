@@ -650,7 +650,9 @@ extern "C" int bgnn_absmax_items_f32(const float* x, int32_t n_items, int64_t it
     while (tpr < 256 && tpr < cols4) tpr <<= 1;
     const int64_t rpi = 256 / tpr;
     int64_t blocks = (rows + rpi - 1) / rpi;
-    if (blocks > 512) blocks = 512;
+    // <= 64 blocks per item: the per-layer weights are 2 MB, and 512 blocks of 2 rows each ran the
+    // 6-layer pass in 32 us (launch-, not bandwidth-bound, 3,072 atomics on 6 words)
+    if (blocks > 64) blocks = 64;
     hipLaunchKernelGGL(k_absmax_items, dim3((unsigned)blocks, (unsigned)n_items), dim3(256), 0, as_stream(stream), x,
                        item_stride, rows, cols4, ld, tpr, reinterpret_cast<uint32_t*>(out), out_stride);
     BGNN_CHECK_LAUNCH();
