@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--shapes", default="fwd,dgrad,dropadd,wgrad")
     ap.add_argument("--rows", type=int, default=80656, help="M (node rows; cfg2 = 80656)")
+    ap.add_argument("--knob", type=int, default=-1, help="a bgnn_set_tuning knob crossed with --cfgs")
+    ap.add_argument("--values", default="", help="comma list of values for --knob")
     args = ap.parse_args()
     M = args.rows
     dev = torch.device("cuda", 0)
@@ -52,7 +54,9 @@ def main():
         "wgrad": (torch.empty(2 * H, H, device=dev),
                   lambda o: fused.gemm(dz, x, True, False, out=o, a_amax=am[2:3], b_amax=am[0:1]), 2.0 * M * 2 * H * H),
     }
-    cfgs = [int(c) for c in args.cfgs.split(",")]
+    vals = [int(v) for v in args.values.split(",")] if args.knob >= 0 and args.values else [None]
+    cfgs = [(int(c), v) for c in args.cfgs.split(",") for v in vals]
+    knob0 = _lib.query("bgnn_get_tuning", args.knob) if args.knob >= 0 else None
     names = args.shapes.split(",")
     times = {(n, c): [] for n in names for c in cfgs}
     outs = {}
@@ -60,7 +64,9 @@ def main():
         for n in names:
             out, fn, _ = shapes[n]
             for c in cfgs:
-                _lib.call("bgnn_gemm_set_cfg", c)
+                _lib.call("bgnn_gemm_set_cfg", c[0])
+                if c[1] is not None:
+                    _lib.call("bgnn_set_tuning", args.knob, c[1])
                 flush.fill_(float(rnd))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -72,6 +78,8 @@ def main():
                 if rnd == 1:
                     outs[(n, c)] = out.clone()
     _lib.call("bgnn_gemm_set_cfg", -1)
+    if args.knob >= 0:
+        _lib.call("bgnn_set_tuning", args.knob, knob0)
     for n in names:
         flop = shapes[n][2]
         for c in cfgs:
@@ -79,7 +87,7 @@ def main():
             med = ts[len(ts) // 2]
             same = "ref" if c == cfgs[0] else ("bit-identical" if torch.equal(outs[(n, c)], outs[(n, cfgs[0])])
                                                else f"differs {(outs[(n, c)] - outs[(n, cfgs[0])]).abs().max().item():.2e}")
-            print(f"{n:8s} cfg {c:3d}: median {med:7.1f} us  min {ts[0]:7.1f}  {flop / med / 1e6:6.1f} TF  "
+            print(f"{n:8s} cfg {c[0]:3d} {'' if c[1] is None else f'k{args.knob}={c[1]:<3d}'}: median {med:7.1f} us  min {ts[0]:7.1f}  {flop / med / 1e6:6.1f} TF  "
                   f"({flop / med / 1e6 / 833.3:.3f} of 833 TF)  {same}", flush=True)
 
 
