@@ -405,7 +405,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor = None, rel
 
 # the node encoder's leading Linear(16,64).ReLU.Linear(64,128).ReLU as one VALU kernel
 # (bgnn_mlp2_fwd / _bwd) instead of two GEMM launches with their operand-max passes:
-# fwd 57 us, bwd 108 us + 11 us slot sums on cfg2; the step 9.94 -> 9.82 ms (tools/ab_step.py)
+# fwd 57 us, bwd 108 us + 11 us slot sums on cfg2; the step 9.94 -> 9.82 ms (tools/ab_step.py);
+# round 4: conflict-free W2^T load, backward at 512 threads: fwd 54 us, bwd 94 us (bit-identical)
 FUSED_MLP2 = True
 
 

@@ -28,21 +28,35 @@ struct MlpSmem {
     float h1[kT][D1 + 4];
 };
 
-template <int F, int D1, int D2>
+template <int F, int D1, int D2, int NT>
 __device__ __forceinline__ void load_weights(MlpSmem<F, D1, D2>& S, const float* W1, const float* b1,
                                              const float* W2, const float* b2, bool w2_transposed) {
-    for (int i = threadIdx.x; i < D1 * F; i += 256) {
+    for (int i = threadIdx.x; i < D1 * F; i += NT) {
         const int j = i / F, f = i % F;
         S.w1t[f][j] = W1[i];
     }
-    for (int i = threadIdx.x; i < D1; i += 256) S.b1[i] = b1 ? b1[i] : 0.f;
+    for (int i = threadIdx.x; i < D1; i += NT) S.b1[i] = b1 ? b1[i] : 0.f;
     float* w2 = &S.w2t[0][0];
-    for (int i = threadIdx.x; i < D2 * D1; i += 256) {
-        const int j = i / D1, k = i % D1;
-        if (w2_transposed) w2[k * D2 + j] = W2[i];   // [D1][D2]
-        else w2[i] = W2[i];                          // [D2][D1]
+    if (w2_transposed && (((uintptr_t)W2 & 15) == 0)) {
+        // W2^T [D1][D2]: lanes run over the output j, so the LDS words a wave writes are
+        // consecutive (the element-order walk wrote one bank 64 times per instruction); each
+        // lane reads one float4 of W2's row j
+        for (int i = threadIdx.x; i < D2 * (D1 / 4); i += NT) {
+            const int j = i % D2, k = (i / D2) * 4;
+            const float4 v = *reinterpret_cast<const float4*>(W2 + j * D1 + k);
+            w2[(k + 0) * D2 + j] = v.x;
+            w2[(k + 1) * D2 + j] = v.y;
+            w2[(k + 2) * D2 + j] = v.z;
+            w2[(k + 3) * D2 + j] = v.w;
+        }
+    } else {
+        for (int i = threadIdx.x; i < D2 * D1; i += NT) {
+            const int j = i / D1, k = i % D1;
+            if (w2_transposed) w2[k * D2 + j] = W2[i];   // [D1][D2]
+            else w2[i] = W2[i];                          // [D2][D1]
+        }
     }
-    for (int i = threadIdx.x; i < D2; i += 256) S.b2[i] = b2 ? b2[i] : 0.f;
+    for (int i = threadIdx.x; i < D2; i += NT) S.b2[i] = b2 ? b2[i] : 0.f;
 }
 
 __device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
@@ -50,14 +64,16 @@ __device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
 }
 
-// h1 = ReLU(x W1^T + b1) for the tile's 64 nodes (xs loaded): thread = 4 nodes x 4 hidden units
-template <int F, int D1, int D2>
+// h1 = ReLU(x W1^T + b1) for the tile's 64 nodes (xs loaded): thread = 64 / (NT / 16) nodes x 4
+// hidden units (every unit's sum runs over f in order, whatever NT)
+template <int F, int D1, int D2, int NT>
 __device__ __forceinline__ void hidden(MlpSmem<F, D1, D2>& S) {
-    static_assert(D1 == 64 && kT == 64, "hidden: 16 x 16 threads of 4 nodes x 4 units");
+    static_assert(D1 == 64 && kT == 64 && (NT == 256 || NT == 512), "hidden: 16 unit groups of 4");
+    constexpr int NP = kT * 16 / NT;   // nodes per thread
     const int tn = threadIdx.x >> 4, tk = threadIdx.x & 15;
-    float acc[4][4];
+    float acc[NP][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NP; ++i)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[i][c] = S.b1[tk * 4 + c];
 #pragma unroll
@@ -65,43 +81,45 @@ __device__ __forceinline__ void hidden(MlpSmem<F, D1, D2>& S) {
         float w[4];
         ld4(&S.w1t[f][tk * 4], w);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float xv = S.xs[tn * 4 + i][f];
+        for (int i = 0; i < NP; ++i) {
+            const float xv = S.xs[tn * NP + i][f];
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc[i][c] = fmaf(xv, w[c], acc[i][c]);
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<float4*>(&S.h1[tn * 4 + i][tk * 4]) =
+    for (int i = 0; i < NP; ++i)
+        *reinterpret_cast<float4*>(&S.h1[tn * NP + i][tk * 4]) =
             make_float4(fmaxf(acc[i][0], 0.f), fmaxf(acc[i][1], 0.f), fmaxf(acc[i][2], 0.f), fmaxf(acc[i][3], 0.f));
 }
 
-template <int F>
+template <int F, int NT>
 __device__ __forceinline__ void load_x(float (*xs)[F + 4], const float* x, int64_t n0, int64_t N) {
-    for (int i = threadIdx.x; i < kT * F; i += 256) {
+    for (int i = threadIdx.x; i < kT * F; i += NT) {
         const int n = i / F, f = i % F;
         xs[n][f] = (n0 + n < N) ? x[(n0 + n) * F + f] : 0.f;
     }
 }
 
-// forward: thread = 4 nodes x 8 outputs of layer 2 (W2^T row segments as float4 pairs)
+// forward: thread = 4 nodes x 8 outputs of layer 2 (W2^T row segments as float4 pairs). 256
+// threads, two workgroups per CU: at 512 threads of 4 x 4 outputs the loop reads twice the LDS
+// bytes per FMA and ran 72 us against 54 (tools/mlp2_ab.py)
 template <int F, int D1, int D2>
 __global__ __launch_bounds__(256) void k_mlp2_fwd(const float* __restrict__ x, int64_t N, const float* W1,
                                                   const float* b1, const float* W2, const float* b2,
                                                   float* __restrict__ h, uint32_t* __restrict__ amax) {
     static_assert(D2 == 128, "k_mlp2_fwd: 16 column groups of 8");
     __shared__ MlpSmem<F, D1, D2> S;
-    load_weights(S, W1, b1, W2, b2, true);
+    load_weights<F, D1, D2, 256>(S, W1, b1, W2, b2, true);
     const int tn = threadIdx.x >> 4, tj = threadIdx.x & 15;
     uint32_t m = 0;
     const int64_t tiles = (N + kT - 1) / kT;
     for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
         const int64_t n0 = t * kT;
         __syncthreads();
-        load_x<F>(S.xs, x, n0, N);
+        load_x<F, 256>(S.xs, x, n0, N);
         __syncthreads();
-        hidden(S);
+        hidden<F, D1, D2, 256>(S);
         __syncthreads();
         float acc[4][8];
 #pragma unroll
@@ -144,38 +162,43 @@ __global__ __launch_bounds__(256) void k_mlp2_fwd(const float* __restrict__ x, i
 }
 
 // Backward. g2 = dh (.) [h > 0];  dW2 += g2^T h1, db2 += sum g2;  g1 = (g2 W2) (.) [h1 > 0];
-// dW1 += g1^T x, db1 += sum g1. Per workgroup partials: [D2*D1 | D2 | D1*F | D1].
+// dW1 += g1^T x, db1 += sum g1. Per workgroup partials: [D2*D1 | D2 | D1*F | D1]. 512 threads (two
+// waves per SIMD: at 256 the one wave per SIMD left every LDS read's latency exposed); every
+// accumulator still sums its nodes in order, so the partials do not depend on the thread count.
+constexpr int kBwdThreads = 512;
+
 template <int F, int D1, int D2>
-__global__ __launch_bounds__(256) void k_mlp2_bwd(const float* __restrict__ x, int64_t N, const float* W1,
-                                                  const float* b1, const float* W2, const float* __restrict__ h,
-                                                  const float* __restrict__ dh, float* __restrict__ part) {
+__global__ __launch_bounds__(kBwdThreads) void k_mlp2_bwd(const float* __restrict__ x, int64_t N, const float* W1,
+                                                          const float* b1, const float* W2, const float* __restrict__ h,
+                                                          const float* __restrict__ dh, float* __restrict__ part) {
     static_assert(D2 == 128 && D1 == 64 && F == 16, "k_mlp2_bwd: built for 16 x 64 x 128");
+    constexpr int NT = kBwdThreads;
     constexpr int G2 = D2 + 4, G1 = D1 + 4;
     extern __shared__ float dyn[];   // g2 [kT][G2], g1 [kT][G1]
     __shared__ MlpSmem<F, D1, D2> S;
     float (*g2)[G2] = reinterpret_cast<float (*)[G2]>(dyn);
     float (*g1)[G1] = reinterpret_cast<float (*)[G1]>(dyn + kT * G2);
-    load_weights(S, W1, b1, W2, nullptr, false);   // W2 kept as [D2][D1] in S.w2t's space
+    load_weights<F, D1, D2, NT>(S, W1, b1, W2, nullptr, false);   // W2 kept as [D2][D1] in S.w2t's space
     const float* w2 = &S.w2t[0][0];
     const int hi = threadIdx.x >> 4, lo = threadIdx.x & 15;
-    // dW2: rows hi*8..+8, columns lo*4..+4 (32 accumulators); db2 by the lo == 0 threads
-    float dw2[8][4], db2[8];
+    // dW2: rows hi*4..+4, columns lo*4..+4 (16 accumulators); db2 by the lo == 0 threads
+    float dw2[4][4], db2[4];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < 4; ++c) {
         db2[c] = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) dw2[c][q] = 0.f;
     }
-    // dW1: row k1 = tid / 4, columns fb1..fb1+4; db1 by the fb1 == 0 threads
-    const int k1 = threadIdx.x >> 2, fb1 = (threadIdx.x & 3) * 4;
-    float dw1[4] = {0.f, 0.f, 0.f, 0.f};
+    // dW1: row k1 = tid / 8, columns fb1..fb1+2; db1 by the fb1 == 0 threads
+    const int k1 = threadIdx.x >> 3, fb1 = (threadIdx.x & 7) * 2;
+    float dw1[2] = {0.f, 0.f};
     float db1 = 0.f;
     const int64_t tiles = (N + kT - 1) / kT;
     for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
         const int64_t n0 = t * kT;
         __syncthreads();
-        load_x<F>(S.xs, x, n0, N);
-        for (int i = threadIdx.x; i < kT * (D2 / 4); i += 256) {
+        load_x<F, NT>(S.xs, x, n0, N);
+        for (int i = threadIdx.x; i < kT * (D2 / 4); i += NT) {
             const int n = i / (D2 / 4), j4 = (i % (D2 / 4)) * 4;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (n0 + n < N) {
@@ -188,52 +211,44 @@ __global__ __launch_bounds__(256) void k_mlp2_bwd(const float* __restrict__ x, i
             *reinterpret_cast<float4*>(&g2[n][j4]) = v;
         }
         __syncthreads();
-        hidden(S);
+        hidden<F, D1, D2, NT>(S);
         __syncthreads();
         // layer-2 weight / bias gradients (rows of padded tail nodes are zero in g2)
         for (int n = 0; n < kT; ++n) {
-            float ga[4], gb[4], hv[4];
-            ld4(&g2[n][hi * 8], ga);
-            ld4(&g2[n][hi * 8 + 4], gb);
+            float ga[4], hv[4];
+            ld4(&g2[n][hi * 4], ga);
             ld4(&S.h1[n][lo * 4], hv);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    dw2[c][q] = fmaf(ga[c], hv[q], dw2[c][q]);
-                    dw2[c + 4][q] = fmaf(gb[c], hv[q], dw2[c + 4][q]);
-                }
-            }
+                for (int c = 0; c < 4; ++c) dw2[c][q] = fmaf(ga[c], hv[q], dw2[c][q]);
             if (lo == 0) {
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    db2[c] += ga[c];
-                    db2[c + 4] += gb[c];
-                }
+                for (int c = 0; c < 4; ++c) db2[c] += ga[c];
             }
         }
-        // g1 = (g2 W2) masked by h1 > 0: thread = 4 nodes (hi) x 4 hidden units (lo)
+        // g1 = (g2 W2) masked by h1 > 0: thread = 2 nodes (hi) x 4 hidden units (lo)
         {
-            float acc[4][4];
+            float acc[2][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 2; ++i)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) acc[i][q] = 0.f;
             for (int j = 0; j < D2; ++j) {
                 float w[4];
                 ld4(&w2[j * D1 + lo * 4], w);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float gv = g2[hi * 4 + i][j];
+                for (int i = 0; i < 2; ++i) {
+                    const float gv = g2[hi * 2 + i][j];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(gv, w[q], acc[i][q]);
                 }
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < 2; ++i) {
                 float hv[4];
-                ld4(&S.h1[hi * 4 + i][lo * 4], hv);
-                *reinterpret_cast<float4*>(&g1[hi * 4 + i][lo * 4]) =
+                ld4(&S.h1[hi * 2 + i][lo * 4], hv);
+                *reinterpret_cast<float4*>(&g1[hi * 2 + i][lo * 4]) =
                     make_float4(hv[0] > 0.f ? acc[i][0] : 0.f, hv[1] > 0.f ? acc[i][1] : 0.f,
                                 hv[2] > 0.f ? acc[i][2] : 0.f, hv[3] > 0.f ? acc[i][3] : 0.f);
             }
@@ -241,20 +256,19 @@ __global__ __launch_bounds__(256) void k_mlp2_bwd(const float* __restrict__ x, i
         __syncthreads();
         for (int n = 0; n < kT; ++n) {
             const float gv = g1[n][k1];
-            float xv[4];
-            ld4(&S.xs[n][fb1], xv);
+            const float2 xv = *reinterpret_cast<const float2*>(&S.xs[n][fb1]);
             db1 += (fb1 == 0) ? gv : 0.f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) dw1[q] = fmaf(gv, xv[q], dw1[q]);
+            dw1[0] = fmaf(gv, xv.x, dw1[0]);
+            dw1[1] = fmaf(gv, xv.y, dw1[1]);
         }
     }
     float* p = part + (int64_t)blockIdx.x * (D2 * D1 + D2 + D1 * F + D1);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        *reinterpret_cast<float4*>(p + (hi * 8 + c) * D1 + lo * 4) = make_float4(dw2[c][0], dw2[c][1], dw2[c][2], dw2[c][3]);
-        if (lo == 0) p[D2 * D1 + hi * 8 + c] = db2[c];
+    for (int c = 0; c < 4; ++c) {
+        *reinterpret_cast<float4*>(p + (hi * 4 + c) * D1 + lo * 4) = make_float4(dw2[c][0], dw2[c][1], dw2[c][2], dw2[c][3]);
+        if (lo == 0) p[D2 * D1 + hi * 4 + c] = db2[c];
     }
-    *reinterpret_cast<float4*>(p + D2 * D1 + D2 + k1 * F + fb1) = make_float4(dw1[0], dw1[1], dw1[2], dw1[3]);
+    *reinterpret_cast<float2*>(p + D2 * D1 + D2 + k1 * F + fb1) = make_float2(dw1[0], dw1[1]);
     if (fb1 == 0) p[D2 * D1 + D2 + D1 * F + k1] = db1;
 }
 
@@ -433,7 +447,7 @@ extern "C" int bgnn_mlp2_bwd(const float* x, int64_t N, int32_t F, int32_t D1, i
     const int blocks = mlp_blocks(N);
     float* part = static_cast<float*>(ws);
     const size_t dyn = sizeof(float) * kT * ((kD2 + 4) + (kD1 + 4));
-    hipLaunchKernelGGL((k_mlp2_bwd<kF, kD1, kD2>), dim3(blocks), dim3(256), dyn, s, x, N, W1, b1, W2, h, dh, part);
+    hipLaunchKernelGGL((k_mlp2_bwd<kF, kD1, kD2>), dim3(blocks), dim3(kBwdThreads), dyn, s, x, N, W1, b1, W2, h, dh, part);
     BGNN_CHECK_LAUNCH();
     // slot sums straight into the four gradient tensors (partial layout [dW2 | db2 | dW1 | db1])
     float* tmp = part + (int64_t)blocks * kPartLen;
