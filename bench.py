@@ -84,6 +84,8 @@ def parse():
                          "BASELINE metric)")
     ap.add_argument("--infer-batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cfg3", action="store_true",
+                    help="skip the cfg3 (super-node) block the default cfg2 line nests after its own measurement")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--cache-graph", action="store_true", help="reuse the CSR across steps (not the default)")
     ap.add_argument("--data", default="store", choices=["static", "store", "host"],
@@ -211,18 +213,9 @@ def run_infer(args, model, dev, world, rank):
         torch.distributed.destroy_process_group()
 
 
-def main():
-    args = parse()
-    import numpy as np
+def setup_dist(args):
     import torch
     import torch.distributed as dist
-
-    import bgnn
-    from bgnn import _lib, fused, synthetic
-
-    for kv in args.tune:
-        k, v = kv.split("=")
-        _lib.call("bgnn_set_tuning", int(k), int(v))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -237,24 +230,43 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    fused.GEMM_BACKEND = args.gemm
+    return world, rank, torch.device("cuda", local)
 
-    # data: each rank owns its own bsz graphs (seeds 1000*rank + g); resident in HBM
-    bsz = synthetic.CONFIGS[args.config]["graphs"]
-    batch_cpu = synthetic.make_config_batch(args.config, rank=rank)
-    batch = batch_cpu.to(dev)
+
+def build_model(args, model_name, dev):
+    import torch
+    import bgnn
+    from bgnn import synthetic
     torch.manual_seed(0)
     model = bgnn.BuckGNN(synthetic.NUM_NODE_FEATURES, synthetic.NUM_EDGE_FEATURES, hidden_channels=512,
                          num_layers=6, pooling_layer="mean", prediction_type="buckling", dropout_rate=0.1,
-                         model_name=args.model)
+                         model_name=model_name)
     state0 = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).train()
     model.use_fused = args.path == "fused"
     if args.path == "per_op" and args.bn == "bgnn":
         bgnn.nn.use_bgnn_batchnorm(model)
     model.ea_bf16 = bool(args.bf16)
-    is_ea = args.model.startswith("EA_GNN")
+    return model, state0
+
+
+def measure_train(args, config, model_name, dev, world, rank, steps, warmup, heavy_timing=False):
+    """Build the data (a resident GraphStore of meshes per rank), model and optimizer, run `warmup`
+    untimed and `steps` timed train steps (barrier + synchronize on both sides, max over ranks).
+    Returns a dict: elapsed (s), timers (bgnn.fused per-launch HIP events), batch (first batch),
+    batch_cpu, loss, lr, state0, bsz, steps, heavy (chunk + combine timing of the super rows)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import bgnn
+    from bgnn import _lib, fused, synthetic
+
+    bsz = synthetic.CONFIGS[config]["graphs"]
+    batch_cpu = synthetic.make_config_batch(config, rank=rank)
+    batch = batch_cpu.to(dev)
+    model, state0 = build_model(args, model_name, dev)
+    is_ea = model_name.startswith("EA_GNN")
     lr = args.lr if args.lr is not None else (1e-3 if is_ea else 1e-2)
     try:
         opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-8, fused=True)
@@ -262,10 +274,9 @@ def main():
         opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=1e-8)
     crit = bgnn.RelativeErrorLoss()
     norm = bgnn.EigenvalueScaler(center=1.0, scale=0.5)
-    if args.mode == "infer":
-        return run_infer(args, model, dev, world, rank)
     ar = bgnn.GradAllReduce(model) if world > 1 else None
 
+    store = None
     if args.data == "static":
         def step():
             if not args.cache_graph:
@@ -273,7 +284,7 @@ def main():
             return bgnn.train_step(model, batch, opt, crit, norm, allreduce=ar)
     else:
         # a pool of meshes per rank, a different shuffled 16-graph batch every step
-        c = synthetic.CONFIGS[args.config]
+        c = synthetic.CONFIGS[config]
         if args.epochs > 0:
             # this rank's shard of a global dataset (graph g seeded by its global id)
             n_global = args.dataset_graphs or args.store_graphs * world
@@ -282,23 +293,21 @@ def main():
                 raise SystemExit(f"--epochs: the shard of rank {rank} has {len(gids)} graphs, fewer than a batch")
             pool = [synthetic.make_mesh_graph(c["n"], g, super_node=c["super_node"]) for g in gids]
             per_epoch = len(gids) // bsz
-            args.steps = args.epochs * per_epoch
+            steps = args.epochs * per_epoch
         else:
             pool = [synthetic.make_mesh_graph(c["n"], 1000 * rank + g, super_node=c["super_node"])
                     for g in range(args.store_graphs)]
         store = bgnn.GraphStore(pool, dev) if args.data == "store" else None
         rng = np.random.default_rng(rank)
-        order = iter(())
-        epoch = -1
+        state = {"order": iter(()), "epoch": -1}
 
         def next_ids():
-            nonlocal order, epoch
-            ids = list(itertools.islice(order, bsz))
+            ids = list(itertools.islice(state["order"], bsz))
             if len(ids) < bsz:   # (drop_last: a partial batch starts the next epoch)
-                epoch += 1
-                order = iter(rng.permutation(len(pool)) if args.epochs <= 0
-                             else np.random.default_rng(1234 + epoch).permutation(len(pool)))
-                ids = list(itertools.islice(order, bsz))
+                state["epoch"] += 1
+                state["order"] = iter(rng.permutation(len(pool)) if args.epochs <= 0
+                                      else np.random.default_rng(1234 + state["epoch"]).permutation(len(pool)))
+                ids = list(itertools.islice(state["order"], bsz))
             return ids
 
         def step():
@@ -309,38 +318,60 @@ def main():
                 b = bgnn.Batch.from_data_list([pool[i] for i in ids]).to(dev, non_blocking=True)
             return bgnn.train_step(model, b, opt, crit, norm, allreduce=ar)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    if args.epochs > 0:   # timed epochs start at an epoch boundary
-        order = iter(())
-        epoch = -1
+    if args.epochs > 0 and args.data != "static":   # timed epochs start at an epoch boundary
+        state["order"] = iter(())
+        state["epoch"] = -1
     torch.cuda.synchronize()
     fused.TIMERS = {}
+    if heavy_timing:
+        _lib.call("bgnn_heavy_timing", 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timers, fused.TIMERS = fused.TIMERS, None
+    heavy = None
+    if heavy_timing:
+        import ctypes
+        _lib.call("bgnn_heavy_timing", 0)
+        heavy = {}
+        for which, name in ((0, "fwd"), (1, "bwd")):
+            ms, n = ctypes.c_float(0.0), ctypes.c_int32(0)
+            _lib.call("bgnn_heavy_timing_read", which, ctypes.addressof(ms), ctypes.addressof(n))
+            heavy[name] = (float(ms.value), int(n.value))
     if args.path == "per_op":   # the per-module SAGEConv launches (bgnn.fused.SageConvFn) under the same keys
         timers = {k[5:]: v for k, v in timers.items() if k.startswith("conv_")}
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    loss_v = float(loss.item())
+    res = {"elapsed": elapsed, "timers": timers, "batch": batch, "batch_cpu": batch_cpu, "loss": float(loss.item()),
+           "lr": lr, "state0": state0, "bsz": bsz, "steps": steps, "heavy": heavy}
+    del model, opt, store
+    return res
+
+
+def roofline_blocks(args, m, model_name):
+    """The roofline objects of one measured run (bench line keys roofline, roofline_gemm,
+    roofline_hbm, roofline_agg_bwd) from its per-launch HIP events."""
+    from bgnn import _lib
+    timers, steps = m["timers"], m["steps"]
+    batch = m["batch"]
 
     def avg_ms(name):
         ev = timers.get(name, [])
         return sum(a.elapsed_time(b) for a, b in ev) / len(ev) if ev else float("nan")
 
     N, E, H = batch.num_nodes, batch.num_edges, 512
-    is_max = "maxAggr" in args.model
+    is_max = "maxAggr" in model_name
     if is_max and "gemm_fwd_max" in timers:   # (the aggregate-first transform: same flops, K = 2H)
         timers.setdefault("gemm_fwd", timers["gemm_fwd_max"])
     # max aggregation (aggregate-first, bgnn/fused.py::_max_transform): bgnn_spmm_fwd(MAX) reads each
@@ -359,11 +390,12 @@ def main():
         seg_kernel == 0 and _graph.GROUP_ROWS == 4) else "k_seg_sweep<2,0,{e},12>"
     traffic = {}
     tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
+    is_ea = model_name.startswith("EA_GNN")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            cfgk = "ea5" if (is_ea and args.bf16 and args.config == "cfg5") else args.config
-            kern = tj.get("configs", {}).get(cfgk, tj["kernels"])
+            cfgk = "ea5" if (is_ea and args.bf16 and m["config"] == "cfg5") else m["config"]
+            kern = tj.get("configs", {}).get(cfgk, tj["kernels"] if m["config"] == "cfg2" else {})
             traffic = {k: v["bytes_per_launch"] for k, v in kern.items()}
         except (ValueError, OSError, KeyError):
             traffic = {}
@@ -376,21 +408,9 @@ def main():
     # wgrad d[W_l;W_r] = [dz_l|dh]^T x (each 2*N*2H*H flops); the folded first layer runs the
     # same three products with the encoder width K_in = 128 in place of one H.
     K_in = 128
-    fams = {
-        "gemm_fwd": (2.0 * N * (2 * H) * H, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", "gemm_fwd_h3",
-                     "fwd z = x [W_l;W_r]^T, K = 512 layers (5 per step)"),
-        "gemm_dgrad": (2.0 * N * H * (2 * H), "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8> (skip layers, drop-add "
-                       "epilogue) + k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0> (last layer)", "gemm_dgrad",
-                       "dgrad dx = [dz_l|dh] [W_l;W_r], K = 512 layers (5 per step)"),
-        "gemm_wgrad": (2.0 * (2 * H) * H * N, "k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0> + split-K slab reduce",
-                       "gemm_wgrad", "wgrad [dz_l|dh]^T x, K = 512 layers (5 per step)"),
-        "gemm_fwd_fold": (2.0 * N * (2 * H) * K_in, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", None,
-                          "folded layer 0 fwd z = h Wf^T, K = 128"),
-        "gemm_dgrad_fold": (2.0 * N * K_in * (2 * H), "k_gemm_x6<1, 0, 1, 256, 128, 4, 2, 0>", None,
-                            "folded layer 0 dgrad dh = dz Wf"),
-        "gemm_wgrad_fold": (2.0 * (2 * H) * K_in * N, "k_gemm_x6<1, 1, 0, 256, 128, 4, 2, 0>", None,
-                            "folded layer 0 wgrad dWf = dz^T h"),
-    }
+    fams = dict(GEMM_FAMILIES)
+    for k, (flop_fn, kname, tkey, what) in GEMM_FAMILIES.items():
+        fams[k] = (flop_fn(N, H, K_in), kname, tkey, what)
 
     def gemm_block(key):
         flop, kname, tkey, what = fams[key]
@@ -402,7 +422,7 @@ def main():
                 "frac": round(tfs / gemm_peak, 4), "traffic": traffic.get(tkey) if tkey else None,
                 "peak_basis": gemm_basis, "f32_mfma_peak": FP32_MFMA_PEAK_TFS, "algorithmic_flop": flop,
                 "avg_launch_ms": round(ms, 5), "launches": n,
-                "ms_per_step": round(ms * n / args.steps, 4) if n else float("nan")}
+                "ms_per_step": round(ms * n / steps, 4) if n else float("nan")}
 
     gemm_blocks = {k: gemm_block(k) for k in fams}
     # all SAGE-layer GEMM launches of the step together: summed flops / summed event time
@@ -412,53 +432,14 @@ def main():
     # `roofline` = the dominant kernel: the GEMM family with the largest time per step
     main_key = max(("gemm_fwd", "gemm_dgrad", "gemm_wgrad"),
                    key=lambda k: (gemm_blocks[k]["launches"] * avg_ms(k)) if gemm_blocks[k]["launches"] else -1)
-    graphs = bsz * world * args.steps
-    out = {
-        "metric": metric_name(args.model, bsz),
-        "value": round(graphs / elapsed, 3),
-        "unit": "graphs/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16" if (args.bf16 and args.model.startswith("EA_GNN")) else "f32",
-        "data": "synthetic",
-        "config": {
-            "workload": f"{args.config}: {bsz} synthetic 71x71 quad+diagonal FE meshes per GPU"
-                        + (" + super node" if args.config == "cfg3" else " + 13.33% random virtual edges")
-                        + f", {args.model} h=512 L=6, mean pool, dropout 0.1, Adam"
-                        + ("; per-op modules (PyG-surface SAGEConv on the bgnn GEMM + fused aggregation/normalize, "
-                           + ("bgnn BatchNorm1d, " if args.bn == "bgnn" else "torch BatchNorm, ")
-                           + "torch ReLU/Dropout/encoder)" if args.path == "per_op" else "")
-                        + (", bf16 GEMM operands" if args.bf16 and args.model.startswith("EA_GNN") else "") + "; "
-                        + {"static": "CSR rebuilt every step" if not args.cache_graph else "CSR cached across steps",
-                           "store": f"new shuffled batch every step gathered on the GPU from a resident "
-                                    f"GraphStore of {args.store_graphs} meshes",
-                           "host": f"new shuffled batch every step collated on the host from {args.store_graphs} "
-                                   f"meshes and copied to the GPU (reference DataLoader path)"}[args.data],
-            "data_path": args.data,
-            **({"epochs": args.epochs, "dataset_graphs": args.dataset_graphs or args.store_graphs * world,
-                "steps_per_epoch": args.steps // args.epochs} if args.epochs > 0 else {}),
-            "global_batch": bsz * world,
-            "nodes_per_gpu": N,
-            "edges_per_gpu": E,
-            "hidden": H,
-            "layers": 6,
-            "parallelism": f"dp{world}",
-            "gemm": args.gemm,
-            "path": args.path,
-            **({"batchnorm": args.bn} if args.path == "per_op" else {}),
-        },
+    return {
         "roofline": dict(gemm_blocks[main_key], family=main_key),
         "roofline_gemm": {
             **{k: {kk: gemm_blocks[k][kk] for kk in ("achieved", "frac", "avg_launch_ms", "launches", "ms_per_step",
                                                      "algorithmic_flop", "kernel")} for k in fams},
             "all_sage_gemms": {"achieved": round(gemm_all_tfs, 2), "frac": round(gemm_all_tfs / gemm_peak, 4),
-                               "ms_per_step": round(tot_ms / args.steps, 4),
-                               "tflop_per_step": round(tot_flop / args.steps / 1e12, 4)},
+                               "ms_per_step": round(tot_ms / steps, 4),
+                               "tflop_per_step": round(tot_flop / steps / 1e12, 4)},
         },
         "roofline_hbm": {
             "kernel": ("bgnn_spmm_fwd(MAX) with the per-element argmax (aggregate-first max layer)" if is_max else
@@ -469,7 +450,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(agg_gbs / HBM_PEAK_GBS, 4),
-            "traffic": None if is_max else traffic.get("sage_fwd"),
+            "traffic": traffic.get("agg_max" if is_max else "sage_fwd"),
             "algorithmic_bytes": agg_bytes,
             "avg_launch_ms": round(agg_ms, 5),
             "launches": len(timers.get("agg_max" if is_max else "sage_fwd", [])),
@@ -482,13 +463,128 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
-            "traffic": None if is_max else traffic.get("spmm_bwd"),
+            "traffic": traffic.get("spmm_bwd_max" if is_max else "spmm_bwd"),
             "algorithmic_bytes": bwd_bytes,
             "avg_launch_ms": round(bwd_ms, 5),
             "launches": len(timers.get("spmm_bwd", [])),
         },
-        "lr": lr,
-        "final_loss": loss_v,
+    }
+
+
+# family -> (flops(N, H, K_in), kernel, traffic key, description)
+GEMM_FAMILIES = {
+    "gemm_fwd": (lambda N, H, K: 2.0 * N * (2 * H) * H, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", "gemm_fwd_h3",
+                 "fwd z = x [W_l;W_r]^T, K = 512 layers (5 per step)"),
+    "gemm_dgrad": (lambda N, H, K: 2.0 * N * H * (2 * H), "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8> (skip layers, "
+                   "drop-add epilogue) + k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0> (last layer)", "gemm_dgrad",
+                   "dgrad dx = [dz_l|dh] [W_l;W_r], K = 512 layers (5 per step)"),
+    "gemm_wgrad": (lambda N, H, K: 2.0 * (2 * H) * H * N, "k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0> + split-K slab "
+                   "reduce", "gemm_wgrad", "wgrad [dz_l|dh]^T x, K = 512 layers (5 per step)"),
+    "gemm_fwd_fold": (lambda N, H, K: 2.0 * N * (2 * H) * K, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", None,
+                      "folded layer 0 fwd z = h Wf^T, K = 128"),
+    "gemm_dgrad_fold": (lambda N, H, K: 2.0 * N * K * (2 * H), "k_gemm_x6<1, 0, 1, 256, 128, 4, 2, 0>", None,
+                        "folded layer 0 dgrad dh = dz Wf"),
+    "gemm_wgrad_fold": (lambda N, H, K: 2.0 * (2 * H) * K * N, "k_gemm_x6<1, 1, 0, 256, 128, 4, 2, 0>", None,
+                        "folded layer 0 wgrad dWf = dz^T h"),
+}
+
+
+def workload_text(args, config, model_name, bsz):
+    return (f"{config}: {bsz} synthetic 71x71 quad+diagonal FE meshes per GPU"
+            + (" + super node" if config == "cfg3" else " + 13.33% random virtual edges")
+            + f", {model_name} h=512 L=6, mean pool, dropout 0.1, Adam"
+            + ("; per-op modules (PyG-surface SAGEConv on the bgnn GEMM + fused aggregation/normalize, "
+               + ("bgnn BatchNorm1d, " if args.bn == "bgnn" else "torch BatchNorm, ")
+               + "torch ReLU/Dropout/encoder)" if args.path == "per_op" else "")
+            + (", bf16 GEMM operands" if args.bf16 and model_name.startswith("EA_GNN") else "") + "; "
+            + {"static": "CSR rebuilt every step" if not args.cache_graph else "CSR cached across steps",
+               "store": f"new shuffled batch every step gathered on the GPU from a resident "
+                        f"GraphStore of {args.store_graphs} meshes",
+               "host": f"new shuffled batch every step collated on the host from {args.store_graphs} "
+                       f"meshes and copied to the GPU (reference DataLoader path)"}[args.data])
+
+
+def cfg3_block(args, dev, world, rank):
+    """BASELINE configs[2] measured in the same process after the headline line:
+    16 stiffened meshes with a super node each (in-degree 5,041: VirtualEdgeCreate.py:81-113) per
+    GPU, the same model and step; the super rows' 64-edge chunks + combine timed by HIP events."""
+    steps = max(5, args.steps // 2)
+    m = measure_train(args, "cfg3", args.model, dev, world, rank, steps, min(args.warmup, 3), heavy_timing=True)
+    m["config"] = "cfg3"
+    blocks = roofline_blocks(args, m, args.model)
+    b = m["batch"]
+    from bgnn import graph as _graph
+    g = _graph.graph_for(b.edge_index, b.num_nodes)
+    heavy = m["heavy"] or {}
+    sup = {"heavy_rows_per_batch": int(g.fwd.plan.n_heavy), "chunks_per_batch": int(g.fwd.plan.n_chunks),
+           "chunk_edges": _graph.DEFAULT_CHUNK}
+    for name, key in (("fwd", "sage_fwd"), ("bwd", "spmm_bwd")):
+        ms, n = heavy.get(name, (0.0, 0))
+        agg = blocks["roofline_hbm" if name == "fwd" else "roofline_agg_bwd"]
+        sup[f"chunk_combine_ms_per_launch_{name}"] = round(ms / n, 5) if n else None
+        sup[f"chunk_combine_share_of_{key}"] = round(ms / n / agg["avg_launch_ms"], 4) if n else None
+        sup[f"chunk_combine_ms_per_step_{name}"] = round(ms / m["steps"], 4) if n else None
+    return {"value": round(m["bsz"] * world * m["steps"] / m["elapsed"], 3), "unit": "graphs/s",
+            "ms_per_step": round(m["elapsed"] / m["steps"] * 1e3, 4), "steps": m["steps"],
+            "workload": workload_text(args, "cfg3", args.model, m["bsz"]),
+            "nodes_per_gpu": b.num_nodes, "edges_per_gpu": b.num_edges, "super_rows": sup,
+            **blocks, "final_loss": m["loss"]}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from bgnn import _lib, fused
+
+    for kv in args.tune:
+        k, v = kv.split("=")
+        _lib.call("bgnn_set_tuning", int(k), int(v))
+    world, rank, dev = setup_dist(args)
+    fused.GEMM_BACKEND = args.gemm
+    if args.mode == "infer":
+        model, _ = build_model(args, args.model, dev)
+        return run_infer(args, model, dev, world, rank)
+
+    m = measure_train(args, args.config, args.model, dev, world, rank, args.steps, args.warmup)
+    m["config"] = args.config
+    steps, bsz, elapsed = m["steps"], m["bsz"], m["elapsed"]
+    batch = m["batch"]
+    is_ea = args.model.startswith("EA_GNN")
+    blocks = roofline_blocks(args, m, args.model)
+    graphs = bsz * world * steps
+    out = {
+        "metric": metric_name(args.model, bsz),
+        "value": round(graphs / elapsed, 3),
+        "unit": "graphs/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if (args.bf16 and is_ea) else "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": workload_text(args, args.config, args.model, bsz),
+            "data_path": args.data,
+            **({"epochs": args.epochs, "dataset_graphs": args.dataset_graphs or args.store_graphs * world,
+                "steps_per_epoch": steps // args.epochs} if args.epochs > 0 else {}),
+            "global_batch": bsz * world,
+            "nodes_per_gpu": batch.num_nodes,
+            "edges_per_gpu": batch.num_edges,
+            "hidden": 512,
+            "layers": 6,
+            "parallelism": f"dp{world}",
+            "gemm": args.gemm,
+            "path": args.path,
+            **({"batchnorm": args.bn} if args.path == "per_op" else {}),
+        },
+        **blocks,
+        "lr": m["lr"],
+        "final_loss": m["loss"],
     }
     if is_ea:
         # the SAGE kernels above never run for EA_GNN. Its dominant kernels are the four per-edge
@@ -498,14 +594,26 @@ def main():
         # storage (ea.BF16_STORAGE) -- so at these sizes they are HBM-bound.
         for k in ("roofline_hbm", "roofline_agg_bwd", "roofline_gemm"):
             out.pop(k)
-        ea_ms = avg_ms("ea_edge_fwd")
-        n_ea = len(timers.get("ea_edge_fwd", []))
+        timers = m["timers"]
+        ev = timers.get("ea_edge_fwd", [])
+        n_ea = len(ev)
+        ea_ms = sum(a.elapsed_time(b) for a, b in ev) / n_ea if n_ea else float("nan")
         from bgnn import ea as ea_mod
+        E, H = batch.num_edges, 512
         ea_bytes = (4.0 if (args.bf16 and ea_mod.BF16_STORAGE) else 8.0) * E * H
         ea_flop = 2.0 * E * H * H
         ea_gbs = ea_bytes / (ea_ms * 1e-3) / 1e9
         ea_tfs = ea_flop / (ea_ms * 1e-3) / 1e12
+        gmode = _lib.query("bgnn_get_tuning", 5) if args.gemm == "hip" else -1
         ea_peak = BF16_MFMA_PEAK_TFS if args.bf16 else (H3_PEAK_TFS if gmode == 2 else FP32_MFMA_PEAK_TFS)
+        traffic = {}
+        tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
+        if os.path.exists(tpath):
+            try:
+                tj = json.load(open(tpath))
+                traffic = {k: v["bytes_per_launch"] for k, v in tj.get("configs", {}).get("ea5", {}).items()}
+            except (ValueError, OSError, KeyError):
+                traffic = {}
         out["roofline"] = {
             "kernel": "per-edge GraphNetBlock GEMMs (edge_mlp / phi, K = H = 512; gather-add + ReLU epilogues): "
                       + ("k_gemm_x6 bf16 operands" if args.bf16 else "k_gemm_x6 f16x3"),
@@ -514,12 +622,19 @@ def main():
             "traffic": traffic.get("ea_edge_b16") if (args.bf16 and ea_mod.BF16_STORAGE) else None,
             "algorithmic_bytes": ea_bytes,
             "avg_launch_ms": round(ea_ms, 5), "launches": n_ea,
-            "ms_per_step": round(ea_ms * n_ea / args.steps, 4) if n_ea else float("nan"),
+            "ms_per_step": round(ea_ms * n_ea / steps, 4) if n_ea else float("nan"),
             "mfma": {"achieved": round(ea_tfs, 2), "peak": ea_peak, "unit": "TFLOP/s",
                      "frac": round(ea_tfs / ea_peak, 4), "algorithmic_flop": ea_flop},
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(batch_cpu, state0, args.model, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(m["batch_cpu"], m["state0"], args.model, args.cpu_steps)
+    batch_cpu = m.pop("batch_cpu")
+    del m, batch, batch_cpu
+    # BASELINE configs[2] (super nodes) nested in the same line; the headline stays cfg2
+    if (args.config == "cfg2" and not args.no_cfg3 and not is_ea and args.path == "fused" and args.epochs <= 0
+            and args.data == "store"):
+        torch.cuda.empty_cache()
+        out["cfg3"] = cfg3_block(args, dev, world, rank)
     if rank == 0:
         def clean(o):   # NaN (a kernel the chosen model never launches) -> null: strict JSON
             if isinstance(o, dict):

@@ -58,6 +58,8 @@ SIGNATURES = {
                                         c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "bgnn_store_gather_rows": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_i64, c_p, c_p]),
     "bgnn_get_tuning": (c_i32, [c_i32]),
+    "bgnn_heavy_timing": (c_i32, [c_i32]),
+    "bgnn_heavy_timing_read": (c_i32, [c_i32, c_p, c_p]),
     "bgnn_set_tuning": (c_i32, [c_i32, c_i32]),
     "bgnn_graph_build_ws_bytes": (c_sz, [c_i64, c_i64]),
     "bgnn_graph_build": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p]),
@@ -80,6 +82,8 @@ SIGNATURES = {
     "bgnn_sage_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p,
                               c_p, c_p]),
     "bgnn_bn_finalize": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
+                                 c_p]),
+    "bgnn_bn_finalize_shifted": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
                                  c_p]),
     "bgnn_bn_eval_coeffs": (c_i32, [c_i32, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p]),
     "bgnn_sage_apply": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_f32, c_u64, c_i64, c_i32, c_p, c_p, c_p]),

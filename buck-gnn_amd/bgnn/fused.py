@@ -125,8 +125,8 @@ def _operand(x):
         return x.t.data_ptr(), blk, (blk if P > 1 else 0), R * blk
     if isinstance(x, Pair):
         diff = x.b.data_ptr() - x.a.data_ptr()
-        if diff % 4:
-            raise ValueError("Pair: the two halves must be 4-byte aligned relative to each other")
+        if diff % 16:   # (the GEMM's float4 loads test plane 0's alignment only)
+            raise ValueError("Pair: the two halves must be 16-byte aligned relative to each other")
         return x.a.data_ptr(), x.a.stride(0), x.a.size(1), diff // 4
     if x.stride(1) != 1:
         raise ValueError("gemm: operands must have unit column stride")
@@ -842,7 +842,8 @@ def _max_transform(x, w_l, w_r, graph: Graph, x_amax, w_amax, name: str):
     with _timed("agg_max"):
         agg, arg = spmm_fwd(graph.fwd, x, 2, N, want_arg=True)
     wk = torch.cat([w_l, w_r], 1)                                    # [H, 2C]
-    a = Pair(agg, x) if C % 32 == 0 else torch.cat([agg, x], 1)
+    in_place = C % 32 == 0 and (x.data_ptr() - agg.data_ptr()) % 16 == 0
+    a = Pair(agg, x) if in_place else torch.cat([agg, x], 1)
     with _timed(name):
         y = gemm(a, wk, trans_a=False, trans_b=True, a_amax=x_amax, b_amax=w_amax)
     return y, agg, arg
@@ -983,36 +984,28 @@ class SageMaxLayerFn(torch.autograd.Function):
                 None, None, None, None, None, None)
 
 
-_WPACK = {}   # (weight pointers, shape, device) -> ([L, 2H, H] pack, its transpose, weight versions)
-
-
 def _weight_pack(pairs, L: int, H: int):
-    """[L, 2H, H] / [L, H, 2H] buffers holding one layer loop's [W_l;W_r] (and transpose), refilled
-    only when a weight changed (its autograd version moved, e.g. an optimizer step). A pack that
-    is refilled is a NEW pair of buffers, never the one a live autograd graph may have saved, so a
-    second forward before the first backward (two micro-batches, an eval forward in between)
-    keeps the first graph's operands intact. (A fresh torch.cat of the 2L weights each step
-    blocked the host ~0.4 ms, tools/host_profile.py; this is one multi-tensor copy.)"""
+    """[L, 2H, H] / [L, H, 2H] buffers holding one layer loop's [W_l;W_r] (and its transpose),
+    filled by one multi-tensor copy and one transpose on every call (~20 us of GPU time per
+    step; a fresh torch.cat of the 2L weights each step blocked the host ~0.4 ms,
+    tools/host_profile.py). Every call packs into NEW buffers, never into ones a live autograd
+    graph may have saved, so a second forward before the first backward (two micro-batches, an
+    eval forward in between) keeps the first graph's operands intact. (Round 4 reused the pack
+    while the weights' data pointers and autograd versions were unchanged; round-4 ADVICE: a
+    freed model's addresses can be handed to a new model with equal versions, and writes through
+    p.data bump no version, so a reused pack could be stale. Refilling costs nothing measurable.)"""
     dev = pairs[0][0].device
-    key = (tuple((a.data_ptr(), b.data_ptr()) for a, b in pairs), L, H, dev, DGRAD_WT)
-    vers = tuple(t._version for pr in pairs for t in pr)
-    ent = _WPACK.get(key)
-    if ent is not None and ent[2] == vers:
-        return ent[0], ent[1]
-    if ent is None and len(_WPACK) > 16:
-        _WPACK.clear()
     W = torch.empty(L, 2 * H, H, dtype=torch.float32, device=dev)
     Wt = torch.empty(L, H, 2 * H, dtype=torch.float32, device=dev) if DGRAD_WT else None
     torch._foreach_copy_([W[i, k * H:(k + 1) * H] for i in range(L) for k in (0, 1)], [t for pr in pairs for t in pr])
     if Wt is not None:
         Wt.copy_(W.transpose(1, 2))
-    _WPACK[key] = (W, Wt, vers)
     return W, Wt
 
 
 def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
     """[W_l;W_r] and its transpose for every layer of a loop in a few launches (one multi-tensor
-    copy into a pack that is reused while the weights are unchanged, one transpose, one max|W|
+    copy into a fresh pack, one transpose, one max|W|
     launch per run of layers that take it) instead of three launches per layer. pairs:
     [(w_l, w_r)] per layer; amax_bufs: the loop's zeroed [L, 3] operand-max slots, whose slot 0
     receives max|[W_l;W_r]| for the layers where fill_amax[i] (a folded layer scales by max|Wf|

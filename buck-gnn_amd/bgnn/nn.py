@@ -145,7 +145,8 @@ class _BatchNormFn(torch.autograd.Function):
             slots = _lib.query("bgnn_bn_slots", N, C)
             part = torch.empty(slots, 2, C, dtype=torch.float32, device=dev)
             _lib.call("bgnn_bn_stats", x.data_ptr(), N, C, part.data_ptr(), s)
-            _lib.call("bgnn_bn_finalize", part.data_ptr(), slots, C, N, None if w is None else w.data_ptr(),
+            _lib.call("bgnn_bn_finalize_shifted", part.data_ptr(), slots, C, N, x.data_ptr(),
+                      None if w is None else w.data_ptr(),
                       None if b is None else b.data_ptr(), float(eps), float(momentum),
                       None if running_mean is None else running_mean.data_ptr(),
                       None if running_var is None else running_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),

@@ -31,7 +31,9 @@ inline int bn_blocks(int64_t n_rows, int C, int64_t* rpb) {
 }
 
 // column partials of a (and, when b != NULL, of a * xhat(b)) over the block's rows -> part[blk]
-// MODE 0: sum x, sum x^2 (forward statistics); MODE 1: sum g, sum g * (x - mean) * invstd
+// MODE 0: sum (x - k), sum (x - k)^2 (forward statistics, shifted by k = `mean`, the input's first
+// row: the variance stays free of the E[x^2] - E[x]^2 cancellation when |mean| >> std; finalized
+// by bgnn_bn_finalize_shifted); MODE 1: sum g, sum g * (x - mean) * invstd
 template <int MODE>
 __global__ __launch_bounds__(256) void k_bn_colsums(const float* __restrict__ a, const float* __restrict__ x,
                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -44,18 +46,22 @@ __global__ __launch_bounds__(256) void k_bn_colsums(const float* __restrict__ a,
     const int64_t r0 = (int64_t)lb * rows_per_block, r1 = min(n_rows, r0 + rows_per_block);
     float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
     float mu[4] = {0.f, 0.f, 0.f, 0.f}, is[4] = {1.f, 1.f, 1.f, 1.f};
-    if (MODE == 1) {
+    {   // MODE 0: the shift k; MODE 1: mean and invstd
         const float4 m4 = *reinterpret_cast<const float4*>(mean + c);
-        const float4 i4 = *reinterpret_cast<const float4*>(invstd + c);
+        const float4 i4 = MODE == 1 ? *reinterpret_cast<const float4*>(invstd + c) : make_float4(1.f, 1.f, 1.f, 1.f);
         mu[0] = m4.x; mu[1] = m4.y; mu[2] = m4.z; mu[3] = m4.w;
-        is[0] = i4.x; is[1] = i4.y; is[2] = i4.z; is[3] = i4.w;
+        if (MODE == 1) { is[0] = i4.x; is[1] = i4.y; is[2] = i4.z; is[3] = i4.w; }
     }
     for (int64_t r = r0 + ph; r < r1; r += rpi) {
         const float4 av = reinterpret_cast<const float4*>(a)[r * C4 + c4];
         const float aa[4] = {av.x, av.y, av.z, av.w};
         if (MODE == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { s0[k] += aa[k]; s1[k] += aa[k] * aa[k]; }
+            for (int k = 0; k < 4; ++k) {
+                const float d = aa[k] - mu[k];
+                s0[k] += d;
+                s1[k] += d * d;
+            }
         } else {
             const float4 xv = reinterpret_cast<const float4*>(x)[r * C4 + c4];
             const float xx[4] = {xv.x, xv.y, xv.z, xv.w};
@@ -142,7 +148,9 @@ extern "C" int bgnn_bn_stats(const float* x, int64_t n_rows, int32_t C, float* p
     BGNN_REQUIRE(x && partial && aligned16(x) && aligned16(partial), "bn_stats: 16-byte aligned x / partial required");
     int64_t rpb = 0;
     const int blocks = bn_blocks(n_rows, C, &rpb);
-    hipLaunchKernelGGL(k_bn_colsums<0>, dim3(blocks), dim3(256), 0, as_stream(stream), x, nullptr, nullptr, nullptr,
+    if (n_rows == 0) return BGNN_OK;
+    // shift = the first row of x (bgnn_bn_finalize_shifted adds it back)
+    hipLaunchKernelGGL(k_bn_colsums<0>, dim3(blocks), dim3(256), 0, as_stream(stream), x, nullptr, x, nullptr,
                        n_rows, C, rpb, partial);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;

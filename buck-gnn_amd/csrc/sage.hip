@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const float* __restrict__ 
                                                       const float* __restrict__ beta, float eps, float momentum,
                                                       float* __restrict__ rmean, float* __restrict__ rvar,
                                                       float* __restrict__ mean, float* __restrict__ invstd,
-                                                      float* __restrict__ scale, float* __restrict__ shift) {
+                                                      float* __restrict__ scale, float* __restrict__ shift,
+                                                      const float* __restrict__ kshift) {
     constexpr int CPB = 8, NPH = 256 / CPB;   // channels per block, slot phases
     __shared__ double red[2][NPH][CPB];
     const int cl = threadIdx.x % CPB, ph = threadIdx.x / CPB;
@@ -175,10 +176,12 @@ __global__ __launch_bounds__(256) void k_reduce_slots(const float* __restrict__ 
         if (out0) out0[c] = accumulate ? out0[c] + (float)s0 : (float)s0;
         if (out1) out1[c] = accumulate ? out1[c] + (float)s1 : (float)s1;
     } else {
+        // (kshift: the partials are sums of x - k and (x - k)^2, mean = k + their mean)
         const double n = (double)count;
-        const double mu = s0 / n;
-        double var = s1 / n - mu * mu;
+        const double mu0 = s0 / n;
+        double var = s1 / n - mu0 * mu0;
         if (var < 0.0) var = 0.0;
+        const double mu = kshift ? (double)kshift[c] + mu0 : mu0;
         const double is = 1.0 / sqrt(var + (double)eps);
         const float g = gamma ? gamma[c] : 1.f;
         const float b = beta ? beta[c] : 0.f;
@@ -687,7 +690,7 @@ extern "C" int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32
     if (g_one_pass_reduce) {
         hipLaunchKernelGGL(k_reduce_slots<0>, dim3((H + 7) / 8), dim3(256), 0, s, partial, n_slots, H, out0, out1,
                            accumulate, (int64_t)0, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr,
-                           nullptr, nullptr);
+                           nullptr, nullptr, nullptr);
         BGNN_CHECK_LAUNCH();
         return BGNN_OK;
     }
@@ -708,7 +711,7 @@ extern "C" int bgnn_bn_finalize(const float* bn_partial, int32_t n_slots, int32_
     if (g_one_pass_reduce) {
         hipLaunchKernelGGL(k_reduce_slots<1>, dim3((H + 7) / 8), dim3(256), 0, s, bn_partial, n_slots, H, nullptr,
                            nullptr, 0, count, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd,
-                           scale, shift);
+                           scale, shift, nullptr);
         BGNN_CHECK_LAUNCH();
         return BGNN_OK;
     }
@@ -716,6 +719,19 @@ extern "C" int bgnn_bn_finalize(const float* bn_partial, int32_t n_slots, int32_
     BGNN_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_bn_finalize, dim3((H + 63) / 64), dim3(256), 0, s, bn_partial, n_slots, stride, H, count,
                        gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_bn_finalize_shifted(const float* bn_partial, int32_t n_slots, int32_t H, int64_t count,
+                                        const float* kshift, const float* gamma, const float* beta, float eps,
+                                        float momentum, float* running_mean, float* running_var, float* mean,
+                                        float* invstd, float* scale, float* shift, void* stream) {
+    BGNN_REQUIRE(bn_partial && kshift && H > 0 && count > 0 && mean && invstd && scale && shift,
+                 "bn_finalize_shifted: bad args");
+    hipLaunchKernelGGL(k_reduce_slots<1>, dim3((H + 7) / 8), dim3(256), 0, as_stream(stream), bn_partial, n_slots, H,
+                       nullptr, nullptr, 0, count, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd,
+                       scale, shift, kshift);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

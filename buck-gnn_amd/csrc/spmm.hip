@@ -17,6 +17,8 @@
 // (super nodes, VirtualEdgeCreate.py:106-111) are skipped here and reduced by
 // `chunk`-edge pieces in k_seg_chunk, then combined in chunk order
 // (k_seg_combine) — deterministic, no atomics.
+#include <vector>
+
 #include "common.h"
 #include "gemm_common.h"
 
@@ -983,6 +985,26 @@ inline int64_t group_grid(int64_t G) {
     return blocks < 8 ? 8 : blocks;
 }
 
+// Optional timing of the heavy-row (super node) launches: while enabled, every launch_all with
+// chunks records a HIP event pair around its k_seg_chunk + k_seg_combine launches (bench.py's
+// cfg3 block reports the super rows' share of the aggregation; bgnn_heavy_timing).
+struct HeavyEv { hipEvent_t a, b; int fwd; };
+static std::vector<HeavyEv> g_heavy_ev;
+static size_t g_heavy_used = 0;
+static bool g_heavy_on = false;
+
+inline HeavyEv* heavy_ev_next(int fwd) {
+    if (!g_heavy_on) return nullptr;
+    if (g_heavy_used == g_heavy_ev.size()) {
+        HeavyEv e{};
+        if (hipEventCreate(&e.a) != hipSuccess || hipEventCreate(&e.b) != hipSuccess) return nullptr;
+        g_heavy_ev.push_back(e);
+    }
+    HeavyEv* e = &g_heavy_ev[g_heavy_used++];
+    e->fwd = fwd;
+    return e;
+}
+
 // Whether launch_all runs the row-group kernel for this CSR / reduce.
 inline bool use_group(const SegArgs& A, int op, int vec, int lpr) {
     return g_seg_kernel == 0 && A.gcnt != nullptr && vec == 4 && lpr == 64 && A.chunk <= 64 &&
@@ -1051,6 +1073,8 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
         BGNN_CHECK_LAUNCH();
     }
     if (A.n_chunks > 0) {
+        HeavyEv* ev = heavy_ev_next(EPI == EPI_SAGE);
+        if (ev) (void)hipEventRecord(ev->a, s);
         constexpr int COP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MAXT ? OP_MAXT : (OP == OP_MEANT ? OP_MEANT : OP_SUM));
         hipLaunchKernelGGL((k_seg_chunk<VEC, NV, LPR, COP>), dim3((A.n_chunks + 3) / 4, ctiles), dim3(256), 0, s,
                            A);
@@ -1059,6 +1083,7 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
         hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles),
                            dim3(MOP == OP_MAX ? 256 : 64 * kCombineWaves), 0, s, A);
         BGNN_CHECK_LAUNCH();
+        if (ev) (void)hipEventRecord(ev->b, s);
     }
     return BGNN_OK;
 }
@@ -1258,4 +1283,28 @@ extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldz
     }
     return reduce == BGNN_REDUCE_SUM ? launch_all<4, 1, 64, OP_SUM, EPI_SAGE>(A, 1, kMaxLightBlocks, s, &blocks)
                                      : launch_all<4, 1, 64, OP_MEAN, EPI_SAGE>(A, 1, kMaxLightBlocks, s, &blocks);
+}
+
+extern "C" int bgnn_heavy_timing(int32_t enable) {
+    g_heavy_on = enable != 0;
+    if (g_heavy_on) g_heavy_used = 0;
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_heavy_timing_read(int32_t which, float* total_ms, int32_t* count) {
+    BGNN_REQUIRE(total_ms && count && (which == 0 || which == 1), "heavy_timing_read: bad args");
+    double t = 0.0;
+    int32_t n = 0;
+    for (size_t i = 0; i < g_heavy_used; ++i) {
+        const HeavyEv& e = g_heavy_ev[i];
+        if (e.fwd != (which == 0 ? 1 : 0)) continue;
+        BGNN_HIP(hipEventSynchronize(e.b));
+        float ms = 0.f;
+        BGNN_HIP(hipEventElapsedTime(&ms, e.a, e.b));
+        t += ms;
+        ++n;
+    }
+    *total_ms = (float)t;
+    *count = n;
+    return BGNN_OK;
 }

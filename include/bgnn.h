@@ -82,6 +82,12 @@ const char* bgnn_last_error_string(void);
                                     rounding (the order of the dh bias partials / of the
                                     BatchNorm statistics sums; deterministic either way).
                                     Default 1 (measured: bits 1-3 gain nothing)              */
+/* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
+ * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
+ * read: which = 0 the forward SAGE aggregations (bgnn_sage_fwd), 1 every other (the transpose
+ * aggregations); total_ms = summed chunk + combine time, count = launches (synchronises). */
+int bgnn_heavy_timing(int32_t enable);
+int bgnn_heavy_timing_read(int32_t which, float* total_ms, int32_t* count);
 /* Current value of a knob (-1 for an unknown knob). */
 int32_t bgnn_get_tuning(int32_t knob);
 int bgnn_set_tuning(int32_t knob, int32_t value);
@@ -521,6 +527,13 @@ int bgnn_add_dropout(const float* a, const float* b, int64_t n, float p, uint64_
  * ---------------------------------------------------------------------- */
 int32_t bgnn_bn_slots(int64_t n_rows, int32_t C);
 int bgnn_bn_stats(const float* x, int64_t n_rows, int32_t C, float* partial, void* stream);
+/* BatchNorm finalize of bgnn_bn_stats' shifted partials (sums of x - k and (x - k)^2 with k =
+ * kshift = the input's first row, which bgnn_bn_stats uses): as bgnn_bn_finalize, mean = k + the
+ * shifted mean (round-4 ADVICE: no E[x^2] - E[x]^2 cancellation when |mean| >> std). */
+int bgnn_bn_finalize_shifted(const float* bn_partial, int32_t n_slots, int32_t H, int64_t count,
+                             const float* kshift, const float* gamma, const float* beta, float eps, float momentum,
+                             float* running_mean, float* running_var, float* mean, float* invstd, float* scale,
+                             float* shift, void* stream);
 int bgnn_bn_apply(const float* x, int64_t n_rows, int32_t C, const float* scale, const float* shift, float* y,
                   void* stream);
 int bgnn_bn_bwd_stats(const float* g, const float* x, const float* mean, const float* invstd, int64_t n_rows,

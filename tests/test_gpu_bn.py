@@ -81,3 +81,30 @@ def test_per_op_model_with_bgnn_batchnorm_matches_torch_batchnorm(dev):
                    + [p.grad for p in m.batch_norms.parameters()] + [m.batch_norms[2].running_var.clone()])
     for a, c in zip(*res):
         torch.testing.assert_close(a, c, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("offset", [1e3, -3e3])
+def test_bgnn_batchnorm_large_channel_offset(dev, offset):
+    """|mean| >> std (x = offset + randn): the statistics are shifted sums (bgnn_bn_stats subtracts
+    the first row, bgnn_bn_finalize_shifted adds it back), so the variance does not cancel; the
+    output, input gradient and running variance stay within the fp32 tolerances against fp64 torch
+    (round-4 ADVICE, low)."""
+    torch.manual_seed(7)
+    N, C = 5041, 512
+    ref = torch.nn.BatchNorm1d(C).double()
+    ours = bnn.use_bgnn_batchnorm(copy.deepcopy(ref).float().to(dev))
+    x = torch.randn(N, C, dtype=torch.float64) + offset
+    x32 = x.float()
+    g = torch.randn(N, C, dtype=torch.float64)
+    xr = x32.double().requires_grad_(True)     # (the fp32 input both sides see)
+    xo = x32.to(dev).requires_grad_(True)
+    yr = ref(xr)
+    yo = ours(xo)
+    yr.backward(g)
+    yo.backward(g.float().to(dev))
+    # (y = x * scale + shift in fp32 carries ~ulp(offset) of rounding: atol 1e-3 at |offset| <= 3e3;
+    # the one-pass E[x^2] - E[x]^2 form missed the variance by ~10 % here)
+    torch.testing.assert_close(yo.detach().cpu(), yr.detach().float(), rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(ours.running_var.cpu(), ref.running_var.float(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(ours.running_mean.cpu(), ref.running_mean.float(), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(xo.grad.cpu(), xr.grad.float(), rtol=1e-3, atol=2e-3)

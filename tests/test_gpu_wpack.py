@@ -36,7 +36,6 @@ def test_second_forward_before_backward(dev, monkeypatch, between):
     out = {}
     for persistent in (False, True):
         monkeypatch.setattr(fused, "PERSISTENT_WPACK", persistent)
-        fused._WPACK.clear()
         bgnn.clear_caches()
         model = _model(dev)
         model.zero_grad(set_to_none=True)
@@ -58,24 +57,80 @@ def test_second_forward_before_backward(dev, monkeypatch, between):
         assert torch.equal(out[True][1][k], out[False][1][k]), k
 
 
-def test_pack_refilled_after_optimizer_step(dev):
-    """After an in-place weight update the next forward sees the new weights (the pack follows
-    the weights' autograd versions), and the pack is reused while they are unchanged."""
+def _fwd(model, b):
+    with torch.no_grad():
+        return model(b.x, b.edge_index, b.edge_attr, b.batch)[0]
+
+
+def _fresh_fwd(model, b, monkeypatch):
+    monkeypatch.setattr(fused, "PERSISTENT_WPACK", False)
+    try:
+        return _fwd(model, b)
+    finally:
+        monkeypatch.setattr(fused, "PERSISTENT_WPACK", True)
+
+
+def test_pack_follows_in_place_writes(dev, monkeypatch):
+    """Weight writes that bump no autograd version (through p.data) and ones that do (no_grad
+    in-place ops) are both seen by the next forward: the pack is refilled on every call."""
     b1, _ = _batches(dev)
-    fused._WPACK.clear()
     bgnn.clear_caches()
-    model = _model(dev)
-    model.eval()
-    with torch.no_grad():
-        y0, _ = model(b1.x, b1.edge_index, b1.edge_attr, b1.batch)
-        n_packs = len(fused._WPACK)
-        y0b, _ = model(b1.x, b1.edge_index, b1.edge_attr, b1.batch)
-        assert len(fused._WPACK) == n_packs and torch.equal(y0, y0b)
-        for conv in model.sage_blocks_add:
-            conv.lin_l.weight.mul_(0.5)
-        y1, _ = model(b1.x, b1.edge_index, b1.edge_attr, b1.batch)
+    model = _model(dev).eval()
+    y0 = _fwd(model, b1)
+    assert torch.equal(y0, _fwd(model, b1))
+    for conv in model.sage_blocks_add:
+        conv.lin_l.weight.data.mul_(0.5)          # (no version bump)
+    y1 = _fwd(model, b1)
     assert not torch.equal(y0, y1)
-    fused._WPACK.clear()
+    assert torch.equal(y1, _fresh_fwd(model, b1, monkeypatch))
     with torch.no_grad():
-        y1_fresh, _ = model(b1.x, b1.edge_index, b1.edge_attr, b1.batch)
-    assert torch.equal(y1, y1_fresh)
+        for conv in model.sage_blocks_add:
+            conv.lin_r.weight.mul_(2.0)           # (version bump)
+    y2 = _fwd(model, b1)
+    assert not torch.equal(y1, y2)
+    assert torch.equal(y2, _fresh_fwd(model, b1, monkeypatch))
+
+
+def test_new_model_at_freed_addresses(dev, monkeypatch):
+    """Model A evaluated and freed, model B of the same shapes built with different weights (the
+    caching allocator may hand B A's addresses, with equal autograd versions): B's forward uses
+    B's weights (INFERENCE.py evaluates one checkpoint after another this way)."""
+    b1, _ = _batches(dev)
+    bgnn.clear_caches()
+    torch.manual_seed(1)
+    a = bgnn.BuckGNN(16, 5, hidden_channels=128, num_layers=4, dropout_rate=0.0,
+                     model_name="GraphSage_addAggr").to(dev).eval()
+    ya = _fwd(a, b1)
+    del a
+    torch.manual_seed(2)
+    b = bgnn.BuckGNN(16, 5, hidden_channels=128, num_layers=4, dropout_rate=0.0,
+                     model_name="GraphSage_addAggr").to(dev).eval()
+    yb = _fwd(b, b1)
+    assert not torch.equal(ya, yb)
+    assert torch.equal(yb, _fresh_fwd(b, b1, monkeypatch))
+
+
+@pytest.mark.parametrize("variant", ["foreach", "fused", "for_loop"])
+def test_adam_steps_match_fresh_pack(dev, monkeypatch, variant):
+    """Three training steps under a real torch.optim.Adam (foreach, fused and for-loop forms):
+    losses and parameters bit-identical to the fresh-concatenation path."""
+    b1, b2 = _batches(dev)
+    res = {}
+    for persistent in (True, False):
+        monkeypatch.setattr(fused, "PERSISTENT_WPACK", persistent)
+        bgnn.clear_caches()
+        model = _model(dev)
+        kw = {"foreach": dict(foreach=True), "fused": dict(fused=True), "for_loop": dict(foreach=False)}[variant]
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2, **kw)
+        losses = []
+        for b in (b1, b2, b1):
+            opt.zero_grad(set_to_none=True)
+            p, _ = model(b.x, b.edge_index, b.edge_attr, b.batch)
+            loss = p.square().mean()
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+        res[persistent] = (losses, {n: t.detach().clone() for n, t in model.state_dict().items()})
+    assert res[True][0] == res[False][0]
+    for k, v in res[False][1].items():
+        assert torch.equal(res[True][1][k], v), k
