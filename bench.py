@@ -518,7 +518,7 @@ def cfg3_block(args, dev, world, rank):
     heavy = m["heavy"] or {}
     sup = {"heavy_rows_per_batch": int(g.fwd.plan.n_heavy), "chunks_per_batch": int(g.fwd.plan.n_chunks),
            "chunk_edges": _graph.DEFAULT_CHUNK}
-    for name, key in (("fwd", "sage_fwd"), ("bwd", "spmm_bwd")):
+    for name, key in (("fwd", "agg_fwd"), ("bwd", "spmm_bwd")):
         ms, n = heavy.get(name, (0.0, 0))
         agg = blocks["roofline_hbm" if name == "fwd" else "roofline_agg_bwd"]
         sup[f"chunk_combine_ms_per_launch_{name}"] = round(ms / n, 5) if n else None

@@ -992,6 +992,7 @@ struct HeavyEv { hipEvent_t a, b; int fwd; };
 static std::vector<HeavyEv> g_heavy_ev;
 static size_t g_heavy_used = 0;
 static bool g_heavy_on = false;
+static int g_heavy_dir = 0;   // set by the entry points: 0 = forward aggregation, 1 = transpose
 
 inline HeavyEv* heavy_ev_next(int fwd) {
     if (!g_heavy_on) return nullptr;
@@ -1073,7 +1074,7 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
         BGNN_CHECK_LAUNCH();
     }
     if (A.n_chunks > 0) {
-        HeavyEv* ev = heavy_ev_next(EPI == EPI_SAGE);
+        HeavyEv* ev = heavy_ev_next(g_heavy_dir == 0);
         if (ev) (void)hipEventRecord(ev->a, s);
         constexpr int COP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MAXT ? OP_MAXT : (OP == OP_MEANT ? OP_MEANT : OP_SUM));
         hipLaunchKernelGGL((k_seg_chunk<VEC, NV, LPR, COP>), dim3((A.n_chunks + 3) / 4, ctiles), dim3(256), 0, s,
@@ -1139,6 +1140,7 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
     BGNN_REQUIRE(reduce >= 0 && reduce <= 2, "spmm_fwd: bad reduce %d", reduce);
     BGNN_REQUIRE(csr->n_chunks == 0 || partial, "spmm_fwd: partial scratch required for heavy rows");
     SegArgs A = args_from_csr(csr);
+    g_heavy_dir = 0;
     A.H = H;
     A.x = x; A.ldx = ldx;
     A.out = out; A.ldo = ldo;
@@ -1177,6 +1179,7 @@ extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t,
     BGNN_REQUIRE(H > 0 && ldg >= H && ldgx >= H, "spmm_bwd: bad H/ld");
     BGNN_REQUIRE(csr_t->n_chunks == 0 || partial, "spmm_bwd: partial scratch required");
     SegArgs A = args_from_csr(csr_t);
+    g_heavy_dir = 1;
     A.H = H;
     A.x = g; A.ldx = ldg;
     A.out = gx; A.ldo = ldgx;
@@ -1266,6 +1269,7 @@ extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldz
                  "sage_fwd: pointers must be 16-byte aligned");
     BGNN_REQUIRE(csr->n_chunks == 0 || partial, "sage_fwd: partial scratch required for heavy rows");
     SegArgs A = args_from_csr(csr);
+    g_heavy_dir = 0;
     A.H = H;
     A.x = zl; A.ldx = ldzl;
     A.zr = zr; A.ldzr = ldzr;

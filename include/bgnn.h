@@ -84,8 +84,9 @@ const char* bgnn_last_error_string(void);
                                     Default 1 (measured: bits 1-3 gain nothing)              */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
- * read: which = 0 the forward SAGE aggregations (bgnn_sage_fwd), 1 every other (the transpose
- * aggregations); total_ms = summed chunk + combine time, count = launches (synchronises). */
+ * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose
+ * aggregations (bgnn_spmm_bwd, bgnn_spmm_bwd_add); total_ms = summed chunk + combine time,
+ * count = launches (synchronises). */
 int bgnn_heavy_timing(int32_t enable);
 int bgnn_heavy_timing_read(int32_t which, float* total_ms, int32_t* count);
 /* Current value of a knob (-1 for an unknown knob). */

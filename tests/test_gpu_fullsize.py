@@ -1,14 +1,25 @@
 """GPU: the bench's whole train-step forward + backward at full BASELINE size against the fp64
-oracle (the reference orchestration Models/BuckGNN.py:67-74,323,430-444 over the PyG
-restatement), on the exact code path bench.py times: GraphSage_addAggr h=512 L=6 on a full
-cfg2 batch (16 x 71x71 meshes with virtual edges: N = 80,656, E = 715,872) and a full cfg3
-batch (16 meshes with super nodes of in-degree 5,041: N = 80,672, E = 792,992), folded node
-encoder + bgnn_mlp2 head, fused layers, BatchNorm in train mode, dropout 0 (torch's dropout RNG
-cannot be matched). Checked: the 16 predictions and the RelativeErrorLoss within the north
-star's 1e-4, every used parameter's gradient within the golden fixtures' checksum tolerance,
-the whole gradient tensors within 1e-3 relative L2 per parameter (with a noise floor for the
-gradients that are exactly 0 in exact arithmetic), BatchNorm running statistics, and the set of
-parameters with gradients."""
+oracle (the reference orchestration Models/BuckGNN.py:67-74,323,430-471 over the PyG
+restatement), on the exact code path bench.py times, for every SAGE variant of the layer loop:
+GraphSage_addAggr (:430-444), GraphSage_meanAggr (:445-458), GraphSage_maxAggr (:459-471) and
+GraphSage_addAggr_Shared (:338-352, TRAIN_FINAL.py's default) at h=512 L=6, on a full cfg2 batch
+(16 x 71x71 meshes with virtual edges: N = 80,656, E = 715,872) and a full cfg3 batch (16 meshes
+with super nodes of in-degree 5,041: N = 80,672, E = 792,992); folded node encoder + bgnn_mlp2
+head (sum / mean) or the unfolded encoder (max), fused layers, BatchNorm in train mode, dropout 0
+(torch's dropout RNG cannot be matched). Checked: the 16 predictions and the RelativeErrorLoss
+within the north star's 1e-4, every used parameter's gradient checksum, the whole gradient
+tensors within 1e-3 relative L2 per parameter (with a noise floor for the gradients that are
+exactly 0 in exact arithmetic), BatchNorm running statistics, and the set of parameters with
+gradients.
+
+Max aggregation (aggr='max'): the gradient of each (target, channel) goes to ONE argmax source,
+so an f32 forward that orders two near-equal neighbours differently from fp64 routes that
+element's gradient elsewhere. The test makes this explicit instead of widening a tolerance: it
+captures every layer's GPU argmax and its layer input, checks that each place where the GPU's
+choice differs from fp64's first argmax is a near tie -- fp64 margin max - x_choice at most twice
+the layer input's largest f32 error (measured, max |x_gpu - x_fp64|) -- and then evaluates the
+fp64 backward along the GPU's choices, so the whole-tensor gradient bounds are the same as for
+the linear aggregations. The flip counts are printed."""
 import numpy as np
 import pytest
 import torch
@@ -17,42 +28,120 @@ import bgnn
 from bgnn import buckgnn, fused
 from bgnn import synthetic as S
 from oracle import buckgnn_ref as R
+from oracle import pyg_ref
 from recipe import grad_checksum
 
 pytestmark = pytest.mark.gpu
 
+VARIANTS = ["GraphSage_addAggr", "GraphSage_meanAggr", "GraphSage_maxAggr", "GraphSage_addAggr_Shared"]
+
+
+class _ForcedMax(torch.autograd.Function):
+    """fp64 segment max whose backward follows a given argmax (the GPU's), after checking that
+    every disagreement with fp64's own first argmax is a near tie (margin <= tol)."""
+
+    @staticmethod
+    def forward(ctx, src, index, dim_size, eid, tol, stats):
+        idx = index.view(-1, 1).expand_as(src)
+        out = src.new_zeros((dim_size, src.size(1))).scatter_reduce_(0, idx, src, reduce="amax", include_self=False)
+        n = src.size(0)
+        pos = torch.arange(n).view(-1, 1).expand_as(src)
+        hit = src == out.index_select(0, index)
+        first = torch.full(out.shape, n, dtype=torch.long)
+        first.scatter_reduce_(0, idx, torch.where(hit, pos, torch.full_like(pos, n)), reduce="amin", include_self=True)
+        del hit, pos
+        valid = first < n
+        assert torch.equal(eid < n, valid), "GPU argmax on an empty row or none on a non-empty one"
+        flip = valid & (eid != first)
+        if flip.any():
+            rows, cols = torch.nonzero(flip, as_tuple=True)
+            margin = out[rows, cols] - src[eid[rows, cols], cols]
+            assert bool((index[eid[rows, cols]] == rows).all()), "GPU argmax outside the row's edges"
+            stats.append((int(flip.sum()), float(margin.max()), tol))
+            assert float(margin.max()) <= tol, ("argmax flip beyond a near tie", float(margin.max()), tol)
+        else:
+            stats.append((0, 0.0, tol))
+        ctx.save_for_backward(torch.where(valid, eid, torch.full_like(eid, n)))
+        ctx.n = n
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (sel,) = ctx.saved_tensors
+        n = ctx.n
+        gs = g.new_zeros((n + 1, g.size(1)))
+        gs.scatter_(0, sel, g)
+        return gs[:n], None, None, None, None, None
+
 
 @pytest.mark.parametrize("cfg", ["cfg2", "cfg3"])
-def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg):
+@pytest.mark.parametrize("model_name", VARIANTS)
+def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg, model_name):
     b = S.make_config_batch(cfg)
     assert (b.num_nodes, b.num_edges) == {"cfg2": (80656, 715872), "cfg3": (80672, 792992)}[cfg]
+    is_max = model_name == "GraphSage_maxAggr"
     torch.manual_seed(0)
-    m = bgnn.BuckGNN(16, 5, hidden_channels=512, num_layers=6, dropout_rate=0.0, model_name="GraphSage_addAggr")
+    m = bgnn.BuckGNN(16, 5, hidden_channels=512, num_layers=6, dropout_rate=0.0, model_name=model_name)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     m = m.to(dev).train()
     folds = []
     real_layer = buckgnn.sage_layer
     monkeypatch.setattr(buckgnn, "sage_layer", lambda *a, **k: folds.append(k.get("w_in") is not None)
                         or real_layer(*a, **k))
+    captured = []   # max: per layer (input x [N, C] f32, argmax [N, C] as forward-CSR positions)
+    if is_max:
+        real_mt = fused._max_transform
+
+        def spy(x, *a, **k):
+            y, agg, arg = real_mt(x, *a, **k)
+            captured.append((x.detach().cpu(), arg.detach().cpu()))
+            return y, agg, arg
+        monkeypatch.setattr(fused, "_max_transform", spy)
     bd = b.to(dev)
     pred, _ = m(bd.x, bd.edge_index, bd.edge_attr, bd.batch)
     loss = bgnn.RelativeErrorLoss()(pred, bd.y)
     loss.backward()
     torch.cuda.synchronize()
-    assert folds == [True] + [False] * 5                       # the bench's folded-encoder path
+    # the bench's path: the encoder folded into the first layer for sum / mean, not for max
+    assert folds == ([False] * 6 if is_max else [True] + [False] * 5)
+    assert len(captured) == (6 if is_max else 0)
     got = {k: p.grad.detach().cpu().double().numpy() for k, p in m.named_parameters() if p.grad is not None}
     state = {k: v.detach().cpu() for k, v in m.state_dict().items() if "running_" in k}
     pred_g, loss_g = pred.detach().cpu().double(), float(loss.item())
     del m, bd, pred, loss
     torch.cuda.empty_cache()
 
-    # fp64 oracle on the host (~25 s with 8-16 threads)
+    # fp64 oracle on the host (~25-60 s with 8-16 threads)
     torch.set_num_threads(min(16, torch.get_num_threads()))
+    flips = []
+    if is_max:
+        # forward-CSR position -> edge id (the CSR is a stable sort of edge_index by target)
+        perm = torch.from_numpy(np.argsort(b.edge_index[1].numpy(), kind="stable"))
+        E = b.edge_index.size(1)
+        layer = [0]
+        real_agg = pyg_ref.sage_aggregate
+
+        def forced_aggregate(x, edge_index, aggr):
+            assert aggr == "max"
+            k = layer[0]
+            layer[0] += 1
+            xg, arg = captured[k]
+            # the layer input's largest f32 error: the flip allowance is twice it
+            tol = 2.0 * float((xg.double() - x.detach()).abs().max())
+            arg = arg.long()
+            eid = torch.where(arg >= 0, perm[arg.clamp_min(0)], torch.full_like(arg, E))
+            msg = x.index_select(0, edge_index[0])
+            return _ForcedMax.apply(msg, edge_index[1], x.size(0), eid, tol, flips)
+        monkeypatch.setattr(pyg_ref, "sage_aggregate", forced_aggregate)
+        monkeypatch.setattr(R, "sage_aggregate", forced_aggregate, raising=False)
     st = {k: v.double().clone().requires_grad_(v.is_floating_point() and "running" not in k
                                                and "num_batches" not in k) for k, v in sd.items()}
-    pred_o = R.forward(st, "GraphSage_addAggr", b.x.double(), b.edge_index, b.batch, True, "mean", 0.0)
+    pred_o = R.forward(st, model_name, b.x.double(), b.edge_index, b.batch, True, "mean", 0.0)
     loss_o = R.relative_error_loss(pred_o, b.y.double())
     loss_o.backward()
+    if is_max:
+        assert len(flips) == 6
+        print("argmax flips per layer (count, largest fp64 margin, allowance):", flips)
 
     np.testing.assert_allclose(pred_g.numpy(), pred_o.detach().numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(loss_g, float(loss_o), rtol=1e-4, atol=1e-4)
