@@ -1,12 +1,12 @@
 #!/usr/bin/env python
-"""A/B of the f16x3 GEMM staging variants on the SAGE layer shapes, in one process: the
-register-staged kernel (staging -1) against the LDS-DMA variants, each timed over REPS launches
-with HIP events with operand maxima supplied (as inside the layer: no absmax passes), with a
-1 GiB cache flush between launches (cold L2 / Infinity Cache, as inside a training step).
+"""A/B of f16x3 GEMM variants on the SAGE layer shapes, in one process, each timed over REPS
+launches with HIP events with operand maxima supplied (as inside the layer: no absmax passes),
+with a 1 GiB cache flush between launches (cold L2 / Infinity Cache, as inside a training step).
 
-    python tools/gemm_ab.py [--reps 20] [--variants=-1,0,1,x5] [--shapes fwd,dgrad]
+    python tools/gemm_ab.py [--reps 20] [--variants=x-1,x2,x102] [--shapes fwd,dgrad]
 
-A variant "xC" runs the register-staged kernel on tile config C (bgnn_gemm_set_cfg).
+A variant "xC" runs tile config C % 100 with timing ablation C // 100 (bgnn_gemm_set_cfg; x-1 =
+the automatic plan); "wN" the pre-split-weight kernel family with variant N (bgnn_gemm_w_variant).
 """
 import argparse
 import os
@@ -25,7 +25,7 @@ SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872,
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="-1,0,1,2")
+    ap.add_argument("--variants", default="x-1")
     ap.add_argument("--shapes", default="fwd,dgrad")
     ap.add_argument("--no-flush", action="store_true")
     args = ap.parse_args()
@@ -40,9 +40,9 @@ def main():
         out = torch.empty(M, N, device=dev)
         ref = None
         for vs in args.variants.split(","):
-            v = -1 if vs.startswith("x") else int(vs)
-            _lib.call("bgnn_set_tuning", 8, v)
             _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if vs.startswith("x") else -1)
+            if hasattr(_lib, "has") and _lib.has("bgnn_gemm_w_variant"):
+                _lib.call("bgnn_gemm_w_variant", int(vs[1:]) if vs.startswith("w") else -1)
             ts = []
             for i in range(args.reps + 3):
                 if flush is not None:
@@ -61,7 +61,6 @@ def main():
                 ref = out.clone()
             print(f"{name:9s} {M}x{N}x{K} staging {vs:>3s}: median {med:7.1f} us  min {us[0]:7.1f}  "
                   f"{2 * M * N * K / med / 1e6:6.1f} TF  {same}", flush=True)
-        _lib.call("bgnn_set_tuning", 8, -1)
         _lib.call("bgnn_gemm_set_cfg", -1)
 
 

@@ -5,7 +5,7 @@
 #   bash tools/gpu_check.sh TAG [STEP ...]        (on the GPU box, from the repo root)
 #
 # Steps (default: tests smoke bench prof):
-#   tests      pytest -m gpu (PYTEST_ARGS adds arguments, e.g. "-k fullsize"); assertion failures
+#   tests      pytest -m gpu over ${TESTS:-tests} (PYTEST_ARGS adds arguments); assertion failures
 #              (rc 1) are reported and do not stop the later measurements
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (the driver's line; BENCH_ARGS adds arguments)
@@ -53,7 +53,7 @@ for s in $STEPS; do
   case $s in
     tests)
       rc=0
-      timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread ${PYTEST_ARGS:-} \
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -rA --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
         > "gpurun_out/gpu_tests_$TAG.log" 2>&1 || rc=$?
       tail -3 "gpurun_out/gpu_tests_$TAG.log"
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then die tests $rc; fi ;;
