@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lock = threading.Lock()
 _lib = None
@@ -59,6 +59,11 @@ SIGNATURES = {
     "bgnn_store_gather_rows": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_i64, c_p, c_p]),
     "bgnn_get_tuning": (c_i32, [c_i32]),
     "bgnn_heavy_timing": (c_i32, [c_i32]),
+    "bgnn_gemm_w_tile": (c_i32, [c_i64, c_i64, c_i64]),
+    "bgnn_gemm_wsplit_bytes": (c_sz, [c_i64, c_i64]),
+    "bgnn_gemm_wsplit": (c_i32, [c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i32, c_p]),
+    "bgnn_gemm_f32_w": (c_i32, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i32, c_p, c_i64, c_p, c_i32, c_p, c_p, c_p,
+                                c_p, c_i64, c_f32, c_u64, c_p]),
     "bgnn_heavy_timing_read": (c_i32, [c_i32, c_p, c_p]),
     "bgnn_set_tuning": (c_i32, [c_i32, c_i32]),
     "bgnn_graph_build_ws_bytes": (c_sz, [c_i64, c_i64]),

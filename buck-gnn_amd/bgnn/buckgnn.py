@@ -254,7 +254,8 @@ class BuckGNN(nn.Module):
             bufs, fold_amax = scratch[:3 * L].view(L, 3), scratch[3 * L:]
             layers = [convs[i] if convs is not None else self.shared_graphsage_block for i in range(L)]
             wprep = prepare_weights([(c.lin_l.weight, c.lin_r.weight) for c in layers], bufs,
-                                    [not (i == 0 and x_in is not None) for i in range(L)])
+                                    [not (i == 0 and x_in is not None) for i in range(L)],
+                                    n_rows=x.size(0) if red != 2 else 0)
             self._count_bn_batches(bns)
             for i in range(L):
                 conv = layers[i]

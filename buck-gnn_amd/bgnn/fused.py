@@ -54,6 +54,10 @@ BF16_PREP = True
 ABSMAX_ITEMS = True
 # [W_l;W_r] of all layers packed by a multi-tensor copy into a persistent buffer (not torch.cat)
 PERSISTENT_WPACK = True
+# forward / input-gradient GEMMs of the K = H layers take [W_l;W_r] (and its transpose) as images
+# pre-split once per step (bgnn_gemm_wsplit), staged by LDS-DMA in the GEMM (bgnn_gemm_f32_w);
+# bit-identical to the register-staged path (A/B switch)
+WSPLIT = True
 
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
@@ -653,7 +657,14 @@ class SageLayerFn(torch.autograd.Function):
         N = x_prev.size(0)
         # [W_l;W_r] [2H, H] and its transpose (dgrad operand): from prepare_weights (all layers in
         # a few launches; the amax slot then already holds max|W|) or built here
-        wcat, wcat_t_pre = wprep if wprep is not None else (torch.cat([w_l, w_r], 0).contiguous(), None)
+        if isinstance(wprep, WPrep):
+            wcat, wcat_t_pre, img_f, img_d = wprep.wcat, wprep.wcat_t, wprep, wprep
+        elif wprep is not None:
+            (wcat, wcat_t_pre), img_f, img_d = wprep, None, None
+        else:
+            wcat, wcat_t_pre, img_f, img_d = torch.cat([w_l, w_r], 0).contiguous(), None, None, None
+        img_f = img_f if (img_f is not None and img_f.img_f is not None) else None
+        img_d = img_d if (img_d is not None and img_d.img_d is not None) else None
         # operand maxima: [0] = max|W|, [1] = max|x_next| (this layer's output), [2] = max|dz|
         # (zeroed; the layer loop passes one slice of a single per-step fill)
         if amax is None:
@@ -697,6 +708,12 @@ class SageLayerFn(torch.autograd.Function):
                 z = torch.empty(2, N, H, dtype=torch.float32, device=dev)
                 gemm(x_prev, wmat, trans_a=False, trans_b=True, out=Planes(z), a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z[0], z[1], H
+            elif img_f is not None and not folded:   # pre-split [W_l;W_r] staged by LDS-DMA
+                z = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)
+                _lib.call("bgnn_gemm_f32_w", N, 2 * H, H, x_prev.data_ptr(), x_prev.stride(0), img_f.img_f.data_ptr(),
+                          img_f.bn_f, z.data_ptr(), 2 * H, None, 0, x_amax.data_ptr(), w_amax.data_ptr(), None, None, 0,
+                          0.0, 0, _stream())
+                zl, zr, ldz = z, z[:, H:], 2 * H
             else:        # interleaved [N, 2H]
                 z = gemm(x_prev, wmat, trans_a=False, trans_b=True, bias=bf, a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z, z[:, H:], 2 * H
@@ -717,6 +734,7 @@ class SageLayerFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.folded = folded
         ctx.wcat_t = wcat_t_pre
+        ctx.img_d = img_d if not folded else None
         ctx.set_materialize_grads(False)   # the amax output never gets a gradient: no zero fill for it
         ctx.fold = (w_in, b_in, wf) if folded else None
         ctx.save_for_backward(x_prev, o, nrm, wcat, gamma if gamma is not None else torch.empty(0, device=dev),
@@ -807,7 +825,15 @@ class SageLayerFn(torch.autograd.Function):
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
         wcat_t = (ctx.wcat_t if ctx.wcat_t is not None else wcat.t().contiguous()) if DGRAD_WT else wcat
-        if dropadd:
+        img_d = ctx.img_d if (not planes and DGRAD_WT) else None
+        if img_d is not None and (dropadd or gskip is None):   # pre-split [W_l;W_r]^T by LDS-DMA
+            dx = torch.empty(N, H, dtype=torch.float32, device=dev)
+            with _timed("gemm_dgrad"):
+                _lib.call("bgnn_gemm_f32_w", N, H, 2 * H, dz.data_ptr(), lddz, img_d.img_d.data_ptr(), img_d.bn_d,
+                          dx.data_ptr(), H, None, 0, dz_amax.data_ptr(), w_amax.data_ptr(), None,
+                          g.data_ptr() if dropadd else None, H, float(cfg.p) if dropadd else 0.0,
+                          cfg.seed if dropadd else 0, s)
+        elif dropadd:
             dx = torch.empty(N, H, dtype=torch.float32, device=dev)
             M_, K_ = N, 2 * H
             ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M_, H, K_, 0, 1, 0)
@@ -930,7 +956,8 @@ class SageMaxLayerFn(torch.autograd.Function):
             amax = torch.zeros(3, dtype=torch.float32, device=dev)
         w_amax, next_amax, dz_amax = amax[0:1], amax[1:2], amax[2:3]
         if wprep is not None:   # (prepare_weights has folded max|[W_l;W_r]| into the slot)
-            wcat_t = wprep[1] if wprep[1] is not None else wprep[0].t().contiguous()
+            w0, w1 = (wprep.wcat, wprep.wcat_t) if isinstance(wprep, WPrep) else wprep
+            wcat_t = w1 if w1 is not None else w0.t().contiguous()
         else:
             wcat_t = torch.cat([w_l, w_r], 0).t().contiguous()
             absmax(wcat_t, w_amax, accumulate=True)
@@ -1003,7 +1030,33 @@ def _weight_pack(pairs, L: int, H: int):
     return W, Wt
 
 
-def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
+class WPrep:
+    """One layer's prepared weight operands (prepare_weights): [W_l;W_r] [2H, H], its transpose
+    [H, 2H] (dgrad B operand), and optionally their pre-split images (fwd: img_f with column tile
+    bn_f; dgrad: img_d, bn_d) for bgnn_gemm_f32_w."""
+    __slots__ = ("wcat", "wcat_t", "img_f", "bn_f", "img_d", "bn_d")
+
+    def __init__(self, wcat, wcat_t, img_f=None, bn_f=0, img_d=None, bn_d=0):
+        self.wcat, self.wcat_t = wcat, wcat_t
+        self.img_f, self.bn_f, self.img_d, self.bn_d = img_f, bn_f, img_d, bn_d
+
+
+def _wsplit_run(W, i, j, amax_bufs, M):
+    """Pre-split images of W[i:j] ([n, N, K] fp32 contiguous, the B^T operands of C = A W^T with
+    M rows) in one launch, each scaled by its layer's max|W| (amax_bufs[k, 0]); (images, bn) or
+    (None, 0) when the shape has no pre-split path."""
+    _, N, K = W.shape
+    bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
+    if bn == 0:
+        return None, 0
+    nb = _lib.query("bgnn_gemm_wsplit_bytes", N, K)
+    img = torch.empty(j - i, nb, dtype=torch.uint8, device=W.device)
+    _lib.call("bgnn_gemm_wsplit", W[i].data_ptr(), j - i, W.stride(0), N, K, W.stride(1), amax_bufs[i].data_ptr(),
+              amax_bufs.stride(0), img.data_ptr(), nb, bn, _stream())
+    return img, bn
+
+
+def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax, n_rows: int = 0):
     """[W_l;W_r] and its transpose for every layer of a loop in a few launches (one multi-tensor
     copy into a fresh pack, one transpose, one max|W|
     launch per run of layers that take it) instead of three launches per layer. pairs:
@@ -1037,7 +1090,29 @@ def prepare_weights(pairs, amax_bufs: torch.Tensor, fill_amax):
                 for k in range(i, j):
                     absmax(W[k], amax_bufs[k, 0:1], accumulate=True)
             i = j
-    return [(W[i], Wt[i] if Wt is not None else None) for i in range(L)]
+        out = [WPrep(W[i], Wt[i] if Wt is not None else None) for i in range(L)]
+        # pre-split images (after the maxima they are scaled by): the layers that scale by
+        # max|[W_l;W_r]| (not a folded layer, whose transform is a per-step weight product)
+        if (WSPLIT and n_rows > 0 and GEMM_BACKEND == "hip" and Wt is not None and not Z_PLANES and not DZ_PLANES
+                and amax_bufs.is_contiguous() and _lib.query("bgnn_get_tuning", 5) == 2):
+            i = 0
+            while i < L:
+                if not fill_amax[i]:
+                    i += 1
+                    continue
+                j = i
+                while j < L and fill_amax[j]:
+                    j += 1
+                img_f, bn_f = _wsplit_run(W, i, j, amax_bufs, n_rows)
+                img_d, bn_d = _wsplit_run(Wt, i, j, amax_bufs, n_rows)
+                for k in range(i, j):
+                    o = out[k]
+                    if img_f is not None:
+                        o.img_f, o.bn_f = img_f[k - i], bn_f
+                    if img_d is not None:
+                        o.img_d, o.bn_d = img_d[k - i], bn_d
+                i = j
+    return out
 
 
 def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: torch.Tensor,

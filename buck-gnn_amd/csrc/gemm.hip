@@ -383,7 +383,7 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 using namespace bgnn;
 
 extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
-    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 1100,
+    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 1200,
                  "gemm: config %d out of range", cfg);
     g_gemm_abl = cfg / 100;
     g_gemm_cfg = cfg % 100;
@@ -538,6 +538,46 @@ extern "C" int bgnn_gemm_f32_dropadd(int32_t ta, int32_t tb, int64_t M, int64_t 
                  "gemm_dropadd: built for the f16x3 family (BGNN_TUNE_GEMM_MODE 2) and C = A B^T only");
     return gemm_scaled_impl(ta, tb, M, N, K, 1.f, A, lda, 0, 0, B, ldb, 1.f, C, ldc, 0, 0, nullptr, 0, a_amax,
                             b_amax, nullptr, 0, ws, ws_bytes, stream, BetaSrc{src, ld_src, seed, p});
+}
+
+extern "C" int32_t bgnn_gemm_w_tile(int64_t M, int64_t N, int64_t K) {
+    if (gemm_mode() != 2 || M <= 0 || N <= 0 || K <= 0) return 0;
+    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0);
+    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg < 1 || pl.cfg > 4) return 0;
+    if (N % pl.bn != 0 || K % 32 != 0) return 0;
+    return pl.bn;
+}
+
+// C = A W^T (+ drop(src)) with W given as its pre-split image (bgnn_gemm_wsplit with column tile
+// bn = bgnn_gemm_w_tile(M, N, K)): the f16x3 kernel stages W by LDS-DMA, A as bgnn_gemm_f32_scaled.
+extern "C" int bgnn_gemm_f32_w(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const void* wimg,
+                               int32_t bn, float* C, int64_t ldc, const float* bias, int32_t relu,
+                               const float* a_amax, const float* b_amax, float* c_amax, const float* src,
+                               int64_t ld_src, float p, uint64_t seed, void* stream) {
+    BGNN_REQUIRE(A && wimg && C && a_amax && b_amax, "gemm_f32_w: null pointer");
+    BGNN_REQUIRE(lda >= K && ldc >= N, "gemm_f32_w: bad lda / ldc");
+    if (M == 0 || N == 0) return BGNN_OK;
+    const int32_t tile = bgnn_gemm_w_tile(M, N, K);
+    BGNN_REQUIRE(tile != 0 && tile == bn, "gemm_f32_w: image column tile %d, plan tile %d (bgnn_gemm_w_tile)", bn,
+                 tile);
+    BGNN_REQUIRE(!src || (ld_src >= N && ld_src % 4 == 0 && N % 4 == 0 && ((uintptr_t)src & 15) == 0),
+                 "gemm_f32_w: src must be 16-byte aligned with N and ld_src multiples of 4");
+    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0);
+    GemmArgs g{A, static_cast<const float*>(wimg), C, nullptr, M, N, K, lda, K, ldc, 1.f, src ? 1.f : 0.f, 0, 1,
+               bias, relu, 0, 0, 0, 0, a_amax, b_amax, c_amax};
+    g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;
+    g.wb = 1;
+    if (src) {
+        g.bsrc = src;
+        g.ld_bsrc = ld_src;
+        g.dseed = seed;
+        g.dthr = dropout_threshold(p);
+        g.dkeep = g.dthr ? 1.f / (1.f - p) : 1.f;
+    }
+    const int64_t tiles = ((M + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
+    launch_x6(1, 0, 1, pl.cfg, src ? 8 : 0, dim3((unsigned)tiles, 1), as_stream(stream), g);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
 }
 
 static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,

@@ -35,6 +35,9 @@ struct GemmArgs {
     // bf16-operand family (PREC 2) only: bf16 STORAGE of A (bit 0), B (bit 1), C (bit 2) -- the
     // pointers then address bf16 elements and lda / ldb / ldc count bf16 elements
     int st;
+    // f16x3 C = A B^T only: B points to a pre-split image of B^T (bgnn_gemm_wsplit, column tile =
+    // the launch tile's BN) instead of f32 rows; the kernel stages it by LDS-DMA
+    int wb;
 };
 
 // the beta operand of 4 consecutive columns (col % 4 == 0) of row `row`: masked bsrc

@@ -1,0 +1,778 @@
+// Kernel template of the split-precision GEMMs (see gemm_x6.hip for the numerics and tiling),
+// shared by the translation units that instantiate it (gemm_x6_nt.hip, gemm_x6_nt_abl.hip,
+// gemm_x6_other.hip, gemm_x6_b16s.hip): one TU per instantiation family keeps the build parallel.
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+#include "gemm_common.h"
+#include "gemm_x6.h"
+
+namespace bgnn {
+
+constexpr int X6_BK = 32;
+
+// 16-B chunk index of (row, chunk) in a [R][32]-bf16 image
+__device__ __forceinline__ int x6_pos(int row, int chunk) { return row * 4 + (chunk ^ ((row >> 2) & 3)); }
+
+// One staging unit = 8 consecutive k of one row r (r = m or n) of the tile.
+//   KCONTIG = 1: element (r, k) at P[r * ld + k];   unit idx -> r = idx / 4, chunk = idx % 4
+//   KCONTIG = 0: element (r, k) at P[k * ld + r];   unit idx -> r = idx % R, chunk = idx / R
+// bf16 element e of operand storage P16 (exact in f32)
+__device__ __forceinline__ float bf16_at(const uint16_t* __restrict__ P16, int64_t e) {
+    return __uint_as_float((uint32_t)P16[e] << 16);
+}
+
+// BF: the operand is stored as bf16 (ld in bf16 elements; the EA_GNN edge activations of the
+// bf16 configuration): loaded at half the bytes and widened exactly to f32 in registers.
+template <int KCONTIG, int R, int NT, bool FULL, bool BF = false>
+__device__ __forceinline__ void x6_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0,
+                                        int64_t k0, int64_t kend, bool vec_ok, float (&v)[R * 4 / NT][8], int t) {
+    constexpr int NU = R * 4 / NT;
+    const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int idx = t + NT * u;
+        if constexpr (BF) {
+            if constexpr (KCONTIG) {
+                const int r = idx >> 2, c = idx & 3;
+                const int64_t gr = r0 + r, gk = k0 + c * 8;
+                if (FULL || (vec_ok && gr < Rlim && gk + 7 < kend)) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(P16 + gr * ld + gk);
+                    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        v[u][2 * h] = __uint_as_float(w[h] << 16);
+                        v[u][2 * h + 1] = __uint_as_float(w[h] & 0xffff0000u);
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) v[u][q] = (gr < Rlim && gk + q < kend) ? bf16_at(P16, gr * ld + gk + q) : 0.f;
+                }
+            } else {
+                const int r = idx % R, c = idx / R;
+                const int64_t gr = r0 + r, gk = k0 + c * 8;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    v[u][q] = (FULL || (gr < Rlim && gk + q < kend)) ? bf16_at(P16, (gk + q) * ld + gr) : 0.f;
+            }
+            continue;
+        }
+        if constexpr (KCONTIG) {
+            const int r = idx >> 2, c = idx & 3;
+            const int64_t gr = r0 + r, gk = k0 + c * 8;
+            if (FULL || (vec_ok && gr < Rlim && gk + 7 < kend)) {
+                const float4 a = *reinterpret_cast<const float4*>(P + gr * ld + gk);
+                const float4 b = *reinterpret_cast<const float4*>(P + gr * ld + gk + 4);
+                v[u][0] = a.x; v[u][1] = a.y; v[u][2] = a.z; v[u][3] = a.w;
+                v[u][4] = b.x; v[u][5] = b.y; v[u][6] = b.z; v[u][7] = b.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[u][q] = (gr < Rlim && gk + q < kend) ? P[gr * ld + gk + q] : 0.f;
+            }
+        } else {
+            const int r = idx % R, c = idx / R;
+            const int64_t gr = r0 + r, gk = k0 + c * 8;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                v[u][q] = (FULL || (gr < Rlim && gk + q < kend)) ? P[(gk + q) * ld + gr] : 0.f;
+        }
+    }
+}
+
+// split the staged units and write the piece images (S = piece 0; piece p at S + p*R*4);
+// PREC 1 scales by sc first (exact: a power of two)
+template <int KCONTIG, int R, int NT, int PREC, int ABL = 0>
+__device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)[R * 4 / NT][8], int t, float sc) {
+    constexpr int NU = R * 4 / NT;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int idx = t + NT * u;
+        const int r = KCONTIG ? (idx >> 2) : (idx % R);
+        const int c = KCONTIG ? (idx & 3) : (idx / R);
+        const int pos = x6_pos(r, c);
+        if constexpr (PREC == 2) {   // bf16: one round-to-nearest piece
+            uint4 q0;
+            q0.x = pack_bf16(v[u][0], v[u][1]); q0.y = pack_bf16(v[u][2], v[u][3]);
+            q0.z = pack_bf16(v[u][4], v[u][5]); q0.w = pack_bf16(v[u][6], v[u][7]);
+            S[pos] = q0;
+            continue;
+        }
+        {
+            uint4 q0, q1;
+            if constexpr (ABL == 1) {
+                q0.x = pack_f16(v[u][0], v[u][1]); q0.y = pack_f16(v[u][2], v[u][3]);
+                q0.z = pack_f16(v[u][4], v[u][5]); q0.w = pack_f16(v[u][6], v[u][7]);
+                q1 = q0;
+            } else {
+                split2h(v[u][0] * sc, v[u][1] * sc, q0.x, q1.x);
+                split2h(v[u][2] * sc, v[u][3] * sc, q0.y, q1.y);
+                split2h(v[u][4] * sc, v[u][5] * sc, q0.z, q1.z);
+                split2h(v[u][6] * sc, v[u][7] * sc, q0.w, q1.w);
+            }
+            S[pos] = q0;
+            S[R * 4 + pos] = q1;
+        }
+    }
+}
+
+typedef __attribute__((address_space(3))) void x6_lds_void_t;
+
+// LDS byte address of a __shared__ pointer (the 32-bit address-space-3 offset)
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+    return (uint32_t)(uintptr_t)(const x6_lds_void_t*)p;
+}
+
+// 16 B per lane from `src` into LDS at the wave-uniform byte address lds_dst + 16 * lane
+// (global_load_lds_dwordx4; M0 saved and restored in the statement). Inline asm on purpose:
+// hipcc does not count it, so its counted waits for the register-staged operand stay partial
+// (a compiler-visible LDS-DMA makes it wait vmcnt(0) at every use of a register load); this
+// code waits for it itself (wait_vmcnt_asm) before the barrier that publishes the slot.
+__device__ __forceinline__ void glds16_asm(const void* src, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_asm() {
+    static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Line-major staging of a K-contiguous f32 operand (k_gemm_x6 with PPV bit 1): the staging unit
+// is one float4 (4 consecutive k of one row); lanes 8i..8i+7 of a wave take the 8 float4 of one
+// row's 32-deep slice, so each wave load instruction reads 8 whole 128-B lines (1 KiB) instead of
+// 16 half lines (x6_load's 8-k units: two float4 per lane 16 B apart). Each float4 is split into
+// 4 f16 of each piece and written as half of its 16-B chunk of the same swizzled image
+// (ds_write_b64). Register layout: unit u2 in v[u2 / 2][4 (u2 % 2) .. +3].
+template <int R, int NT, bool FULL>
+__device__ __forceinline__ void lm_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
+                                        int64_t kend, bool vec_ok, float (&v)[R * 4 / NT][8], int t) {
+    constexpr int NU2 = R * 8 / NT;
+#pragma unroll
+    for (int u2 = 0; u2 < NU2; ++u2) {
+        const int idx = t + NT * u2;
+        const int64_t gr = r0 + (idx >> 3), gk = k0 + (idx & 7) * 4;
+        float* d = &v[u2 >> 1][(u2 & 1) * 4];
+        if (FULL || (vec_ok && gr < Rlim && gk + 3 < kend)) {
+            const float4 a = *reinterpret_cast<const float4*>(P + gr * ld + gk);
+            d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d[q] = (gr < Rlim && gk + q < kend) ? P[gr * ld + gk + q] : 0.f;
+        }
+    }
+}
+
+// rows [roff, roff + RH) of an R-row tile image (roff = 0, RH = R: the whole tile)
+template <int RH, int NT, int R>
+__device__ __forceinline__ void lm_store(uint4* __restrict__ S, const float (&v)[RH * 4 / NT][8], int t, float sc,
+                                         int roff) {
+    constexpr int NU2 = RH * 8 / NT;
+    uint2* __restrict__ S2 = reinterpret_cast<uint2*>(S);
+#pragma unroll
+    for (int u2 = 0; u2 < NU2; ++u2) {
+        const int idx = t + NT * u2;
+        const int q = idx & 7;
+        const int pos = 2 * x6_pos(roff + (idx >> 3), q >> 1) + (q & 1);
+        const float* d = &v[u2 >> 1][(u2 & 1) * 4];
+        uint2 h0, h1;
+        split2h(d[0] * sc, d[1] * sc, h0.x, h1.x);
+        split2h(d[2] * sc, d[3] * sc, h0.y, h1.y);
+        S2[pos] = h0;
+        S2[R * 8 + pos] = h1;
+    }
+}
+
+// ping-pong staging (k_gemm_x6 with PPV): one wave group stages the rows [roff, roff + RH) of an
+// R-row operand tile -- the same [piece][row][4 chunks] swizzled image x6_store writes
+template <int RH, int NTG, int R>
+__device__ __forceinline__ void pp_store(uint4* __restrict__ S, const float (&v)[RH * 4 / NTG][8], int t, float sc,
+                                         int roff) {
+    constexpr int NU = RH * 4 / NTG;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int idx = t + NTG * u;
+        const int pos = x6_pos(roff + (idx >> 2), idx & 3);
+        uint4 q0, q1;
+        split2h(v[u][0] * sc, v[u][1] * sc, q0.x, q1.x);
+        split2h(v[u][2] * sc, v[u][3] * sc, q0.y, q1.y);
+        split2h(v[u][4] * sc, v[u][5] * sc, q0.z, q1.z);
+        split2h(v[u][6] * sc, v[u][7] * sc, q0.w, q1.w);
+        S[pos] = q0;
+        S[R * 4 + pos] = q1;
+    }
+}
+
+// k-major quad staging (f16x3, both operands k-major: the weight gradient dW = dZ^T X, whose
+// K is the node dimension). A quad is 4 consecutive rows r x 8 consecutive k of one operand:
+// eight coalesced float4 loads along r (one per k), transposed in registers into four
+// 8-k units, written as the same [row][32 k] swizzled images as the K-contiguous path (so
+// the MFMA reads are unchanged). Quads of A go to threads [0, BM), of B to [BM, BM + BN).
+// Measured (wgrad 1024x512x80656, 256x256 tiles): 804 -> 300 us against per-lane dword loads.
+// KTAIL: rows in range and 16-B aligned, only k may run past kend (the last split-K slab of a
+// K that is no multiple of the slice): float4 loads from row min(k, kend - 1), zeroed past kend.
+template <int R, bool FULL, bool BF = false, bool KTAIL = false>
+__device__ __forceinline__ void kq_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
+                                        int64_t kend, bool vec_ok, float (&v)[4][8], int q) {
+    const int r4 = q % (R / 4), c = q / (R / 4);
+    const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
+    if constexpr (KTAIL && !BF) {
+        if (k0 + X6_BK <= kend) {   // (uniform) every slice but the last: the interior loads
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float4 f = *reinterpret_cast<const float4*>(P + (gk + k) * ld + gr);
+                v[0][k] = f.x; v[1][k] = f.y; v[2][k] = f.z; v[3][k] = f.w;
+            }
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool ok = gk + k < kend;
+            const float4 f = *reinterpret_cast<const float4*>(P + (ok ? gk + k : kend - 1) * ld + gr);
+            v[0][k] = ok ? f.x : 0.f; v[1][k] = ok ? f.y : 0.f; v[2][k] = ok ? f.z : 0.f; v[3][k] = ok ? f.w : 0.f;
+        }
+        return;
+    }
+    if constexpr (BF) {   // bf16 storage: 4 consecutive rows = one 8-B load per k
+        const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
+                const uint2 f = *reinterpret_cast<const uint2*>(P16 + (gk + k) * ld + gr);
+                v[0][k] = __uint_as_float(f.x << 16); v[1][k] = __uint_as_float(f.x & 0xffff0000u);
+                v[2][k] = __uint_as_float(f.y << 16); v[3][k] = __uint_as_float(f.y & 0xffff0000u);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[i][k] = (gr + i < Rlim && gk + k < kend) ? bf16_at(P16, (gk + k) * ld + gr + i) : 0.f;
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
+            const float4 f = *reinterpret_cast<const float4*>(P + (gk + k) * ld + gr);
+            v[0][k] = f.x; v[1][k] = f.y; v[2][k] = f.z; v[3][k] = f.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i][k] = (gr + i < Rlim && gk + k < kend) ? P[(gk + k) * ld + gr + i] : 0.f;
+        }
+    }
+}
+
+template <int R, int PREC>
+__device__ __forceinline__ void kq_store(uint4* __restrict__ S, const float (&v)[4][8], int q, float sc) {
+    const int r4 = q % (R / 4), c = q / (R / 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (PREC == 2) {
+            uint4 q0;
+            q0.x = pack_bf16(v[i][0], v[i][1]); q0.y = pack_bf16(v[i][2], v[i][3]);
+            q0.z = pack_bf16(v[i][4], v[i][5]); q0.w = pack_bf16(v[i][6], v[i][7]);
+            S[x6_pos(4 * r4 + i, c)] = q0;
+            continue;
+        }
+        uint4 q0, q1;
+        split2h(v[i][0] * sc, v[i][1] * sc, q0.x, q1.x);
+        split2h(v[i][2] * sc, v[i][3] * sc, q0.y, q1.y);
+        split2h(v[i][4] * sc, v[i][5] * sc, q0.z, q1.z);
+        split2h(v[i][6] * sc, v[i][7] * sc, q0.w, q1.w);
+        const int pos = x6_pos(4 * r4 + i, c);
+        S[pos] = q0;
+        S[R * 4 + pos] = q1;
+    }
+}
+
+
+
+
+// k-major quads of a bf16-STORED operand kept packed (PREC 2, A and B both bf16: the EA_GNN
+// weight gradient g^T e, K = E): per k one 8-B load of 4 consecutive rows, held as the raw
+// 16-bit pairs (8 VGPRs per quad instead of 32 widened floats), so two register sets fit and
+// the slice pipeline runs at prefetch distance 2. The LDS image is the one kq_store writes
+// (bf16 values are exact, the same bits).
+template <int R, bool FULL>
+__device__ __forceinline__ void kq_load16(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0, int64_t k0,
+                                          int64_t kend, bool vec_ok, uint2 (&f)[8], int q) {
+    const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
+    const int r4 = q % (R / 4), c = q / (R / 4);
+    const int64_t gr = r0 + 4 * r4, gk = k0 + 8 * c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (FULL || (vec_ok && gr + 3 < Rlim && gk + k < kend)) {
+            f[k] = *reinterpret_cast<const uint2*>(P16 + (gk + k) * ld + gr);
+        } else {
+            uint32_t e[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) e[i] = (gr + i < Rlim && gk + k < kend) ? P16[(gk + k) * ld + gr + i] : 0u;
+            f[k] = make_uint2(e[0] | (e[1] << 16), e[2] | (e[3] << 16));
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void kq_store16(uint4* __restrict__ S, const uint2 (&f)[8], int q) {
+    const int r4 = q % (R / 4), c = q / (R / 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = (i < 2) ? f[k].x : f[k].y;
+        uint32_t p[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            p[j] = (i & 1) ? ((w[2 * j] >> 16) | (w[2 * j + 1] & 0xffff0000u))
+                           : ((w[2 * j] & 0xffffu) | (w[2 * j + 1] << 16));
+        S[x6_pos(4 * r4 + i, c)] = make_uint4(p[0], p[1], p[2], p[3]);
+    }
+}
+
+// the leading piece products of one 16-deep k-step, small terms first
+template <int TM, int TN, int PREC, int NP>
+__device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa)[TM][NP],
+                                       const uint4 (&fb)[TN][NP]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            floatx16 t = acc[i][j];
+            if constexpr (PREC == 2) {   // bf16 operands: one product
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[i][0]), as_bf16x8(fb[j][0]), t, 0, 0, 0);
+                continue;
+            }
+            // f16x3: the two cross terms, then the leading product
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+            acc[i][j] = t;
+        }
+}
+
+
+// ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored in
+// every piece slot), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA +
+// barriers), 4 = MFMA + barriers only, 5 = everything but the C stores, 6 = cached C stores,
+// 7 = prefetch distance 1 (one register set) and per-lane dword staging of k-major operands,
+// 9 = no A loads, 10 = no B loads, 11 = no MFMAs (staging, LDS reads, barriers, epilogue).
+// ABL >= 16: not an ablation but the bf16 STORAGE flags ST = ABL - 16 of the bf16-operand family
+// (PREC 2): bit 0 = A, bit 1 = B, bit 2 = C stored as bf16 (EA_GNN's per-edge activations).
+// PPV bit 1: line-major staging loads (lm_load). PPV bit 0: ping-pong main loop (f16x3, A and B
+// K-contiguous): waves 0..NW/2-1 (group 0, rows
+// [0, BM/2) of the tile) and NW/2..NW-1 (group 1, rows [BM/2, BM)) -- one wave of each group per
+// SIMD -- alternate roles every half step: while one group runs the MFMAs of slice k, the other
+// splits its half of slice k+1 (its A rows and half of the B rows) into LDS and issues the loads of
+// slice k+2; a barrier between the halves. The matrix pipe of each SIMD is fed by one group while
+// the other's split VALU, LDS writes and loads run beside it, instead of both waves competing for
+// the pipe and then both staging with the pipe idle.
+template <int PREC, int TA, int TB, int BM, int BN, int WM, int WN, int ABL_ = 0, int PPV = 0>
+__global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
+    constexpr int ST = ABL_ >= 16 ? ABL_ - 16 : 0;
+    constexpr int ABL = ABL_ >= 16 ? 0 : ABL_;
+    constexpr bool A16 = (ST & 1) != 0, B16 = (ST & 2) != 0, C16 = (ST & 4) != 0;
+    static_assert(ST == 0 || PREC == 2, "bf16 storage is for the bf16-operand family only");
+    static_assert(PREC == 1 || PREC == 2, "f16x3 (1) or bf16 operands (2)");
+    constexpr int NT = 64 * WM * WN;
+    constexpr int NP = PREC == 1 ? 2 : 1;   // pieces per operand
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
+    constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
+    static_assert(BM * 4 % NT == 0 && BN * 4 % NT == 0, "staging units must divide evenly");
+    // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
+    // epilogue as one [TM*32][32] f32 stage per wave
+    constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
+    // PPV bit 2: B pre-split (bgnn_gemm_wsplit) and staged by LDS-DMA into a ring of 3 slots
+    constexpr bool kWB = (PPV & 4) != 0;
+    constexpr int TILE_U4 = 2 * A_U4 + (kWB ? 3 : 2) * B_U4, STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
+    static_assert((TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
+    __shared__ uint4 smem[TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4];
+    uint4 (*As)[A_U4] = reinterpret_cast<uint4 (*)[A_U4]>(smem);
+    uint4 (*Bs)[B_U4] = reinterpret_cast<uint4 (*)[B_U4]>(smem + 2 * A_U4);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int t = threadIdx.x;
+    const int64_t ntn = (g.N + BN - 1) / BN;
+    const int64_t ntm = (g.M + BM - 1) / BM;
+    const int tiles = (int)(ntm * ntn);
+    // XCD-aware order over the whole (tile, split) grid: the workgroups one XCD runs take
+    // consecutive tiles of the same K slice, so that slice's operand rows are fetched into
+    // that XCD's L2 once and shared (split-K wgrad: 16 tiles x 16 slices)
+    const int lt_all = xcd_remap(blockIdx.x + tiles * blockIdx.y, tiles * (int)gridDim.y);
+    const int lt = lt_all % tiles, ks = lt_all / tiles;
+    const int64_t tm = lt / ntn, tn = lt % ntn;
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+    const int64_t kb = (int64_t)ks * g.kchunk;
+    const int64_t ke = min(g.K, kb + g.kchunk);
+
+    // vector loads need 16-B aligned rows (bf16 storage: 8 elements; k-major quads: 8 B, 4 elements)
+    const bool a_vec = (((uintptr_t)g.A & 15) == 0) && (g.lda % ((A16 && AK) ? 8 : 4) == 0);
+    const bool b_vec = (((uintptr_t)g.B & 15) == 0) && (g.ldb % ((B16 && BKc) ? 8 : 4) == 0);
+
+    float sa = 1.f, sb = 1.f, ia = 1.f, ib = 1.f;
+    if constexpr (PREC == 1) {
+        h3_scale(*g.a_amax, sa, ia);
+        h3_scale(*g.b_amax, sb, ib);
+    }
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    constexpr bool KQ = !AK && !BKc && PREC >= 1 && ABL != 7 && BM + BN <= NT && BM % 64 == 0 && BN % 64 == 0 &&
+                        BM * BN >= 256 * 128;   // (128x128: measured slower than the dword path)
+    // two register sets for the staged slices: slice kt+1 is split into LDS while slices kt+2
+    // and kt+3 are in flight (prefetch distance 2; ABL 7 = distance 1 for measurement). The
+    // second set fits the VGPR budget only for K-contiguous operands and tiles up to 256x128
+    // (measured: fwd 363 -> 334 us, dgrad 384 -> 322 us at 256x128).
+    // both k-major operands stored bf16: the quads stay packed (kq_load16), two sets fit
+    constexpr bool KQ16 = KQ && A16 && B16 && PREC == 2;
+    constexpr int PF = (ABL == 7 || (BM * BN > 256 * 128 && !KQ16) || (!(AK && BKc) && !KQ)) ? 1 : 2;
+    // k-major quad staging for the weight gradient (both operands k-major, f16x3)
+    struct RegsStd { float a[BM * 4 / NT][8]; float b[BN * 4 / NT][8]; };
+    struct RegsKQ { float q[4][8]; };
+    struct RegsKQ16 { uint2 q[8]; };
+    using Regs = std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ, RegsStd>>;
+    Regs rs[2];
+    const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
+    const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
+    constexpr bool kStage = ABL != 3 && ABL != 4, kLoad = kStage && ABL != 2;
+    // line-major f32 staging (lm_load / lm_store) of K-contiguous f16x3 operands
+    constexpr bool kLM = (PPV & 2) != 0;
+    static_assert(!kLM || (PREC == 1 && AK && BKc && !A16 && !B16 && ABL != 1), "line-major: f16x3, K-contiguous f32");
+    // (s_setprio(1) around the MFMA block, guide T5, measured in round 3 and dropped: fwd 317 ->
+    // 341 us, dgrad 324 -> 359, wgrad 303 -> 406 in an interleaved A/B, profiles/r03_*)
+    // the main loop is instantiated twice (interior tiles without guards, edge tiles with
+    // them) and selected once, so the hot loop carries no per-slice bounds branches
+    // MODE 1 = interior tile, 2 = interior rows / columns with a ragged K range (k-major quads
+    // only), 0 = edge tile (element guards)
+    auto mainloop = [&](auto mode_tag) {
+        constexpr int MODE = decltype(mode_tag)::value;
+        constexpr bool FULL = MODE == 1, KT = MODE == 2;
+        auto load_ab = [&](int64_t k0, Regs& r) {
+            const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
+            if constexpr (KQ16) {
+                if (t < BM) kq_load16<BM, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
+                else if (t < BM + BN) kq_load16<BN, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+            } else if constexpr (KQ) {
+                if (t < BM) kq_load<BM, FULL, A16, KT>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
+                else if (t < BM + BN) kq_load<BN, FULL, B16, KT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+            } else if constexpr (kLM) {
+                lm_load<BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
+                lm_load<BN, NT, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
+            } else {
+                if constexpr (ABL != 9) x6_load<AK, BM, NT, FULL, A16>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
+                if constexpr (ABL != 10) x6_load<BKc, BN, NT, FULL, B16>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
+            }
+        };
+        auto store_ab = [&](int buf, const Regs& r) {
+            if constexpr (KQ16) {
+                if (t < BM) kq_store16<BM>(As[buf], r.q, t);
+                else if (t < BM + BN) kq_store16<BN>(Bs[buf], r.q, t - BM);
+            } else if constexpr (KQ) {
+                if (t < BM) kq_store<BM, PREC>(As[buf], r.q, t, sa);
+                else if (t < BM + BN) kq_store<BN, PREC>(Bs[buf], r.q, t - BM, sb);
+            } else if constexpr (kLM) {
+                lm_store<BM, NT, BM>(As[buf], r.a, t, sa, 0);
+                lm_store<BN, NT, BN>(Bs[buf], r.b, t, sb, 0);
+            } else {
+                x6_store<AK, BM, NT, PREC, ABL>(As[buf], r.a, t, sa);
+                x6_store<BKc, BN, NT, PREC, ABL>(Bs[buf], r.b, t, sb);
+            }
+        };
+        const int li = lane & 31, lh = lane >> 5;
+        auto mma_slice = [&](int cur, int64_t kt) {
+#pragma unroll
+            for (int kk = 0; kk < X6_BK / 16; ++kk) {
+                uint4 a[TM][NP], b[TN][NP];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm * (BM / WM) + i * 32;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        if constexpr (ABL == 4) a[i][p] = make_uint4(row + p, kk, i, (int)kt);
+                        else a[i][p] = As[cur][p * BM * 4 + x6_pos(row + li, 2 * kk + lh)];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn * (BN / WN) + j * 32;
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        if constexpr (ABL == 4) b[j][p] = make_uint4(row - p, kk, j, (int)kt);
+                        else b[j][p] = Bs[cur][p * BN * 4 + x6_pos(row + li, 2 * kk + lh)];
+                    }
+                }
+                if constexpr (ABL != 11) x6_mma<TM, TN, PREC, NP>(acc, a, b);
+                else if (kt < 0) x6_mma<TM, TN, PREC, NP>(acc, a, b);   // (keeps the reads live)
+            }
+        };
+        // one pipeline step: split slice kt+1 (register set S) into LDS buffer (kt+1)&1, refill
+        // set S with slice kt+1+PF, multiply slice kt, barrier. S = (kt+1) & 1 for PF = 2.
+        auto step = [&](int64_t kt, Regs& r) {
+            const int cur = (int)(kt & 1);
+            if (kt + 1 < nk && kStage) store_ab(cur ^ 1, r);
+            if (kt + 1 + PF < nk && kLoad) load_ab(kb + (kt + 1 + PF) * X6_BK, r);
+            // keep the staging (split VALU, LDS writes, global loads) out of the MFMA block
+            __builtin_amdgcn_sched_barrier(0);
+            mma_slice(cur, kt);
+            __syncthreads();
+        };
+        if (nk > 0) {
+            load_ab(kb, rs[0]);
+            store_ab(0, rs[0]);
+            if (nk > 1 && kLoad) load_ab(kb + X6_BK, rs[1]);
+            if (PF == 2 && nk > 2 && kLoad) load_ab(kb + 2 * X6_BK, rs[0]);
+        }
+        __syncthreads();
+        if constexpr (PF == 2) {
+            int64_t kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                step(kt, rs[1]);
+                step(kt + 1, rs[0]);
+            }
+            if (kt < nk) step(kt, rs[1]);
+        } else {
+            for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
+        }
+    };
+    if constexpr (kWB) {
+        // B (the weights, B^T [N][K] K-contiguous) arrives pre-split: per (column tile, 32-deep
+        // slice) the exact [piece][row][4 chunks] swizzled image this kernel would have written,
+        // BN * 128 bytes, copied into a ring of 3 LDS slots by LDS-DMA (no VGPRs, no VALU, no
+        // ds_write; inline asm, so hipcc's vmcnt bookkeeping of the A loads stays its own). A is
+        // register-staged and split as before, two register sets (prefetch distance 2).
+        // Step kt: split A slice kt+1 into As[(kt+1)&1]; DMA B slice kt+2 into slot (kt+2)%3;
+        // load A slice kt+3; MFMAs of slice kt (As[kt&1], slot kt%3); wait for B slice kt+1; barrier.
+        static_assert(PREC == 1 && AK && BKc && !A16 && !B16 && (PPV & 3) == 0, "pre-split B: f16x3 NT only");
+        constexpr int NW = WM * WN;
+        constexpr int SLICE_B = BN * 128;
+        constexpr int GPW = SLICE_B / (NW * 1024);   // LDS-DMA instructions per wave and slice
+        static_assert(GPW * NW * 1024 == SLICE_B, "B slice must split into whole 1-KiB wave copies");
+        constexpr int NA = BM * 4 / NT;                 // A staging units (8 k) per thread
+        float va[2][NA][8];
+        const int64_t nks = g.K / X6_BK;
+        const char* bsrc = reinterpret_cast<const char*>(g.B) + (int64_t)tn * nks * SLICE_B +
+                           (int64_t)(wave * GPW) * 1024 + lane * 16;
+        const uint32_t bdst = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)(lds_u32(&Bs[0][0]) + (uint32_t)(wave * GPW * 1024)));
+        auto glds_b = [&](int64_t sl) {   // slice sl (kb == 0: no split-K) -> slot sl % 3
+            const char* src = bsrc + sl * SLICE_B;
+            const uint32_t dst = bdst + (uint32_t)((sl % 3) * SLICE_B);
+#pragma unroll
+            for (int q = 0; q < GPW; ++q) glds16_asm(src + q * 1024, dst + q * 1024);
+        };
+        auto wb_loop = [&](auto mode_tag) {
+            constexpr bool FULL = decltype(mode_tag)::value == 1;
+            auto load_a = [&](int64_t k0, float (&v)[NA][8]) {
+                if constexpr (kLoad) {
+                    const float* Ab = plane_base(g.A, k0, g.a_blk, g.a_pstride);
+                    x6_load<1, BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, v, t);
+                }
+            };
+            auto store_a = [&](int buf, const float (&v)[NA][8]) {
+                if constexpr (kStage) x6_store<1, BM, NT, PREC, ABL>(As[buf], v, t, sa);
+            };
+            const int li = lane & 31, lh = lane >> 5;
+            auto mma = [&](int abuf, int bslot) {
+                const uint4* __restrict__ Ac = As[abuf];
+                const uint4* __restrict__ Bc = Bs[bslot];
+#pragma unroll
+                for (int kk = 0; kk < X6_BK / 16; ++kk) {
+                    uint4 a[TM][NP], b[TN][NP];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            a[i][p] = Ac[p * BM * 4 + x6_pos(wm * (BM / WM) + i * 32 + li, 2 * kk + lh)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            b[j][p] = Bc[p * BN * 4 + x6_pos(wn * (BN / WN) + j * 32 + li, 2 * kk + lh)];
+                    x6_mma<TM, TN, PREC, NP>(acc, a, b);
+                }
+            };
+            if (nk > 0) {
+                glds_b(0);
+                if (nk > 1) glds_b(1);
+                load_a(kb, va[0]);
+                if (nk > 1) load_a(kb + X6_BK, va[1]);
+                store_a(0, va[0]);
+                if (nk > 2) load_a(kb + 2 * X6_BK, va[0]);
+            }
+            wait_vmcnt_asm<0>();   // (prologue: slice 0's B landed)
+            __syncthreads();
+            for (int64_t kt = 0; kt < nk; ++kt) {
+                const int cur = (int)(kt & 1);
+                if (kt + 1 < nk) store_a(cur ^ 1, va[cur ^ 1]);
+                if (kt + 2 < nk) glds_b(kt + 2);
+                if (kt + 3 < nk) load_a(kb + (kt + 3) * X6_BK, va[cur ^ 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(cur, (int)(kt % 3));
+                // B slice kt+1 (issued at step kt-1) landed: younger are A slice kt+2 (step kt-1),
+                // B slice kt+2 and A slice kt+3 (this step) -- a lower bound of the instructions
+                if (kt + 3 < nk) wait_vmcnt_asm<4 * NA + GPW>();
+                else wait_vmcnt_asm<0>();
+                __builtin_amdgcn_s_barrier();
+            }
+        };
+        if (full) wb_loop(std::integral_constant<int, 1>{});
+        else wb_loop(std::integral_constant<int, 0>{});
+    } else if constexpr ((PPV & 1) != 0) {
+        static_assert(PREC == 1 && AK && BKc && ABL != 7, "ping-pong: f16x3 with K-contiguous A and B");
+        constexpr int NTG = NT / 2, RA = BM / 2, RB = BN / 2;
+        static_assert(RA * 4 % NTG == 0 && RB * 4 % NTG == 0 && (WM * WN) % 2 == 0 && (WM % 2 == 0 || WM == 1),
+                      "ping-pong: each group stages whole units and owns half of the tile's wave rows");
+        const int grp = wave >= (WM * WN) / 2;
+        const int tg = t - grp * NTG;
+        float va[RA * 4 / NTG][8], vb[RB * 4 / NTG][8];
+        auto pp_loop = [&](auto mode_tag) {
+            constexpr bool FULL = decltype(mode_tag)::value == 1;
+            auto load = [&](int64_t k0) {
+                if constexpr (kLoad) {
+                    const float* Ab = plane_base(g.A, k0, g.a_blk, g.a_pstride);
+                    if constexpr (kLM) {
+                        lm_load<RA, NTG, FULL>(Ab, g.lda, g.M, m0 + grp * RA, k0, ke, a_vec, va, tg);
+                        lm_load<RB, NTG, FULL>(g.B, g.ldb, g.N, n0 + grp * RB, k0, ke, b_vec, vb, tg);
+                    } else {
+                        x6_load<1, RA, NTG, FULL>(Ab, g.lda, g.M, m0 + grp * RA, k0, ke, a_vec, va, tg);
+                        x6_load<1, RB, NTG, FULL>(g.B, g.ldb, g.N, n0 + grp * RB, k0, ke, b_vec, vb, tg);
+                    }
+                }
+            };
+            auto store = [&](int buf) {
+                if constexpr (kStage) {
+                    if constexpr (kLM) {
+                        lm_store<RA, NTG, BM>(As[buf], va, tg, sa, grp * RA);
+                        lm_store<RB, NTG, BN>(Bs[buf], vb, tg, sb, grp * RB);
+                    } else {
+                        pp_store<RA, NTG, BM>(As[buf], va, tg, sa, grp * RA);
+                        pp_store<RB, NTG, BN>(Bs[buf], vb, tg, sb, grp * RB);
+                    }
+                }
+            };
+            const int li = lane & 31, lh = lane >> 5;
+            auto mma = [&](int cur) {
+#pragma unroll
+                for (int kk = 0; kk < X6_BK / 16; ++kk) {
+                    uint4 a[TM][NP], b[TN][NP];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            a[i][p] = As[cur][p * BM * 4 + x6_pos(wm * (BM / WM) + i * 32 + li, 2 * kk + lh)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            b[j][p] = Bs[cur][p * BN * 4 + x6_pos(wn * (BN / WN) + j * 32 + li, 2 * kk + lh)];
+                    x6_mma<TM, TN, PREC, NP>(acc, a, b);
+                }
+            };
+            auto stage = [&](int64_t kt) {   // split slice kt+1 into the other buffer, load slice kt+2
+                if (kt + 1 < nk) {
+                    store((int)((kt + 1) & 1));
+                    if (kt + 2 < nk) load(kb + (kt + 2) * X6_BK);
+                }
+            };
+            if (nk > 0) {
+                load(kb);
+                store(0);
+                if (nk > 1) load(kb + X6_BK);
+            }
+            __syncthreads();
+            for (int64_t kt = 0; kt < nk; ++kt) {
+                const int cur = (int)(kt & 1);
+                if (grp == 0) mma(cur);
+                else stage(kt);
+                __syncthreads();
+                if (grp == 0) stage(kt);
+                else mma(cur);
+                __syncthreads();
+            }
+        };
+        if (full) pp_loop(std::integral_constant<int, 1>{});
+        else pp_loop(std::integral_constant<int, 0>{});
+    } else if (full) {
+        mainloop(std::integral_constant<int, 1>{});
+    } else {
+        // the last split-K slab of the weight gradient (K = the node count, rarely a multiple of
+        // 32): interior rows and columns, only k ragged -- the guarded edge loop would set the
+        // whole kernel's time (one round of workgroups: 413 vs 280 us at K = 80,656 vs 80,640)
+        bool ktail = false;
+        if constexpr (KQ && !A16 && !B16)
+            ktail = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && (g.lda % 4 == 0) && (g.ldb % 4 == 0);
+        if constexpr (KQ && !A16 && !B16) {
+            if (ktail) mainloop(std::integral_constant<int, 2>{});
+            else mainloop(std::integral_constant<int, 0>{});
+        } else {
+            mainloop(std::integral_constant<int, 0>{});
+        }
+    }
+    // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
+    float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
+    x6_epilogue<TM, TN, ABL, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
+}
+
+template <int PREC, int TA, int TB, int ABL>
+inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if constexpr (PREC == 1 && TA == 0 && TB == 1 && (ABL == 0 || ABL == 8)) {
+        if (g.wb) {   // pre-split B image (bgnn_gemm_f32_w): tiles with BN = the image's column tile
+            switch (cfg) {
+                case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;
+                case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
+                case 3: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
+                default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;
+            }
+        }
+    }
+    if constexpr (PREC == 1 && TA == 0 && TB == 1 && (ABL == 0 || ABL == 8 || (ABL >= 2 && ABL <= 5))) {
+        const int ppv = gemm_pp();
+        if (ppv >= 1 && ppv <= 3) {
+#define BGNN_PPV(V)                                                                                                  \
+    switch (cfg) {                                                                                                   \
+        case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, V>), grid, dim3(512), 0, s, g); return; \
+        case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, V>), grid, dim3(512), 0, s, g); return; \
+        case 3: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL, V>), grid, dim3(512), 0, s, g); return; \
+        case 4: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, V>), grid, dim3(512), 0, s, g); return; \
+        default: break;                                                                                              \
+    }
+            if (ppv == 1) { BGNN_PPV(1) }
+            else if (ppv == 2) { BGNN_PPV(2) }
+            else { BGNN_PPV(3) }
+#undef BGNN_PPV
+        }
+    }
+    // 256x256 tiles (cfg 3, 4): f16x3 and bf16 (one or two pieces fit the LDS; bf16x6's three do
+    // not, make_plan never picks them for it). The tile here must be the plan's tile
+    // (bgnn_gemm_f32_scaled sizes the grid from it).
+    if constexpr (PREC >= 1) {
+        if (cfg == 3) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); return; }
+        if (cfg == 4) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL>), grid, dim3(512), 0, s, g); return; }
+    }
+    switch (cfg) {
+        case 0: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 128, 2, 2, ABL>), grid, dim3(256), 0, s, g); break;
+        case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); break;
+        default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL>), grid, dim3(512), 0, s, g); break;
+    }
+}
+
+
+// per-family launchers (one translation unit each)
+void launch_x6_nt_main(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);    // gemm_x6_nt.hip
+void launch_x6_nt_abl(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);     // gemm_x6_nt_abl.hip
+void launch_x6_h3_other(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);  // _other
+void launch_x6_prec2(int ta, int tb, int cfg, dim3 grid, hipStream_t s, const GemmArgs& g);        // _b16s
+void launch_x6_bf16_storage(int ta, int tb, int cfg, int st, dim3 grid, hipStream_t s, const GemmArgs& g);
+
+}  // namespace bgnn

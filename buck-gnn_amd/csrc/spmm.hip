@@ -1222,6 +1222,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
         case BGNN_TUNE_ROWS_REV: return rows_rev();
+        case BGNN_TUNE_GEMM_PP: return gemm_pp();
         default: return -1;
     }
 }
@@ -1248,6 +1249,10 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
+        case BGNN_TUNE_GEMM_PP:
+            BGNN_REQUIRE(value >= 0 && value <= 3, "set_tuning: gemm staging variant must be 0..3");
+            set_gemm_pp(value);
+            return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value == 0 || value == 2, "set_tuning: gemm mode must be 0 (f32 MFMA) or 2 (f16x3)");
             set_gemm_mode(value);

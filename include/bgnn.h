@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 9
+#define BGNN_ABI_VERSION 10
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -82,6 +82,11 @@ const char* bgnn_last_error_string(void);
                                     rounding (the order of the dh bias partials / of the
                                     BatchNorm statistics sums; deterministic either way).
                                     Default 1 (measured: bits 1-3 gain nothing)              */
+#define BGNN_TUNE_GEMM_PP 14  /* f16x3 GEMMs with K-contiguous f32 operands (measurement): bit 0
+                                    = ping-pong main loop (the two waves of a SIMD alternate MFMA
+                                    and staging half steps), bit 1 = line-major staging loads
+                                    (whole 128-B lines per wave load); 0 = neither (default:
+                                    both measured slower, profiles/r05_ab_gemm_*). Bit-identical. */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose
@@ -388,6 +393,29 @@ int bgnn_gemm_f32_dropadd(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N
                           const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                           const float* a_amax, const float* b_amax, const float* src, int64_t ld_src,
                           float p, uint64_t seed, void* ws, size_t ws_bytes, void* stream);
+/* Pre-split weights (round 5). The f16x3 GEMM C = A W^T of the SAGE layers (forward z = x
+ * [W_l;W_r]^T, input gradient dx = dz [W_l;W_r]) takes its weight operand W [N, K] as a
+ * pre-split image: W scaled by the power of two of max|W| (amax) and split into two f16 pieces
+ * once per step (bgnn_gemm_wsplit, n_items matrices of one shape in one launch: W_i at W + i *
+ * item_stride, max|W_i| at amax[i * amax_stride], image i at img + i * img_stride bytes), stored
+ * per (column tile of bn rows, 32-deep K slice) as the GEMM's own LDS image, so the GEMM copies
+ * it into LDS by LDS-DMA instead of loading, splitting and storing it in every row tile. The
+ * product is bit-identical to bgnn_gemm_f32_scaled / bgnn_gemm_f32_dropadd on the same operands.
+ *   bgnn_gemm_w_tile(M, N, K): the column tile bn the image must use for that GEMM shape, or 0
+ *     when the shape has no pre-split path (then use bgnn_gemm_f32_scaled);
+ *   bgnn_gemm_wsplit_bytes(N, K): bytes of one image (N % bn == 0, K % 32 == 0);
+ *   bgnn_gemm_f32_w: C = A W^T (+ bias, ReLU, max|C| into c_amax) or, with src != NULL, the
+ *     drop-add epilogue of bgnn_gemm_f32_dropadd (C = A W^T + drop(src)); a_amax / b_amax are
+ *     max|A| and the max|W| the image was split with. */
+int32_t bgnn_gemm_w_tile(int64_t M, int64_t N, int64_t K);
+size_t bgnn_gemm_wsplit_bytes(int64_t N, int64_t K);
+int bgnn_gemm_wsplit(const float* W, int32_t n_items, int64_t item_stride, int64_t N, int64_t K, int64_t ldw,
+                     const float* amax, int64_t amax_stride, void* img, int64_t img_stride, int32_t bn,
+                     void* stream);
+int bgnn_gemm_f32_w(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const void* wimg, int32_t bn,
+                    float* C, int64_t ldc, const float* bias, int32_t relu, const float* a_amax,
+                    const float* b_amax, float* c_amax, const float* src, int64_t ld_src, float p, uint64_t seed,
+                    void* stream);
 size_t bgnn_gemm_ws_bytes_ex(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b,
                              int32_t precision);
 /* C = act(op(A) op(B) + bias + add0[idx0[r], :] (+ add1[idx1[r], :])) -- gathered row adds

@@ -219,3 +219,70 @@ def test_gemm_bf16_precision(dev, ta, tb, mnk):
     B = B.t() if tb else B
     r, mag = A @ B, A.abs() @ B.abs()
     assert ((c.double().cpu() - r).abs() / mag).max().item() < 2e-6
+
+
+def _wsplit(w, w_amax, M):
+    """Pre-split image of the weight operand W [N, K] for the C = A W^T shape (M, N, K)."""
+    N, K = w.shape
+    bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
+    assert bn in (128, 256), (M, N, K, bn)
+    img = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=w.device)
+    _lib.call("bgnn_gemm_wsplit", w.data_ptr(), 1, 0, N, K, w.stride(0), w_amax.data_ptr(), 0, img.data_ptr(),
+              img.numel(), bn, fused._stream())
+    return img, bn
+
+
+# the SAGE layer shapes (forward, input gradient, the folded layer's K = 128 / N = 128 forms) with a
+# ragged last row tile (M % BM != 0), and a small M
+@pytest.mark.parametrize("M,N,K", [(80656, 1024, 512), (80656, 512, 1024), (80656, 1024, 128), (80656, 128, 1024),
+                                   (1000, 512, 1024), (4097, 1024, 512)])
+@pytest.mark.parametrize("dropadd", [False, True])
+def test_gemm_presplit_weights_bit_identical(dev, M, N, K, dropadd):
+    """bgnn_gemm_wsplit + bgnn_gemm_f32_w (the weight operand pre-split once and staged by LDS-DMA)
+    produce exactly the bits of bgnn_gemm_f32_scaled / bgnn_gemm_f32_dropadd on the same operands
+    and maxima (the LDS image is the one the register-staged kernel writes), with bias, ReLU and
+    max|C| in the plain epilogue and the masked beta source in the drop-add epilogue."""
+    if _lib.query("bgnn_gemm_w_tile", M, N, K) == 0:
+        pytest.skip("no pre-split path for this shape")
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) * 0.03
+    am = torch.stack([a.abs().max(), w.abs().max()]).contiguous()
+    img, bn = _wsplit(w, am[1:2], M)
+    if dropadd:
+        src = torch.randn(M, N, device=dev)
+        ref = torch.empty(M, N, device=dev)
+        ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, 0, 1, 0)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M, N, K, a.data_ptr(), K, w.data_ptr(), K, ref.data_ptr(), N,
+                  am[0:1].data_ptr(), am[1:2].data_ptr(), src.data_ptr(), N, 0.1, 1234, ws.data_ptr(), ws_bytes,
+                  fused._stream())
+        out = torch.full((M, N), float("nan"), device=dev)
+        _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N, None, 0,
+                  am[0:1].data_ptr(), am[1:2].data_ptr(), None, src.data_ptr(), N, 0.1, 1234, fused._stream())
+        assert torch.equal(out, ref)
+        return
+    bias = torch.randn(N, device=dev)
+    ca_ref = torch.zeros(1, device=dev)
+    ref = fused.gemm(a, w, False, True, bias=bias, relu=True, a_amax=am[0:1], b_amax=am[1:2], c_amax=ca_ref)
+    out = torch.full((M, N), float("nan"), device=dev)
+    ca = torch.zeros(1, device=dev)
+    _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N, bias.data_ptr(), 1,
+              am[0:1].data_ptr(), am[1:2].data_ptr(), ca.data_ptr(), None, 0, 0.0, 0, fused._stream())
+    assert torch.equal(out, ref)
+    assert torch.equal(ca, ca_ref)
+
+
+def test_gemm_presplit_rejects_mismatched_tile(dev):
+    """An image split with the wrong column tile is refused (no silent misread)."""
+    M, N, K = 80656, 512, 1024
+    w = torch.randn(N, K, device=dev)
+    am = w.abs().max().view(1)
+    bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
+    wrong = 128 if bn == 256 else 256
+    img = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
+    a = torch.randn(M, K, device=dev)
+    out = torch.empty(M, N, device=dev)
+    with pytest.raises(_lib.BgnnError):
+        _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), wrong, out.data_ptr(), N, None, 0,
+                  am.data_ptr(), am.data_ptr(), None, None, 0, 0.0, 0, fused._stream())

@@ -85,7 +85,7 @@ VARIANTS = ["GraphSage_addAggr", "GraphSage_sumAggr", "GraphSage_meanAggr", "Gra
 def test_state_dict_layout_matches_reference(name, hidden):
     """The reference's BuckGNN (imported unchanged through bgnn's PyG shim) and bgnn.BuckGNN
     have identical state-dict keys and shapes, so checkpoints load both ways."""
-    bgnn.install_pyg_shim()
+    bgnn.install_pyg_shim(batchnorm=False, fused_model=False)
     sys.path.insert(0, REF)
     try:
         from Models.BuckGNN import BuckGNN as RefBuckGNN
@@ -162,9 +162,10 @@ def test_relu_mask_matches_reference_form():
     assert torch.equal(torch.ops.aten.threshold_backward(g, out, 0.0), g * (out > 0))
 
 
-def test_pyg_shim_batchnorm_opt_in_patches_and_restores():
-    """install_pyg_shim(batchnorm=True) makes torch.nn.BatchNorm1d bgnn's subclass (same state-dict
-    keys) for modules built while it is installed; uninstall restores torch's class."""
+def test_pyg_shim_batchnorm_patches_and_restores():
+    """install_pyg_shim() (batchnorm=True, the default since round 5) makes torch.nn.BatchNorm1d
+    bgnn's subclass (same state-dict keys) for modules built while it is installed; uninstall
+    restores torch's class."""
     import torch
     import bgnn
     from bgnn import nn as bnn
@@ -179,3 +180,42 @@ def test_pyg_shim_batchnorm_opt_in_patches_and_restores():
     finally:
         bgnn.uninstall_pyg_shim()
     assert torch.nn.BatchNorm1d is orig
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="needs the reference checkout")
+def test_pyg_shim_binds_fused_model_class():
+    """install_pyg_shim()'s import hook: the reference's unchanged Models/BuckGNN.py, imported the way
+    TRAIN_FINAL.py / INFERENCE.py import it, exports bgnn.BuckGNN as BuckGNN (same constructor and
+    state-dict keys as the reference class, kept as BuckGNN_reference); a module imported before the
+    shim is rebound in place; uninstall restores the reference class."""
+    for k in [k for k in sys.modules if k == "Models" or k.startswith("Models.")]:
+        del sys.modules[k]
+    sys.path.insert(0, REF)
+    try:
+        bgnn.install_pyg_shim(batchnorm=False)
+        try:
+            from Models.BuckGNN import BuckGNN
+            import Models.BuckGNN as M
+            assert BuckGNN is bgnn.BuckGNN and M.BuckGNN is bgnn.BuckGNN
+            ref_cls = M.BuckGNN_reference
+            assert ref_cls is not bgnn.BuckGNN and ref_cls.__module__ == "Models.BuckGNN"
+            kw = dict(hidden_channels=64, num_layers=6, pooling_layer="mean", dropout_rate=0.1,
+                      model_name="GraphSage_addAggr_Shared")
+            assert list(BuckGNN(16, 5, **kw).state_dict()) == list(ref_cls(16, 5, **kw).state_dict())
+        finally:
+            bgnn.uninstall_pyg_shim()
+        assert M.BuckGNN is ref_cls
+        # imported first (with the shim's PyG modules but without the hook), then rebound in place
+        bgnn.install_pyg_shim(batchnorm=False, fused_model=False)
+        assert sys.modules["Models.BuckGNN"].BuckGNN is ref_cls
+        bgnn.uninstall_pyg_shim()
+        bgnn.install_pyg_shim(batchnorm=False)
+        try:
+            assert sys.modules["Models.BuckGNN"].BuckGNN is bgnn.BuckGNN
+        finally:
+            bgnn.uninstall_pyg_shim()
+        assert sys.modules["Models.BuckGNN"].BuckGNN is ref_cls
+    finally:
+        sys.path.remove(REF)
+        for k in [k for k in sys.modules if k == "Models" or k.startswith("Models.")]:
+            del sys.modules[k]

@@ -6,7 +6,9 @@ with a 1 GiB cache flush between launches (cold L2 / Infinity Cache, as inside a
     python tools/gemm_ab.py [--reps 20] [--variants=x-1,x2,x102] [--shapes fwd,dgrad]
 
 A variant "xC" runs tile config C % 100 with timing ablation C // 100 (bgnn_gemm_set_cfg; x-1 =
-the automatic plan); "wN" the pre-split-weight kernel family with variant N (bgnn_gemm_w_variant).
+the automatic plan); "pC" the same with the ping-pong main loop (BGNN_TUNE_GEMM_PP = 1), "lC" with
+line-major staging loads (2), "qC" with both (3); "w" the pre-split weight path (bgnn_gemm_wsplit +
+bgnn_gemm_f32_w, LDS-DMA staging of the weight operand).
 """
 import argparse
 import os
@@ -19,7 +21,7 @@ import torch  # noqa: E402
 from bgnn import _lib, fused  # noqa: E402
 
 SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872, 512, 512),
-          "fwd_small": (10082, 1024, 512)}
+          "fwd_small": (10082, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
 
 
 def main():
@@ -40,16 +42,29 @@ def main():
         out = torch.empty(M, N, device=dev)
         ref = None
         for vs in args.variants.split(","):
-            _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if vs.startswith("x") else -1)
-            if hasattr(_lib, "has") and _lib.has("bgnn_gemm_w_variant"):
-                _lib.call("bgnn_gemm_w_variant", int(vs[1:]) if vs.startswith("w") else -1)
+            wimg = None
+            if vs[0] == "w":   # pre-split weight image + bgnn_gemm_f32_w
+                _lib.call("bgnn_gemm_set_cfg", -1)
+                _lib.call("bgnn_set_tuning", 14, 0)
+                bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
+                wimg = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
+                _lib.call("bgnn_gemm_wsplit", b.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, wimg.data_ptr(),
+                          wimg.numel(), bn, fused._stream())
+            else:
+                _lib.call("bgnn_gemm_set_cfg", int(vs[1:]))
+                _lib.call("bgnn_set_tuning", 14, {"x": 0, "p": 1, "l": 2, "q": 3}[vs[0]])   # BGNN_TUNE_GEMM_PP
             ts = []
             for i in range(args.reps + 3):
                 if flush is not None:
                     flush.fill_(float(i))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
+                if wimg is not None:
+                    _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, wimg.data_ptr(), bn, out.data_ptr(), N,
+                              None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None, None, 0, 0.0, 0,
+                              fused._stream())
+                else:
+                    fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 e1.record()
                 ts.append((e0, e1))
             torch.cuda.synchronize()
@@ -62,6 +77,7 @@ def main():
             print(f"{name:9s} {M}x{N}x{K} staging {vs:>3s}: median {med:7.1f} us  min {us[0]:7.1f}  "
                   f"{2 * M * N * K / med / 1e6:6.1f} TF  {same}", flush=True)
         _lib.call("bgnn_gemm_set_cfg", -1)
+        _lib.call("bgnn_set_tuning", 14, 0)
 
 
 if __name__ == "__main__":
