@@ -116,32 +116,6 @@ __device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)
     }
 }
 
-typedef __attribute__((address_space(3))) void x6_lds_void_t;
-
-// LDS byte address of a __shared__ pointer (the 32-bit address-space-3 offset)
-__device__ __forceinline__ uint32_t lds_u32(const void* p) {
-    return (uint32_t)(uintptr_t)(const x6_lds_void_t*)p;
-}
-
-// 16 B per lane from `src` into LDS at the wave-uniform byte address lds_dst + 16 * lane
-// (global_load_lds_dwordx4; M0 saved and restored in the statement). Inline asm on purpose:
-// hipcc does not count it, so its counted waits for the register-staged operand stay partial
-// (a compiler-visible LDS-DMA makes it wait vmcnt(0) at every use of a register load); this
-// code waits for it itself (wait_vmcnt_asm) before the barrier that publishes the slot.
-__device__ __forceinline__ void glds16_asm(const void* src, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds_dst)
-                 : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_asm() {
-    static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // Line-major staging of a K-contiguous f32 operand (k_gemm_x6 with PPV bit 1): the staging unit
 // is one float4 (4 consecutive k of one row); lanes 8i..8i+7 of a wave take the 8 float4 of one
 // row's 32-deep slice, so each wave load instruction reads 8 whole 128-B lines (1 KiB) instead of
@@ -385,9 +359,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
     // epilogue as one [TM*32][32] f32 stage per wave
     constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
-    // PPV bit 2: B pre-split (bgnn_gemm_wsplit) and staged by LDS-DMA into a ring of 3 slots
+    // PPV bit 2: B arrives pre-split (bgnn_gemm_wsplit): its LDS image is copied, not split
     constexpr bool kWB = (PPV & 4) != 0;
-    constexpr int TILE_U4 = 2 * A_U4 + (kWB ? 3 : 2) * B_U4, STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
+    constexpr int TILE_U4 = 2 * (A_U4 + B_U4), STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
     static_assert((TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
     __shared__ uint4 smem[TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4];
     uint4 (*As)[A_U4] = reinterpret_cast<uint4 (*)[A_U4]>(smem);
@@ -437,11 +411,16 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // both k-major operands stored bf16: the quads stay packed (kq_load16), two sets fit
     constexpr bool KQ16 = KQ && A16 && B16 && PREC == 2;
     constexpr int PF = (ABL == 7 || (BM * BN > 256 * 128 && !KQ16) || (!(AK && BKc) && !KQ)) ? 1 : 2;
+    static_assert(!kWB || (PREC == 1 && AK && BKc && !A16 && !B16 && (PPV & 3) == 0 && (BN * 8) % NT == 0),
+                  "pre-split B: f16x3 NT, whole 16-B pieces per thread");
     // k-major quad staging for the weight gradient (both operands k-major, f16x3)
     struct RegsStd { float a[BM * 4 / NT][8]; float b[BN * 4 / NT][8]; };
+    // pre-split B (kWB): per thread BN * 8 / NT 16-B pieces of the slice's image, copied to LDS as is
+    struct RegsWB { float a[BM * 4 / NT][8]; uint4 b[BN * 8 / NT]; };
     struct RegsKQ { float q[4][8]; };
     struct RegsKQ16 { uint2 q[8]; };
-    using Regs = std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ, RegsStd>>;
+    using Regs = std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ,
+                                    std::conditional_t<kWB, RegsWB, RegsStd>>>;
     Regs rs[2];
     const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
@@ -466,6 +445,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             } else if constexpr (KQ) {
                 if (t < BM) kq_load<BM, FULL, A16, KT>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
                 else if (t < BM + BN) kq_load<BN, FULL, B16, KT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
+            } else if constexpr (kWB) {   // B: the image of slice k0 / 32 of column tile tn
+                x6_load<1, BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
+                const uint4* img = reinterpret_cast<const uint4*>(g.B) + (tn * (g.K / X6_BK) + k0 / X6_BK) * (BN * 8);
+#pragma unroll
+                for (int q = 0; q < BN * 8 / NT; ++q) r.b[q] = img[t + NT * q];
             } else if constexpr (kLM) {
                 lm_load<BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
                 lm_load<BN, NT, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.b, t);
@@ -481,6 +465,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             } else if constexpr (KQ) {
                 if (t < BM) kq_store<BM, PREC>(As[buf], r.q, t, sa);
                 else if (t < BM + BN) kq_store<BN, PREC>(Bs[buf], r.q, t - BM, sb);
+            } else if constexpr (kWB) {
+                x6_store<1, BM, NT, PREC, ABL>(As[buf], r.a, t, sa);
+#pragma unroll
+                for (int q = 0; q < BN * 8 / NT; ++q) Bs[buf][t + NT * q] = r.b[q];
             } else if constexpr (kLM) {
                 lm_store<BM, NT, BM>(As[buf], r.a, t, sa, 0);
                 lm_store<BN, NT, BN>(Bs[buf], r.b, t, sb, 0);
@@ -545,90 +533,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
         }
     };
-    if constexpr (kWB) {
-        // B (the weights, B^T [N][K] K-contiguous) arrives pre-split: per (column tile, 32-deep
-        // slice) the exact [piece][row][4 chunks] swizzled image this kernel would have written,
-        // BN * 128 bytes, copied into a ring of 3 LDS slots by LDS-DMA (no VGPRs, no VALU, no
-        // ds_write; inline asm, so hipcc's vmcnt bookkeeping of the A loads stays its own). A is
-        // register-staged and split as before, two register sets (prefetch distance 2).
-        // Step kt: split A slice kt+1 into As[(kt+1)&1]; DMA B slice kt+2 into slot (kt+2)%3;
-        // load A slice kt+3; MFMAs of slice kt (As[kt&1], slot kt%3); wait for B slice kt+1; barrier.
-        static_assert(PREC == 1 && AK && BKc && !A16 && !B16 && (PPV & 3) == 0, "pre-split B: f16x3 NT only");
-        constexpr int NW = WM * WN;
-        constexpr int SLICE_B = BN * 128;
-        constexpr int GPW = SLICE_B / (NW * 1024);   // LDS-DMA instructions per wave and slice
-        static_assert(GPW * NW * 1024 == SLICE_B, "B slice must split into whole 1-KiB wave copies");
-        constexpr int NA = BM * 4 / NT;                 // A staging units (8 k) per thread
-        float va[2][NA][8];
-        const int64_t nks = g.K / X6_BK;
-        const char* bsrc = reinterpret_cast<const char*>(g.B) + (int64_t)tn * nks * SLICE_B +
-                           (int64_t)(wave * GPW) * 1024 + lane * 16;
-        const uint32_t bdst = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)(lds_u32(&Bs[0][0]) + (uint32_t)(wave * GPW * 1024)));
-        auto glds_b = [&](int64_t sl) {   // slice sl (kb == 0: no split-K) -> slot sl % 3
-            const char* src = bsrc + sl * SLICE_B;
-            const uint32_t dst = bdst + (uint32_t)((sl % 3) * SLICE_B);
-#pragma unroll
-            for (int q = 0; q < GPW; ++q) glds16_asm(src + q * 1024, dst + q * 1024);
-        };
-        auto wb_loop = [&](auto mode_tag) {
-            constexpr bool FULL = decltype(mode_tag)::value == 1;
-            auto load_a = [&](int64_t k0, float (&v)[NA][8]) {
-                if constexpr (kLoad) {
-                    const float* Ab = plane_base(g.A, k0, g.a_blk, g.a_pstride);
-                    x6_load<1, BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, v, t);
-                }
-            };
-            auto store_a = [&](int buf, const float (&v)[NA][8]) {
-                if constexpr (kStage) x6_store<1, BM, NT, PREC, ABL>(As[buf], v, t, sa);
-            };
-            const int li = lane & 31, lh = lane >> 5;
-            auto mma = [&](int abuf, int bslot) {
-                const uint4* __restrict__ Ac = As[abuf];
-                const uint4* __restrict__ Bc = Bs[bslot];
-#pragma unroll
-                for (int kk = 0; kk < X6_BK / 16; ++kk) {
-                    uint4 a[TM][NP], b[TN][NP];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int p = 0; p < NP; ++p)
-                            a[i][p] = Ac[p * BM * 4 + x6_pos(wm * (BM / WM) + i * 32 + li, 2 * kk + lh)];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-#pragma unroll
-                        for (int p = 0; p < NP; ++p)
-                            b[j][p] = Bc[p * BN * 4 + x6_pos(wn * (BN / WN) + j * 32 + li, 2 * kk + lh)];
-                    x6_mma<TM, TN, PREC, NP>(acc, a, b);
-                }
-            };
-            if (nk > 0) {
-                glds_b(0);
-                if (nk > 1) glds_b(1);
-                load_a(kb, va[0]);
-                if (nk > 1) load_a(kb + X6_BK, va[1]);
-                store_a(0, va[0]);
-                if (nk > 2) load_a(kb + 2 * X6_BK, va[0]);
-            }
-            wait_vmcnt_asm<0>();   // (prologue: slice 0's B landed)
-            __syncthreads();
-            for (int64_t kt = 0; kt < nk; ++kt) {
-                const int cur = (int)(kt & 1);
-                if (kt + 1 < nk) store_a(cur ^ 1, va[cur ^ 1]);
-                if (kt + 2 < nk) glds_b(kt + 2);
-                if (kt + 3 < nk) load_a(kb + (kt + 3) * X6_BK, va[cur ^ 1]);
-                __builtin_amdgcn_sched_barrier(0);
-                mma(cur, (int)(kt % 3));
-                // B slice kt+1 (issued at step kt-1) landed: younger are A slice kt+2 (step kt-1),
-                // B slice kt+2 and A slice kt+3 (this step) -- a lower bound of the instructions
-                if (kt + 3 < nk) wait_vmcnt_asm<4 * NA + GPW>();
-                else wait_vmcnt_asm<0>();
-                __builtin_amdgcn_s_barrier();
-            }
-        };
-        if (full) wb_loop(std::integral_constant<int, 1>{});
-        else wb_loop(std::integral_constant<int, 0>{});
-    } else if constexpr ((PPV & 1) != 0) {
+    if constexpr ((PPV & 1) != 0) {
         static_assert(PREC == 1 && AK && BKc && ABL != 7, "ping-pong: f16x3 with K-contiguous A and B");
         constexpr int NTG = NT / 2, RA = BM / 2, RB = BN / 2;
         static_assert(RA * 4 % NTG == 0 && RB * 4 % NTG == 0 && (WM * WN) % 2 == 0 && (WM % 2 == 0 || WM == 1),

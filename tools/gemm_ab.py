@@ -43,8 +43,8 @@ def main():
         ref = None
         for vs in args.variants.split(","):
             wimg = None
-            if vs[0] == "w":   # pre-split weight image + bgnn_gemm_f32_w
-                _lib.call("bgnn_gemm_set_cfg", -1)
+            if vs[0] == "w":   # pre-split weight image + bgnn_gemm_f32_w ("wC": tile config C)
+                _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if len(vs) > 1 else -1)
                 _lib.call("bgnn_set_tuning", 14, 0)
                 bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
                 wimg = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)

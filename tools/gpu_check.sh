@@ -22,7 +22,7 @@
 #   profcfg3   the same for cfg3
 #   profea5    the same for EA_GNN cfg5 bf16
 #   pmc        FETCH_SIZE and WRITE_SIZE passes of the cfg2 bench -> gpurun_out/traffic_TAG.json
-#   pmcgemm    SQ counter passes of the cfg2 bench (tools/pmc_gemm.sh)
+#   pmcgemm    SQ counter passes of the SAGE GEMM shapes (tools/pmc_passes.sh, tools/gemm_cfg_ab.py)
 # Outputs land in gpurun_out/ named by step and TAG.
 set -o pipefail
 TAG=${1:-run}
@@ -83,7 +83,11 @@ for s in $STEPS; do
       (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$ROOT/gpurun_out/pmc_$TAG/write" \
          -o run -- python "$ROOT/bench.py" --steps 3 --warmup 2 --no-cpu-baseline --no-cfg3 > /dev/null 2>&1) || die pmc_write $?
       python tools/traffic.py "gpurun_out/pmc_$TAG" "gpurun_out/traffic_$TAG.json" > /dev/null || true ;;
-    pmcgemm) bash tools/pmc_gemm.sh "$TAG" || die pmcgemm $? ;;
+    pmcgemm)   # SQ counter anatomy of the SAGE GEMM shapes (default plans), two counter passes
+      bash tools/pmc_passes.sh "gpurun_out/pmc_gemm_$TAG" "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU" \
+        "SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM" \
+        -- python tools/gemm_cfg_ab.py --cfgs=-1 --rounds 3 || die pmcgemm $?
+      python tools/pmc_summary.py "gpurun_out/pmc_gemm_$TAG" k_gemm_x6 > "gpurun_out/pmc_gemm_$TAG.txt" || true ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
