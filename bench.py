@@ -110,6 +110,8 @@ def parse():
                     help="EA_GNN only: bf16 GEMM operands with f32 accumulation (BASELINE configs[4])")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="bgnn_set_tuning(KNOB, VALUE) before the run (A/B profiling; include/bgnn.h BGNN_TUNE_*)")
+    ap.add_argument("--py-set", action="append", default=[], metavar="MODULE.ATTR=EXPR",
+                    help="set a bgnn module switch before the run (A/B profiling), e.g. bgnn.fused.WSPLIT=False")
     return ap.parse_args()
 
 
@@ -473,10 +475,12 @@ def roofline_blocks(args, m, model_name):
 
 # family -> (flops(N, H, K_in), kernel, traffic key, description)
 GEMM_FAMILIES = {
-    "gemm_fwd": (lambda N, H, K: 2.0 * N * (2 * H) * H, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>", "gemm_fwd_h3",
+    "gemm_fwd": (lambda N, H, K: 2.0 * N * (2 * H) * H, "k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0, 4> (weights "
+                 "pre-split once per step, bgnn_gemm_f32_w)", "gemm_fwd_h3",
                  "fwd z = x [W_l;W_r]^T, K = 512 layers (5 per step)"),
-    "gemm_dgrad": (lambda N, H, K: 2.0 * N * H * (2 * H), "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8> (skip layers, "
-                   "drop-add epilogue) + k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0> (last layer)", "gemm_dgrad",
+    "gemm_dgrad": (lambda N, H, K: 2.0 * N * H * (2 * H), "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8, 4> (skip layers, "
+                   "drop-add epilogue) + k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0, 4> (last layer); weights pre-split "
+                   "once per step (bgnn_gemm_f32_w)", "gemm_dgrad",
                    "dgrad dx = [dz_l|dh] [W_l;W_r], K = 512 layers (5 per step)"),
     "gemm_wgrad": (lambda N, H, K: 2.0 * (2 * H) * H * N, "k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0> + split-K slab "
                    "reduce", "gemm_wgrad", "wgrad [dz_l|dh]^T x, K = 512 layers (5 per step)"),
@@ -541,6 +545,11 @@ def main():
     for kv in args.tune:
         k, v = kv.split("=")
         _lib.call("bgnn_set_tuning", int(k), int(v))
+    import importlib
+    for kv in args.py_set:
+        k, v = kv.split("=", 1)
+        mod, attr = k.rsplit(".", 1)
+        setattr(importlib.import_module(mod), attr, eval(v, {}, {}))
     world, rank, dev = setup_dist(args)
     fused.GEMM_BACKEND = args.gemm
     if args.mode == "infer":
