@@ -72,15 +72,18 @@ SIGNATURES = {
     "bgnn_heavy_plan_ws_bytes": (c_sz, [c_i64]),
     "bgnn_heavy_plan": (c_i32, [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
-    "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
-                              c_p, c_p, c_p]),
+    "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p,
+                              c_p]),
     "bgnn_bn_slots": (c_i32, [c_i64, c_i32]),
     "bgnn_bn_stats": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
     "bgnn_bn_apply": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
     "bgnn_bn_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p]),
     "bgnn_bn_bwd_dx": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i32, c_p, c_p]),
-    "bgnn_spmm_bwd_add": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_i64,
-                                  c_p, c_i64, c_p, c_p, c_p]),
+    "bgnn_spmm_bwd_add": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p,
+                                  c_i64, c_p, c_p, c_p]),
+    "bgnn_spmm_bwd_max": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_i64, c_p, c_i64, c_i32, c_p, c_p, c_i64, c_p,
+                                  c_i64, c_p, c_p, c_p]),
+    "bgnn_spmm_max_arg_bytes": (c_sz, [c_i64, c_i32, c_i32]),
     "bgnn_sage_fwd_slots": (c_i32, [ctypes.POINTER(CsrStruct)]),
     "bgnn_group_plan": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "bgnn_store_gather_groups": (c_i32, [c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64] + [c_p] * 14),

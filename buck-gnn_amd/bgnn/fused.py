@@ -791,7 +791,7 @@ class SageLayerFn(torch.autograd.Function):
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("spmm_bwd"):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
-                      dh.data_ptr(), lddz, H, cfg.reduce, None, dzl.data_ptr(), lddz, _ptr(part),
+                      dh.data_ptr(), lddz, H, cfg.reduce, dzl.data_ptr(), lddz, _ptr(part),
                       dz_amax.data_ptr(), s)
         has_affine = bn and gamma.numel() > 0
         if ctx.folded:
@@ -896,7 +896,7 @@ def _max_rows_fwd(y, b_l, H: int):
 def _max_backward(dh, dz_amax, wcat_t, x, agg, arg, graph: Graph, x_amax, w_amax, addend_beta_src,
                   need_dx: bool, p: float = 0.0, seed: int = 0):
     """Backward of y = [agg | x] [W_l | W_r]^T with agg = max-aggregate(x), given dh = dL/dy:
-        dagg = dh W_l, then dx = A_max^T dagg + (dh W_r [+ drop(g)])   (bgnn_spmm_bwd_add: the
+        dagg = dh W_l, then dx = A_max^T dagg + (dh W_r [+ drop(g)])   (bgnn_spmm_bwd_max: the
              gradient of each (target, column) goes to its argmax edge's source, CSR-first on ties)
         dW_l = dh^T agg,  dW_r = dh^T x
     wcat_t = [W_l ; W_r]^T ([C, 2H]); addend_beta_src: the skip connection's incoming gradient g
@@ -924,8 +924,8 @@ def _max_backward(dh, dz_amax, wcat_t, x, agg, arg, graph: Graph, x_amax, w_amax
         bw = graph.bwd
         part = torch.empty(bw.plan.n_chunks * x.size(1), dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("spmm_bwd"):
-            _lib.call("bgnn_spmm_bwd_add", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
-                      dagg.data_ptr(), dagg.stride(0), x.size(1), 2, arg.data_ptr(), t.data_ptr(), t.stride(0),
+            _lib.call("bgnn_spmm_bwd_max", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(), N,
+                      dagg.data_ptr(), dagg.stride(0), x.size(1), arg.data_ptr(), t.data_ptr(), t.stride(0),
                       dx.data_ptr(), dx.stride(0), _ptr(part), None, _stream())
     with _timed("gemm_wgrad"):
         dw_l = gemm(dh, agg, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
@@ -1247,7 +1247,7 @@ class SageConvFn(torch.autograd.Function):
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("conv_spmm_bwd"):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
-                      dh.data_ptr(), 2 * H, H, ctx.reduce, None, dz.data_ptr(), 2 * H, _ptr(part),
+                      dh.data_ptr(), 2 * H, H, ctx.reduce, dz.data_ptr(), 2 * H, _ptr(part),
                       dz_amax.data_ptr(), s)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -36,9 +36,14 @@ def _partial(csr, H: int, reduce: int, dev) -> torch.Tensor:
 
 
 def spmm_fwd(csr, x: torch.Tensor, reduce: int, out_rows: int, want_arg: bool = False):
+    """AGG over the CSR rows; for MAX with want_arg also the argmax state (a uint8 buffer of
+    bgnn_spmm_max_arg_bytes: per-row edge offsets, int32 for heavy rows; max_arg_positions decodes)."""
     H = x.size(1)
     out = torch.empty(out_rows, H, dtype=torch.float32, device=x.device)
-    arg = torch.empty(out_rows, H, dtype=torch.int32, device=x.device) if (reduce == 2 and want_arg) else None
+    arg = None
+    if reduce == 2 and want_arg:
+        arg = torch.empty(_lib.query("bgnn_spmm_max_arg_bytes", out_rows, H, csr.plan.n_heavy), dtype=torch.uint8,
+                          device=x.device)
     part = _partial(csr, H, reduce, x.device)
     if out_rows > 0 and H > 0:
         _lib.call("bgnn_spmm_fwd", csr.ref(), x.data_ptr(), x.stride(0), H, reduce, out.data_ptr(), out.stride(0),
@@ -47,16 +52,43 @@ def spmm_fwd(csr, x: torch.Tensor, reduce: int, out_rows: int, want_arg: bool = 
 
 
 def spmm_bwd(csr_t, perm_t, fwd_rowptr, g: torch.Tensor, reduce: int, arg, out_rows: int, amax=None):
+    """Transpose aggregation (rows = sources); MAX routes each (target, column) gradient to the
+    argmax edge recorded in `arg` (the forward's state; the forward had g.size(0) rows)."""
     g = g.contiguous()
     H = g.size(1)
     gx = torch.empty(out_rows, H, dtype=torch.float32, device=g.device)
     part = _partial(csr_t, H, 0, g.device)
     if out_rows > 0 and H > 0:
-        _lib.call("bgnn_spmm_bwd", csr_t.ref(), None if perm_t is None else perm_t.data_ptr(),
-                  None if fwd_rowptr is None else fwd_rowptr.data_ptr(), g.data_ptr(), g.stride(0), H, reduce,
-                  None if arg is None else arg.data_ptr(), gx.data_ptr(), gx.stride(0),
-                  None if part is None else part.data_ptr(), None if amax is None else amax.data_ptr(), _stream())
+        if reduce == 2:
+            _lib.call("bgnn_spmm_bwd_max", csr_t.ref(), perm_t.data_ptr(), fwd_rowptr.data_ptr(), g.size(0),
+                      g.data_ptr(), g.stride(0), H, arg.data_ptr(), None, 0, gx.data_ptr(), gx.stride(0),
+                      None if part is None else part.data_ptr(), None if amax is None else amax.data_ptr(), _stream())
+        else:
+            _lib.call("bgnn_spmm_bwd", csr_t.ref(), None if perm_t is None else perm_t.data_ptr(),
+                      None if fwd_rowptr is None else fwd_rowptr.data_ptr(), g.data_ptr(), g.stride(0), H, reduce,
+                      gx.data_ptr(), gx.stride(0), None if part is None else part.data_ptr(),
+                      None if amax is None else amax.data_ptr(), _stream())
     return gx
+
+
+def max_arg_positions(csr, arg: torch.Tensor, rows: int, H: int) -> torch.Tensor:
+    """Decode spmm_fwd's MAX argmax state into int64 CSR positions [rows, H] (-1 for empty rows):
+    test / inspection helper (torch ops on the device)."""
+    from .graph import Plan  # noqa: F401  (documentation: heavy rows come from csr.plan)
+    n = rows * H
+    hoff = (n + 255) // 256 * 256
+    aoff = hoff + (rows * 4 + 255) // 256 * 256
+    a8 = arg[:n].view(rows, H).long()
+    rp = csr.rowptr.long()
+    deg = rp[1:] - rp[:-1]
+    pos = rp[:-1].view(-1, 1) + a8
+    nh = csr.plan.n_heavy
+    if nh > 0:
+        heavy_of = arg[hoff:hoff + rows * 4].view(torch.int32)
+        ah = arg[aoff:aoff + nh * H * 4].view(torch.int32).view(nh, H).long()
+        hr = csr.plan.heavy_row[:nh].long()
+        pos[hr] = rp[hr].view(-1, 1) + ah[heavy_of[hr].long()]
+    return torch.where(deg.view(-1, 1) > 0, pos, torch.full_like(pos, -1))
 
 
 class _Aggregate(torch.autograd.Function):

@@ -41,13 +41,20 @@ struct SegArgs {
     // data
     const float* x;     int64_t ldx;
     float* out;         int64_t ldo;
-    int32_t* arg;       // MAX: [n_rows, H] (ld = H)
+    // MAX argmax state (bgnn_spmm_max_arg_bytes): arg8 [n_rows, H] uint8 = the argmax edge's offset
+    // in its row's edge list for light rows (deg <= chunk <= 64), kArgHeavy for heavy rows, whose
+    // offsets are int32 in arg_h [n_heavy, H]; heavy_of[r] = heavy index of heavy row r
+    uint8_t* arg8;
+    int32_t* heavy_of;
+    int32_t* arg_h;
     float* partial;     // [n_chunks, H]
     int32_t* partial_arg;
     // transpose helpers
-    const int32_t* fwd_rowptr;  // MEANT
+    const int32_t* fwd_rowptr;  // MEANT, MAXT
     const int32_t* perm_t;      // MAXT
-    const int32_t* arg_in;      // MAXT: forward arg [n_fwd_rows, H]
+    const uint8_t* arg8_in;     // MAXT: the forward argmax state (arg8 / heavy_of / arg_h above)
+    const int32_t* heavy_of_in;
+    const int32_t* arg_h_in;
     // SAGE epilogue
     const float* zr;    int64_t ldzr;   // lin_r term rows (z + H)
     const float* bias;
@@ -156,6 +163,32 @@ struct Acc {
     }
 };
 
+constexpr uint8_t kArgHeavy = 255;
+
+// MAXT: whether the forward edge at CSR position pe (target row i, first edge at fwd_rowptr[i]) is
+// the argmax of (i, c..c+VEC-1): one flag per column
+template <int VEC>
+__device__ __forceinline__ void maxt_match(const SegArgs& A, int32_t i, int32_t pe, int c, bool ok, bool (&m)[VEC]) {
+    const int32_t o = pe - A.fwd_rowptr[i];
+    uint8_t a8[VEC];
+    if constexpr (VEC == 4) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(A.arg8_in + (int64_t)i * A.H + c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a8[k] = (uint8_t)(w >> (8 * k));
+    } else {
+        a8[0] = A.arg8_in[(int64_t)i * A.H + c];
+    }
+    if (a8[0] == kArgHeavy) {   // (a heavy row: every column holds the marker)
+        int32_t ah[VEC];
+        ldi<VEC>(A.arg_h_in + (int64_t)A.heavy_of_in[i] * A.H + c, ah);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) m[k] = ok && ah[k] == o;
+    } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) m[k] = ok && (int32_t)a8[k] == o;
+    }
+}
+
 // Gather-accumulate the edges [e0, e1) of one row into acc. cols are shared by
 // the lanes of the row (wave-uniform when LPR == 64). `cpos[v]` = column offset
 // of this lane's v-th vector, `cok[v]` = whether it is inside H.
@@ -192,16 +225,11 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if constexpr (OP == OP_MAXT) {
-                int32_t ga[VEC];
-                if (cok[v]) ldi<VEC>(A.arg_in + (int64_t)j[u] * A.H + cpos[v], ga);
-                else {
-#pragma unroll
-                    for (int k = 0; k < VEC; ++k) ga[k] = -2;
-                }
                 const int32_t pe = A.perm_t[e + (u < nvalid ? u : 0)];
+                bool m[VEC];
+                maxt_match<VEC>(A, j[u], pe, cok[v] ? cpos[v] : 0, ok && cok[v], m);
 #pragma unroll
-                for (int k = 0; k < VEC; ++k)
-                    acc.a[v][k] += (ok && ga[k] == pe) ? val[u][v].f[k] : 0.f;
+                for (int k = 0; k < VEC; ++k) acc.a[v][k] += m[k] ? val[u][v].f[k] : 0.f;
             } else if constexpr (OP == OP_MAX) {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) {
@@ -232,7 +260,11 @@ __device__ __forceinline__ void gather_range(const SegArgs& A, Acc<VEC, NV, OP>&
 template <int VEC, int NV, int OP>
 __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& acc, int64_t r,
                                             int32_t deg, const int (&cpos)[NV],
-                                            const bool (&cok)[NV], uint32_t& tmax) {
+                                            const bool (&cok)[NV], uint32_t& tmax, int32_t h = -1) {
+    int32_t rb = 0;
+    if constexpr (OP == OP_MAX) {
+        if (A.arg8) rb = A.rowptr[r];
+    }
     const float sc = (OP == OP_MEAN) ? inv_deg(deg) : 1.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -258,11 +290,21 @@ __device__ __forceinline__ void store_plain(const SegArgs& A, Acc<VEC, NV, OP>& 
             st<VEC>(A.out + r * A.ldo + cpos[v], o);
         }
         if constexpr (OP == OP_MAX) {
-            if (A.arg) {
-                int32_t gi[VEC];
+            if (A.arg8) {   // offsets in the row's edge list (heavy rows: int32 in arg_h)
+                uint32_t w = 0;
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) gi[k] = deg > 0 ? acc.g[v][k] : -1;
-                sti<VEC>(A.arg + r * A.H + cpos[v], gi);
+                for (int k = 0; k < VEC; ++k) {
+                    const uint32_t o = h >= 0 ? kArgHeavy : (deg > 0 ? (uint32_t)(acc.g[v][k] - rb) : 0u);
+                    w |= (o & 0xffu) << (8 * k);
+                }
+                if constexpr (VEC == 4) *reinterpret_cast<uint32_t*>(A.arg8 + r * A.H + cpos[v]) = w;
+                else A.arg8[r * A.H + cpos[v]] = (uint8_t)w;
+                if (h >= 0) {
+                    int32_t gi[VEC];
+#pragma unroll
+                    for (int k = 0; k < VEC; ++k) gi[k] = acc.g[v][k] - rb;
+                    sti<VEC>(A.arg_h + (int64_t)h * A.H + cpos[v], gi);
+                }
             }
         }
     }
@@ -516,7 +558,10 @@ __global__ __launch_bounds__(1024) void k_seg_combine(SegArgs A) {
             }
     } else {
         uint32_t tmax = 0;
-        store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok, tmax);
+        store_plain<VEC, NV, OP>(A, acc, r, deg, cpos, cok, tmax, OP == OP_MAX ? h : -1);
+        if constexpr (OP == OP_MAX) {
+            if (A.arg8 && blockIdx.y == 0 && lane == 0) A.heavy_of[r] = h;
+        }
         if (A.amax && tmax) atomicMax(A.amax, tmax);   // one heavy row per wave: few atomics
     }
 }
@@ -582,11 +627,11 @@ __device__ __forceinline__ void sweep_gather(const SegArgs& A, Acc<4, NV, OP>& a
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if constexpr (OP == OP_MAXT) {
-                int32_t ga[4];
-                ldi<4>(A.arg_in + (int64_t)j[u] * A.H + (cok[v] ? cpos[v] : 0), ga);
                 const int32_t pe = A.perm_t[beg + e0 + (ok ? u : 0)];
+                bool m[4];
+                maxt_match<4>(A, j[u], pe, cok[v] ? cpos[v] : 0, ok && cok[v], m);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) acc.a[v][k] += (ok && ga[k] == pe) ? val[u][v].f[k] : 0.f;
+                for (int k = 0; k < 4; ++k) acc.a[v][k] += m[k] ? val[u][v].f[k] : 0.f;
             } else if constexpr (OP == OP_MAX) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -1106,6 +1151,17 @@ int dispatch_plain(SegArgs A, const Geometry& g, hipStream_t s) {
 }
 
 
+// byte layout of the MAX argmax state buffer (bgnn_spmm_max_arg_bytes)
+struct MaxArgLayout {
+    int64_t heavy_of, arg_h;
+};
+inline MaxArgLayout max_arg_layout(int64_t rows, int64_t H) {
+    MaxArgLayout L;
+    L.heavy_of = (int64_t)align_up((size_t)(rows * H), 256);
+    L.arg_h = L.heavy_of + (int64_t)align_up((size_t)(rows * 4), 256);
+    return L;
+}
+
 inline SegArgs args_from_csr(const bgnn_csr_t* c) {
     SegArgs A{};
     A.rowptr = c->rowptr;
@@ -1133,7 +1189,7 @@ inline SegArgs args_from_csr(const bgnn_csr_t* c) {
 using namespace bgnn;
 
 extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H, int32_t reduce,
-                             float* out, int64_t ldo, int32_t* arg, float* partial, void* stream) {
+                             float* out, int64_t ldo, void* arg, float* partial, void* stream) {
     // (no max |out| here: nothing downstream scales by it)
     BGNN_REQUIRE(csr && csr->rowptr, "spmm_fwd: null csr");
     BGNN_REQUIRE(H > 0 && ldx >= H && ldo >= H, "spmm_fwd: bad H/ld");
@@ -1144,7 +1200,12 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
     A.H = H;
     A.x = x; A.ldx = ldx;
     A.out = out; A.ldo = ldo;
-    A.arg = arg;
+    if (arg) {
+        const MaxArgLayout L = max_arg_layout(csr->n_rows, H);
+        A.arg8 = static_cast<uint8_t*>(arg);
+        A.heavy_of = reinterpret_cast<int32_t*>(static_cast<char*>(arg) + L.heavy_of);
+        A.arg_h = reinterpret_cast<int32_t*>(static_cast<char*>(arg) + L.arg_h);
+    }
     A.partial = partial;
     A.partial_arg = partial ? reinterpret_cast<int32_t*>(partial + (int64_t)csr->n_chunks * H) : nullptr;
     const bool al = aligned16(x) && aligned16(out) && ldx % 4 == 0 && ldo % 4 == 0 &&
@@ -1158,22 +1219,40 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
     }
 }
 
-extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
-                                 const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
-                                 const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
-                                 float* amax, void* stream);
+static int spmm_bwd_impl(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                         int64_t fwd_rows, const float* g, int64_t ldg, int32_t H, int32_t reduce, const void* arg,
+                         const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial, float* amax,
+                         void* stream);
 
 extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
-                             const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
-                             float* gx, int64_t ldgx, float* partial, float* amax, void* stream) {
-    return bgnn_spmm_bwd_add(csr_t, perm_t, fwd_rowptr, g, ldg, H, reduce, arg, nullptr, 0, gx, ldgx, partial, amax,
-                             stream);
+                             const float* g, int64_t ldg, int32_t H, int32_t reduce, float* gx, int64_t ldgx,
+                             float* partial, float* amax, void* stream) {
+    BGNN_REQUIRE(reduce != BGNN_REDUCE_MAX, "spmm_bwd: max aggregation takes bgnn_spmm_bwd_max");
+    return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, 0, g, ldg, H, reduce, nullptr, nullptr, 0, gx, ldgx, partial, amax,
+                         stream);
 }
 
 extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
-                                 const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                                 const float* g, int64_t ldg, int32_t H, int32_t reduce, const float* addend,
+                                 int64_t ld_add, float* gx, int64_t ldgx, float* partial, float* amax, void* stream) {
+    BGNN_REQUIRE(reduce != BGNN_REDUCE_MAX, "spmm_bwd_add: max aggregation takes bgnn_spmm_bwd_max");
+    return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, 0, g, ldg, H, reduce, nullptr, addend, ld_add, gx, ldgx, partial,
+                         amax, stream);
+}
+
+extern "C" int bgnn_spmm_bwd_max(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                                 int64_t fwd_rows, const float* g, int64_t ldg, int32_t H, const void* arg,
                                  const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
                                  float* amax, void* stream) {
+    BGNN_REQUIRE(perm_t && fwd_rowptr && arg && fwd_rows >= 0, "spmm_bwd_max: perm_t, fwd_rowptr and arg required");
+    return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, fwd_rows, g, ldg, H, BGNN_REDUCE_MAX, arg, addend, ld_add, gx, ldgx,
+                         partial, amax, stream);
+}
+
+static int spmm_bwd_impl(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                         int64_t fwd_rows, const float* g, int64_t ldg, int32_t H, int32_t reduce, const void* arg,
+                         const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial, float* amax,
+                         void* stream) {
     BGNN_REQUIRE(csr_t && csr_t->rowptr, "spmm_bwd: null csr");
     BGNN_REQUIRE(!addend || ld_add >= H, "spmm_bwd: bad ld_add");
     BGNN_REQUIRE(H > 0 && ldg >= H && ldgx >= H, "spmm_bwd: bad H/ld");
@@ -1186,7 +1265,12 @@ extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t,
     A.partial = partial;
     A.fwd_rowptr = fwd_rowptr;
     A.perm_t = perm_t;
-    A.arg_in = arg;
+    if (arg) {
+        const MaxArgLayout L = max_arg_layout(fwd_rows, H);
+        A.arg8_in = static_cast<const uint8_t*>(arg);
+        A.heavy_of_in = reinterpret_cast<const int32_t*>(static_cast<const char*>(arg) + L.heavy_of);
+        A.arg_h_in = reinterpret_cast<const int32_t*>(static_cast<const char*>(arg) + L.arg_h);
+    }
     A.amax = reinterpret_cast<uint32_t*>(amax);
     A.add = addend;
     A.ld_add = ld_add;
@@ -1201,7 +1285,7 @@ extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t,
             BGNN_REQUIRE(fwd_rowptr, "spmm_bwd(mean): fwd_rowptr required");
             return dispatch_plain<OP_MEANT>(A, geo, s);
         default:
-            BGNN_REQUIRE(perm_t && arg, "spmm_bwd(max): perm_t and arg required");
+            BGNN_REQUIRE(perm_t && arg && fwd_rowptr, "spmm_bwd(max): perm_t, fwd_rowptr and arg required");
             return dispatch_plain<OP_MAXT>(A, geo, s);
     }
 }
@@ -1316,4 +1400,9 @@ extern "C" int bgnn_heavy_timing_read(int32_t which, float* total_ms, int32_t* c
     *total_ms = (float)t;
     *count = n;
     return BGNN_OK;
+}
+
+extern "C" size_t bgnn_spmm_max_arg_bytes(int64_t rows, int32_t H, int32_t n_heavy) {
+    if (rows < 0 || H <= 0 || n_heavy < 0) return 0;
+    return (size_t)max_arg_layout(rows, H).arg_h + (size_t)n_heavy * (size_t)H * 4;
 }

@@ -183,26 +183,38 @@ int bgnn_group_plan(const int32_t* rowptr, const int32_t* col, int64_t n_rows, i
  * `partial` is scratch of n_chunks * H floats (+ n_chunks * H int32 for MAX).
  * ---------------------------------------------------------------------- */
 int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H,
-                  int32_t reduce, float* out, int64_t ldo, int32_t* arg,
+                  int32_t reduce, float* out, int64_t ldo, void* arg,
                   float* partial, void* stream);
+/* MAX: `arg` (optional; needed for the backward) receives the argmax state, a device buffer of
+ * bgnn_spmm_max_arg_bytes(n_rows, H, n_heavy) bytes (round 5, ABI 10; was an int32 [rows, H]
+ * array of CSR positions): per (row, column) the argmax edge's offset in the row's edge list as
+ * one byte for light rows (deg <= chunk <= 64), and for heavy rows (super nodes) a marker byte
+ * plus the int32 offset in a per-heavy-row array -- 1 B instead of 4 B per element written by the
+ * forward and gathered per edge by the backward. Ties: the first maximising edge in CSR order. */
+size_t bgnn_spmm_max_arg_bytes(int64_t n_rows, int32_t H, int32_t n_heavy);
 
 /* Backward of bgnn_spmm_fwd through the transpose CSR (rows = sources):
  *   SUM : gx[j] = sum_{q in rowT j} g[col_t[q]]
  *   MEAN: gx[j] = sum_{q in rowT j} g[col_t[q]] / max(deg_fwd(col_t[q]), 1)
- *   MAX : gx[j, c] = sum_{q in rowT j, arg[col_t[q], c] == perm_t[q]} g[col_t[q], c]
- * `fwd_rowptr` is the forward CSR's rowptr (for MEAN degrees); `perm_t` and `arg`
- * are needed for MAX only. Deterministic (gather form, no atomics on gx).
- * amax (optional): *amax = max(*amax, max |gx|), the operand scale of the f16x3 GEMMs
- * that consume gx (bgnn_gemm_f32_scaled). */
+ * `fwd_rowptr` is the forward CSR's rowptr (MEAN degrees). Deterministic (gather form, no
+ * atomics on gx). amax (optional): *amax = max(*amax, max |gx|), the operand scale of the f16x3
+ * GEMMs that consume gx (bgnn_gemm_f32_scaled). MAX takes bgnn_spmm_bwd_max. */
 int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
-                  const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                  const float* g, int64_t ldg, int32_t H, int32_t reduce,
                   float* gx, int64_t ldgx, float* partial, float* amax, void* stream);
 /* bgnn_spmm_bwd with an addend: gx[j] = (A^T g)[j] + addend[j] (addend [rows, H], ld ld_add),
- * added after the reduction, in the same pass. The max-aggregation SAGEConv backward
- * (aggregate-first form) adds the lin_r input gradient dh W_r (+ the skip gradient) to the
- * scattered lin_l gradient this way (bgnn/fused.py). */
+ * added after the reduction, in the same pass. */
 int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
-                      const float* g, int64_t ldg, int32_t H, int32_t reduce, const int32_t* arg,
+                      const float* g, int64_t ldg, int32_t H, int32_t reduce,
+                      const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
+                      float* amax, void* stream);
+/* MAX backward: gx[j, c] = sum over j's out-edges q (target i = col_t[q]) that are the argmax of
+ * (i, c) -- fwd CSR position perm_t[q] == fwd_rowptr[i] + offset in the argmax state `arg` of the
+ * forward (fwd_rows = its row count) -- of g[i, c], plus the optional addend (the max-aggregation
+ * SAGEConv backward adds the lin_r input gradient dh W_r (+ the skip gradient) this way,
+ * bgnn/fused.py). */
+int bgnn_spmm_bwd_max(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
+                      int64_t fwd_rows, const float* g, int64_t ldg, int32_t H, const void* arg,
                       const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial,
                       float* amax, void* stream);
 

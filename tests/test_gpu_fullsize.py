@@ -92,9 +92,12 @@ def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg, model_n
     if is_max:
         real_mt = fused._max_transform
 
-        def spy(x, *a, **k):
-            y, agg, arg = real_mt(x, *a, **k)
-            captured.append((x.detach().cpu(), arg.detach().cpu()))
+        from bgnn import ops
+
+        def spy(x, w_l, w_r, graph, *a, **k):
+            y, agg, arg = real_mt(x, w_l, w_r, graph, *a, **k)
+            pos = ops.max_arg_positions(graph.fwd, arg, x.size(0), x.size(1))   # CSR positions, -1: empty row
+            captured.append((x.detach().cpu(), pos.cpu()))
             return y, agg, arg
         monkeypatch.setattr(fused, "_max_transform", spy)
     bd = b.to(dev)

@@ -253,8 +253,13 @@ def test_spmm_bwd_add_equals_spmm_bwd_plus_addend(dev, reduce, graph):
     gx = torch.empty(n, H, device=dev)
     amax = torch.zeros(1, device=dev)
     part = torch.empty(max(g.bwd.plan.n_chunks, 1) * H, device=dev)
-    _lib.call("bgnn_spmm_bwd_add", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), gy.data_ptr(), H, H,
-              reduce, None if arg is None else arg.data_ptr(), add.data_ptr(), H, gx.data_ptr(), H, part.data_ptr(),
-              amax.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    if reduce == 2:
+        _lib.call("bgnn_spmm_bwd_max", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), n, gy.data_ptr(), H,
+                  H, arg.data_ptr(), add.data_ptr(), H, gx.data_ptr(), H, part.data_ptr(), amax.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
+    else:
+        _lib.call("bgnn_spmm_bwd_add", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), gy.data_ptr(), H,
+                  H, reduce, add.data_ptr(), H, gx.data_ptr(), H, part.data_ptr(), amax.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
     assert torch.equal(gx, ref)
     assert amax.item() == gx.abs().max().item()

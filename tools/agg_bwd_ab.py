@@ -59,7 +59,7 @@ def main():
     def bwd(csr, src, ld_src, dst, ld_dst):
         def f():
             _lib.call("bgnn_spmm_bwd", csr.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), src.data_ptr(),
-                      ld_src, H, 0, None, dst.data_ptr(), ld_dst, part.data_ptr(), None, s)
+                      ld_src, H, 0, dst.data_ptr(), ld_dst, part.data_ptr(), None, s)
         return f
 
     def nt0(f):

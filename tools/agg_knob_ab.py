@@ -114,7 +114,7 @@ def main():
 
     def bwd_t():
         _lib.call("bgnn_spmm_bwd", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), dz[:, H:].data_ptr(),
-                  2 * H, H, 0, None, dz.data_ptr(), 2 * H, part.data_ptr(), None, s)
+                  2 * H, H, 0, dz.data_ptr(), 2 * H, part.data_ptr(), None, s)
         return dz[:, :H]
 
     def apply(setting, undo=None):
