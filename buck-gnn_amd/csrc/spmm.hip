@@ -165,27 +165,27 @@ struct Acc {
 
 constexpr uint8_t kArgHeavy = 255;
 
-// MAXT: whether the forward edge at CSR position pe (target row i, first edge at fwd_rowptr[i]) is
-// the argmax of (i, c..c+VEC-1): one flag per column
+// MAXT: the forward argmax bytes of (i, c..c+VEC-1), packed (VEC 4: one dword, VEC 1: one byte).
+// Loaded in the same batch as the x rows, so that a gather batch issues all its loads at once.
 template <int VEC>
-__device__ __forceinline__ void maxt_match(const SegArgs& A, int32_t i, int32_t pe, int c, bool ok, bool (&m)[VEC]) {
-    const int32_t o = pe - A.fwd_rowptr[i];
-    uint8_t a8[VEC];
-    if constexpr (VEC == 4) {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(A.arg8_in + (int64_t)i * A.H + c);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) a8[k] = (uint8_t)(w >> (8 * k));
-    } else {
-        a8[0] = A.arg8_in[(int64_t)i * A.H + c];
-    }
-    if (a8[0] == kArgHeavy) {   // (a heavy row: every column holds the marker)
+__device__ __forceinline__ uint32_t maxt_bytes(const SegArgs& A, int32_t i, int c) {
+    if constexpr (VEC == 4) return *reinterpret_cast<const uint32_t*>(A.arg8_in + (int64_t)i * A.H + c);
+    else return A.arg8_in[(int64_t)i * A.H + c];
+}
+
+// MAXT: whether the forward edge at offset o of its target row i is the argmax of (i, c..c+VEC-1),
+// one flag per column, from the bytes maxt_bytes loaded (heavy rows: the int32 offsets in arg_h)
+template <int VEC>
+__device__ __forceinline__ void maxt_match(const SegArgs& A, int32_t i, int32_t o, int c, uint32_t w, bool ok,
+                                           bool (&m)[VEC]) {
+    if ((w & 0xffu) == kArgHeavy) {   // (a heavy row: every column holds the marker; rare)
         int32_t ah[VEC];
         ldi<VEC>(A.arg_h_in + (int64_t)A.heavy_of_in[i] * A.H + c, ah);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) m[k] = ok && ah[k] == o;
     } else {
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) m[k] = ok && (int32_t)a8[k] == o;
+        for (int k = 0; k < VEC; ++k) m[k] = ok && (int32_t)((w >> (8 * k)) & 0xffu) == o;
     }
 }
 
@@ -198,6 +198,7 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
                                              const bool (&cok)[NV]) {
     int32_t j[U];
     float w[U];
+    int32_t off[(OP == OP_MAXT) ? U : 1];   // MAXT: the edge's offset in its forward row
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int32_t eu = e + (u < nvalid ? u : 0);
@@ -207,8 +208,10 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
             const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
             w[u] = inv_deg(d);
         }
+        if constexpr (OP == OP_MAXT) off[u] = A.perm_t[eu] - A.fwd_rowptr[j[u]];
     }
     Vec<VEC> val[U][NV];
+    uint32_t aw[(OP == OP_MAXT) ? U : 1][(OP == OP_MAXT) ? NV : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -218,6 +221,7 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) val[u][v].f[k] = 0.f;
             }
+            if constexpr (OP == OP_MAXT) aw[u][v] = maxt_bytes<VEC>(A, j[u], cok[v] ? cpos[v] : 0);
         }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -225,9 +229,8 @@ __device__ __forceinline__ void gather_batch(const SegArgs& A, Acc<VEC, NV, OP>&
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if constexpr (OP == OP_MAXT) {
-                const int32_t pe = A.perm_t[e + (u < nvalid ? u : 0)];
                 bool m[VEC];
-                maxt_match<VEC>(A, j[u], pe, cok[v] ? cpos[v] : 0, ok && cok[v], m);
+                maxt_match<VEC>(A, j[u], off[u], cok[v] ? cpos[v] : 0, aw[u][v], ok && cok[v], m);
 #pragma unroll
                 for (int k = 0; k < VEC; ++k) acc.a[v][k] += m[k] ? val[u][v].f[k] : 0.f;
             } else if constexpr (OP == OP_MAX) {
@@ -606,6 +609,7 @@ __device__ __forceinline__ void sweep_gather(const SegArgs& A, Acc<4, NV, OP>& a
     const int nvalid = min(U, deg - e0);
     int32_t j[U];
     float w[U];
+    int32_t off[(OP == OP_MAXT) ? U : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int slot = (u < nvalid) ? e0 + u : e0;   // masked slots re-read the first row (L1 hit)
@@ -615,21 +619,25 @@ __device__ __forceinline__ void sweep_gather(const SegArgs& A, Acc<4, NV, OP>& a
             const int32_t d = A.fwd_rowptr[j[u] + 1] - A.fwd_rowptr[j[u]];
             w[u] = inv_deg(d);
         }
+        if constexpr (OP == OP_MAXT) off[u] = A.perm_t[beg + slot] - A.fwd_rowptr[j[u]];
     }
     Vec<4> val[U][NV];
+    uint32_t aw[(OP == OP_MAXT) ? U : 1][(OP == OP_MAXT) ? NV : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int v = 0; v < NV; ++v) val[u][v] = ld<4>(A.x + (int64_t)j[u] * A.ldx + (cok[v] ? cpos[v] : 0));
+        for (int v = 0; v < NV; ++v) {
+            val[u][v] = ld<4>(A.x + (int64_t)j[u] * A.ldx + (cok[v] ? cpos[v] : 0));
+            if constexpr (OP == OP_MAXT) aw[u][v] = maxt_bytes<4>(A, j[u], cok[v] ? cpos[v] : 0);
+        }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const bool ok = u < nvalid;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if constexpr (OP == OP_MAXT) {
-                const int32_t pe = A.perm_t[beg + e0 + (ok ? u : 0)];
                 bool m[4];
-                maxt_match<4>(A, j[u], pe, cok[v] ? cpos[v] : 0, ok && cok[v], m);
+                maxt_match<4>(A, j[u], off[u], cok[v] ? cpos[v] : 0, aw[u][v], ok && cok[v], m);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) acc.a[v][k] += m[k] ? val[u][v].f[k] : 0.f;
             } else if constexpr (OP == OP_MAX) {
