@@ -400,12 +400,13 @@ struct Plan {
 };
 
 static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk,
-                      int precision = 0) {
+                      int precision = 0, bool wb = false) {
     Plan p{};
     if (precision == 1) {   // bf16 operands, f32 accumulation (the split kernel with one piece)
         p.x6 = 1;
         p.prec = 2;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, 1);
+        if (p.cfg == kX6CfgWB) p.cfg = 4;
         if (a_blk != 0 || c_blk != 0) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves, kX6Cfgs[p.cfg].blocks_per_cu});
@@ -418,6 +419,7 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.x6 = 1;
         p.prec = 1;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
+        if (p.cfg == kX6CfgWB && !wb) p.cfg = 4;   // (the 320-row tile exists for pre-split B only)
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves,
@@ -542,8 +544,8 @@ extern "C" int bgnn_gemm_f32_dropadd(int32_t ta, int32_t tb, int64_t M, int64_t 
 
 extern "C" int32_t bgnn_gemm_w_tile(int64_t M, int64_t N, int64_t K) {
     if (gemm_mode() != 2 || M <= 0 || N <= 0 || K <= 0) return 0;
-    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0);
-    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg < 1 || pl.cfg > 4) return 0;
+    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0, 0, true);
+    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg < 1 || pl.cfg > kX6CfgWB) return 0;
     if (N % pl.bn != 0 || K % 32 != 0) return 0;
     return pl.bn;
 }
@@ -562,7 +564,7 @@ extern "C" int bgnn_gemm_f32_w(int64_t M, int64_t N, int64_t K, const float* A, 
                  tile);
     BGNN_REQUIRE(!src || (ld_src >= N && ld_src % 4 == 0 && N % 4 == 0 && ((uintptr_t)src & 15) == 0),
                  "gemm_f32_w: src must be 16-byte aligned with N and ld_src multiples of 4");
-    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0);
+    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0, 0, true);
     GemmArgs g{A, static_cast<const float*>(wimg), C, nullptr, M, N, K, lda, K, ldc, 1.f, src ? 1.f : 0.f, 0, 1,
                bias, relu, 0, 0, 0, 0, a_amax, b_amax, c_amax};
     g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;

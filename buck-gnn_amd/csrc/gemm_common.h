@@ -81,6 +81,7 @@ struct X6Cfg {
 };
 extern const X6Cfg kX6Cfgs[];
 extern const int kNumX6Cfgs;
+constexpr int kX6CfgWB = 5;   // the 320 x 256 tile, built for pre-split B (bgnn_gemm_f32_w) only
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
 // bf16-operand GEMM on bf16-STORED A and B (gemm_b16.hip): b16_ok = the call qualifies (ta 0,
 // tb 1, storage bits 0 and 1, K % 64 == 0, dense 16-B aligned rows, no split-K / drop-add);

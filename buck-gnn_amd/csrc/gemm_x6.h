@@ -100,7 +100,8 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
     // drop-add dgrad (ABL 8), interior tile: every bsrc float4 this lane adds is loaded before the
     // first staging pass, so the HBM latency overlaps the LDS staging and only the first 32-column
     // block waits for it (the main loop's staging registers are dead here: 16 float4 fit)
-    constexpr bool kPre = ABL == 8 && !C16;
+    // (up to 32 float4: larger tiles keep the per-row loads, their accumulators fill the VGPRs)
+    constexpr bool kPre = ABL == 8 && !C16 && TN * TM * 4 <= 32;
     float4 gpre[kPre ? TN : 1][kPre ? TM * 4 : 1];
     if constexpr (kPre) {
         if (fast && g.beta != 0.f) {

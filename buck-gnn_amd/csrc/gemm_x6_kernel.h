@@ -12,6 +12,11 @@ namespace bgnn {
 
 constexpr int X6_BK = 32;
 
+// staging units (8 k of one row) per thread for an R-row operand tile over NT threads; a tile
+// whose unit count is no multiple of NT (320 rows over 512 threads) gives the last unit to the
+// first threads only (a wave-uniform guard)
+constexpr int x6_nu(int R, int NT) { return (R * 4 + NT - 1) / NT; }
+
 // 16-B chunk index of (row, chunk) in a [R][32]-bf16 image
 __device__ __forceinline__ int x6_pos(int row, int chunk) { return row * 4 + (chunk ^ ((row >> 2) & 3)); }
 
@@ -27,12 +32,13 @@ __device__ __forceinline__ float bf16_at(const uint16_t* __restrict__ P16, int64
 // bf16 configuration): loaded at half the bytes and widened exactly to f32 in registers.
 template <int KCONTIG, int R, int NT, bool FULL, bool BF = false>
 __device__ __forceinline__ void x6_load(const float* __restrict__ P, int64_t ld, int64_t Rlim, int64_t r0,
-                                        int64_t k0, int64_t kend, bool vec_ok, float (&v)[R * 4 / NT][8], int t) {
-    constexpr int NU = R * 4 / NT;
+                                        int64_t k0, int64_t kend, bool vec_ok, float (&v)[x6_nu(R, NT)][8], int t) {
+    constexpr int NU = x6_nu(R, NT);
     const uint16_t* __restrict__ P16 = reinterpret_cast<const uint16_t*>(P);
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int idx = t + NT * u;
+        if (R * 4 % NT != 0 && idx >= R * 4) break;
         if constexpr (BF) {
             if constexpr (KCONTIG) {
                 const int r = idx >> 2, c = idx & 3;
@@ -83,11 +89,12 @@ __device__ __forceinline__ void x6_load(const float* __restrict__ P, int64_t ld,
 // split the staged units and write the piece images (S = piece 0; piece p at S + p*R*4);
 // PREC 1 scales by sc first (exact: a power of two)
 template <int KCONTIG, int R, int NT, int PREC, int ABL = 0>
-__device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)[R * 4 / NT][8], int t, float sc) {
-    constexpr int NU = R * 4 / NT;
+__device__ __forceinline__ void x6_store(uint4* __restrict__ S, const float (&v)[x6_nu(R, NT)][8], int t, float sc) {
+    constexpr int NU = x6_nu(R, NT);
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int idx = t + NT * u;
+        if (R * 4 % NT != 0 && idx >= R * 4) break;
         const int r = KCONTIG ? (idx >> 2) : (idx % R);
         const int c = KCONTIG ? (idx & 3) : (idx / R);
         const int pos = x6_pos(r, c);
@@ -355,13 +362,19 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
-    static_assert(BM * 4 % NT == 0 && BN * 4 % NT == 0, "staging units must divide evenly");
+    // PPV bit 2: B arrives pre-split (bgnn_gemm_wsplit): its LDS image is copied, not split
+    constexpr bool kWB = (PPV & 4) != 0;
+    // (pre-split B: A may have a unit count that is no multiple of NT, x6_nu's guarded last unit)
+    static_assert((BM * 4 % NT == 0 || kWB) && BN * 4 % NT == 0, "staging units must divide evenly");
+    // PPV bit 3: B's MFMA fragments are loaded straight from the pre-split image into registers
+    // (no LDS image of B: its writes and reads leave the LDS port to A)
+    constexpr bool kWR = (PPV & 8) != 0;
+    static_assert(!kWR || (PREC == 1 && AK && BKc && !A16 && !B16 && (PPV & 7) == 0 && ABL != 7),
+                  "B in registers: f16x3 NT on a pre-split image");
     // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
     // epilogue as one [TM*32][32] f32 stage per wave
     constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
-    // PPV bit 2: B arrives pre-split (bgnn_gemm_wsplit): its LDS image is copied, not split
-    constexpr bool kWB = (PPV & 4) != 0;
-    constexpr int TILE_U4 = 2 * (A_U4 + B_U4), STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
+    constexpr int TILE_U4 = 2 * (A_U4 + (kWR ? 0 : B_U4)), STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
     static_assert((TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
     __shared__ uint4 smem[TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4];
     uint4 (*As)[A_U4] = reinterpret_cast<uint4 (*)[A_U4]>(smem);
@@ -414,9 +427,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     static_assert(!kWB || (PREC == 1 && AK && BKc && !A16 && !B16 && (PPV & 3) == 0 && (BN * 8) % NT == 0),
                   "pre-split B: f16x3 NT, whole 16-B pieces per thread");
     // k-major quad staging for the weight gradient (both operands k-major, f16x3)
-    struct RegsStd { float a[BM * 4 / NT][8]; float b[BN * 4 / NT][8]; };
+    struct RegsStd { float a[x6_nu(BM, NT)][8]; float b[x6_nu(BN, NT)][8]; };
     // pre-split B (kWB): per thread BN * 8 / NT 16-B pieces of the slice's image, copied to LDS as is
-    struct RegsWB { float a[BM * 4 / NT][8]; uint4 b[BN * 8 / NT]; };
+    struct RegsWB { float a[x6_nu(BM, NT)][8]; uint4 b[BN * 8 / NT]; };
     struct RegsKQ { float q[4][8]; };
     struct RegsKQ16 { uint2 q[8]; };
     using Regs = std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ,
@@ -533,7 +546,72 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
         }
     };
-    if constexpr ((PPV & 1) != 0) {
+    if constexpr (kWR) {
+        // A through LDS as in the main loop (prefetch distance 2, split in registers); the B
+        // fragments of slice kt+1 are loaded from the image (one 16-B load per lane, fragment and
+        // piece: L2-resident, shared by every row tile of the column tile) while slice kt's
+        // MFMAs run, into the second of two register sets
+        const int li = lane & 31, lh = lane >> 5;
+        const uint4* __restrict__ img = reinterpret_cast<const uint4*>(g.B) + tn * (g.K / X6_BK) * (BN * 8);
+        const int64_t s0 = kb / X6_BK;
+        float ra[2][x6_nu(BM, NT)][8];
+        uint4 rb[2][2][TN][NP];   // [set][kk][j][piece]
+        auto load_b = [&](int64_t kt, uint4 (&b)[2][TN][NP]) {
+            const uint4* __restrict__ blk = img + (s0 + kt) * (BN * 8);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int p = 0; p < NP; ++p)   // (fragment-order image: one 1-KiB wave load each)
+                        b[kk][j][p] = blk[(((wn * (BN / WN) / 32 + j) * 2 + kk) * 2 + p) * 64 + lane];
+        };
+        auto wr_loop = [&](auto mode_tag) {
+            constexpr bool FULL = decltype(mode_tag)::value == 1;
+            auto load_a = [&](int64_t kt, float (&v)[x6_nu(BM, NT)][8]) {
+                const int64_t k0 = kb + kt * X6_BK;
+                x6_load<1, BM, NT, FULL>(plane_base(g.A, k0, g.a_blk, g.a_pstride), g.lda, g.M, m0, k0, ke, a_vec, v, t);
+            };
+            auto mma = [&](int cur, const uint4 (&b)[2][TN][NP]) {
+#pragma unroll
+                for (int kk = 0; kk < X6_BK / 16; ++kk) {
+                    uint4 a[TM][NP];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            a[i][p] = As[cur][p * BM * 4 + x6_pos(wm * (BM / WM) + i * 32 + li, 2 * kk + lh)];
+                    if constexpr (ABL != 11) x6_mma<TM, TN, PREC, NP>(acc, a, b[kk]);
+                }
+            };
+            auto step = [&](int64_t kt, float (&va)[x6_nu(BM, NT)][8], const uint4 (&bc)[2][TN][NP],
+                            uint4 (&bnx)[2][TN][NP]) {
+                const int cur = (int)(kt & 1);
+                if (kt + 1 < nk) x6_store<1, BM, NT, PREC, 0>(As[cur ^ 1], va, t, sa);
+                if (kt + 3 < nk) load_a(kt + 3, va);
+                if (kt + 1 < nk) load_b(kt + 1, bnx);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(cur, bc);
+                __syncthreads();
+            };
+            if (nk > 0) {
+                load_a(0, ra[0]);
+                x6_store<1, BM, NT, PREC, 0>(As[0], ra[0], t, sa);
+                load_b(0, rb[0]);
+                if (nk > 1) load_a(1, ra[1]);
+                if (nk > 2) load_a(2, ra[0]);
+            }
+            __syncthreads();
+            int64_t kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                step(kt, ra[1], rb[0], rb[1]);
+                step(kt + 1, ra[0], rb[1], rb[0]);
+            }
+            if (kt < nk) step(kt, ra[1], rb[0], rb[1]);
+        };
+        if (full) wr_loop(std::integral_constant<int, 1>{});
+        else wr_loop(std::integral_constant<int, 0>{});
+    } else if constexpr ((PPV & 1) != 0) {
         static_assert(PREC == 1 && AK && BKc && ABL != 7, "ping-pong: f16x3 with K-contiguous A and B");
         constexpr int NTG = NT / 2, RA = BM / 2, RB = BN / 2;
         static_assert(RA * 4 % NTG == 0 && RB * 4 % NTG == 0 && (WM * WN) % 2 == 0 && (WM % 2 == 0 || WM == 1),
@@ -633,10 +711,15 @@ template <int PREC, int TA, int TB, int ABL>
 inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if constexpr (PREC == 1 && TA == 0 && TB == 1 && (ABL == 0 || ABL == 8)) {
         if (g.wb) {   // pre-split B image (bgnn_gemm_f32_w): tiles with BN = the image's column tile
+            if (gemm_pp() == 4) {   // B fragments in registers (BGNN_TUNE_GEMM_PP = 4)
+                if (cfg == 1) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 8>), grid, dim3(512), 0, s, g); return; }
+                if (cfg == 2) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 8>), grid, dim3(512), 0, s, g); return; }
+            }
             switch (cfg) {
                 case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;
                 case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
                 case 3: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
+                case 5: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 320, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
                 default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;
             }
         }

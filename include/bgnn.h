@@ -86,7 +86,10 @@ const char* bgnn_last_error_string(void);
                                     = ping-pong main loop (the two waves of a SIMD alternate MFMA
                                     and staging half steps), bit 1 = line-major staging loads
                                     (whole 128-B lines per wave load); 0 = neither (default:
-                                    both measured slower, profiles/r05_ab_gemm_*). Bit-identical. */
+                                    both measured slower, profiles/r05_ab_gemm_*); 4 = the
+                                    pre-split weight path (bgnn_gemm_f32_w) on 128x256 / 256x128
+                                    tiles loads B's MFMA fragments straight from the image into
+                                    registers instead of through LDS. Bit-identical. */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose
@@ -405,13 +408,17 @@ int bgnn_gemm_f32_dropadd(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N
                           const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                           const float* a_amax, const float* b_amax, const float* src, int64_t ld_src,
                           float p, uint64_t seed, void* ws, size_t ws_bytes, void* stream);
+#define BGNN_WSPLIT_FRAG 0x10000
 /* Pre-split weights (round 5). The f16x3 GEMM C = A W^T of the SAGE layers (forward z = x
  * [W_l;W_r]^T, input gradient dx = dz [W_l;W_r]) takes its weight operand W [N, K] as a
  * pre-split image: W scaled by the power of two of max|W| (amax) and split into two f16 pieces
  * once per step (bgnn_gemm_wsplit, n_items matrices of one shape in one launch: W_i at W + i *
  * item_stride, max|W_i| at amax[i * amax_stride], image i at img + i * img_stride bytes), stored
  * per (column tile of bn rows, 32-deep K slice) as the GEMM's own LDS image, so the GEMM copies
- * it into LDS by LDS-DMA instead of loading, splitting and storing it in every row tile. The
+ * it into LDS (16-B register copies) instead of loading, splitting and storing it in every row
+ * tile. bn | BGNN_WSPLIT_FRAG stores each slice in MFMA-fragment order instead ([32-column
+ * block][k16 step][piece][64 lanes x 16 B]), the layout the B-in-registers variant
+ * (BGNN_TUNE_GEMM_PP = 4, measurement) loads with one 1-KiB load per wave and fragment. The
  * product is bit-identical to bgnn_gemm_f32_scaled / bgnn_gemm_f32_dropadd on the same operands.
  *   bgnn_gemm_w_tile(M, N, K): the column tile bn the image must use for that GEMM shape, or 0
  *     when the shape has no pre-split path (then use bgnn_gemm_f32_scaled);

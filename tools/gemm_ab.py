@@ -8,7 +8,9 @@ with a 1 GiB cache flush between launches (cold L2 / Infinity Cache, as inside a
 A variant "xC" runs tile config C % 100 with timing ablation C // 100 (bgnn_gemm_set_cfg; x-1 =
 the automatic plan); "pC" the same with the ping-pong main loop (BGNN_TUNE_GEMM_PP = 1), "lC" with
 line-major staging loads (2), "qC" with both (3); "w" the pre-split weight path (bgnn_gemm_wsplit +
-bgnn_gemm_f32_w, LDS-DMA staging of the weight operand).
+bgnn_gemm_f32_w, the weight image copied into LDS), "d" the same with the drop-add epilogue (src = a
+[M, N] gradient, p = 0.1: the skip layers' dgrad); "r" / "s" as "w" / "d" with B's MFMA fragments
+loaded from the image into registers (BGNN_TUNE_GEMM_PP = 4).
 """
 import argparse
 import os
@@ -40,16 +42,17 @@ def main():
         b = torch.randn(N, K, device=dev) * 0.05
         am = torch.stack([a.abs().max(), b.abs().max()]).contiguous()
         out = torch.empty(M, N, device=dev)
+        src = torch.randn(M, N, device=dev)
         ref = None
         for vs in args.variants.split(","):
             wimg = None
-            if vs[0] == "w":   # pre-split weight image + bgnn_gemm_f32_w ("wC": tile config C)
+            if vs[0] in "wdrs":   # pre-split weight image + bgnn_gemm_f32_w ("wC": tile config C)
                 _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if len(vs) > 1 else -1)
-                _lib.call("bgnn_set_tuning", 14, 0)
+                _lib.call("bgnn_set_tuning", 14, 4 if vs[0] in "rs" else 0)
                 bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
                 wimg = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
                 _lib.call("bgnn_gemm_wsplit", b.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, wimg.data_ptr(),
-                          wimg.numel(), bn, fused._stream())
+                          wimg.numel(), bn | (0x10000 if vs[0] in "rs" else 0), fused._stream())
             else:
                 _lib.call("bgnn_gemm_set_cfg", int(vs[1:]))
                 _lib.call("bgnn_set_tuning", 14, {"x": 0, "p": 1, "l": 2, "q": 3}[vs[0]])   # BGNN_TUNE_GEMM_PP
@@ -61,8 +64,8 @@ def main():
                 e0.record()
                 if wimg is not None:
                     _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, wimg.data_ptr(), bn, out.data_ptr(), N,
-                              None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None, None, 0, 0.0, 0,
-                              fused._stream())
+                              None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None,
+                              src.data_ptr() if vs[0] in "ds" else None, N, 0.1, 1234, fused._stream())
                 else:
                     fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 e1.record()
