@@ -201,7 +201,9 @@ def test_pyg_shim_binds_fused_model_class():
             assert ref_cls is not bgnn.BuckGNN and ref_cls.__module__ == "Models.BuckGNN"
             kw = dict(hidden_channels=64, num_layers=6, pooling_layer="mean", dropout_rate=0.1,
                       model_name="GraphSage_addAggr_Shared")
-            assert list(BuckGNN(16, 5, **kw).state_dict()) == list(ref_cls(16, 5, **kw).state_dict())
+            ours, ref = BuckGNN(16, 5, **kw), ref_cls(16, 5, **kw)
+            assert list(ours.state_dict()) == list(ref.state_dict())
+            ours.load_state_dict(ref.state_dict())   # a reference checkpoint loads unchanged (strict)
         finally:
             bgnn.uninstall_pyg_shim()
         assert M.BuckGNN is ref_cls
