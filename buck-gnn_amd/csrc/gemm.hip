@@ -420,7 +420,13 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.prec = 1;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
         if (p.cfg == kX6CfgWB && !wb) p.cfg = 4;   // (the 320-row tile exists for pre-split B only)
-        if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
+        // plane blocks must be whole tiles: fall back to an 8-wave tile that divides them (the
+        // 16x16x32 MFMA family, the same rounding as the dense layout's), else the 128x128 tile
+        if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) {
+            p.cfg = 0;
+            for (int c = 1; c <= 2; ++c)
+                if (planes_ok(kX6Cfgs[c].bm, kX6Cfgs[c].bn, 32)) { p.cfg = c; break; }
+        }
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves,
                                                  kX6Cfgs[p.cfg].blocks_per_cu});

@@ -5,6 +5,7 @@
 namespace bgnn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
     const float* A;

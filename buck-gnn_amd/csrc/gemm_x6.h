@@ -71,8 +71,35 @@ __device__ __forceinline__ void st_bf16x4(float* p, const float (&e)[4]) {
     *reinterpret_cast<uint2*>(p) = q;
 }
 
-template <int TM, int TN, int ABL = 0, bool C16 = false>
-__device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
+// the accumulators of column block j into the wave's LDS stage [TM*32][32]: 32x32x16 MFMA tiles
+// (C/D map col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)) ...
+template <int TM, int TN>
+__device__ __forceinline__ void x6_stage_write(float* __restrict__ stage, const floatx16 (&acc)[TM][TN], int j,
+                                               int lane) {
+    const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+}
+// ... or 16x16x32 MFMA tiles, four per 32x32 block (C/D map col = lane & 15, row = 4 (lane >> 4) + r)
+template <int TM, int TN>
+__device__ __forceinline__ void x6_stage_write(float* __restrict__ stage, const floatx4 (&acc)[2 * TM][2 * TN], int j,
+                                               int lane) {
+    const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int si = 0; si < 2; ++si)
+#pragma unroll
+            for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    stage[(i * 32 + si * 16 + 4 * lq + r) * 32 + sj * 16 + l16] = acc[2 * i + si][2 * j + sj][r];
+}
+
+template <int TM, int TN, int ABL = 0, bool C16 = false, typename Acc>
+__device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
                                             int64_t c0, int64_t n0, int ks, int lane, float ia, float ib,
                                             float* __restrict__ stage) {
     const bool split = g.split > 1;
@@ -85,7 +112,6 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
     const int64_t ldd = split ? g.N : g.ldc;
     const bool vec = (((uintptr_t)dst & 15) == 0) && (ldd % 4 == 0);
     const bool bias_vec = g.bias && (((uintptr_t)g.bias & 15) == 0);
-    const int li = lane & 31, lh = lane >> 5;
     const int rq = lane >> 3, c4 = (lane & 7) * 4;
     uint32_t cmax = 0;
     // interior tile, no split-K, aligned: per-column-block bias and pointer, per-row pointer
@@ -115,10 +141,7 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const floatx16 (&
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+        x6_stage_write<TM, TN>(stage, acc, j, lane);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (fast) {
             const int64_t col = c0 + j * 32 + c4;

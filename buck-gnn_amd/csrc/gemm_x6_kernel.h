@@ -3,6 +3,7 @@
 // gemm_x6_other.hip, gemm_x6_b16s.hip): one TU per instantiation family keeps the build parallel.
 #pragma once
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 #include "gemm_common.h"
@@ -17,8 +18,14 @@ constexpr int X6_BK = 32;
 // first threads only (a wave-uniform guard)
 constexpr int x6_nu(int R, int NT) { return (R * 4 + NT - 1) / NT; }
 
-// 16-B chunk index of (row, chunk) in a [R][32]-bf16 image
-__device__ __forceinline__ int x6_pos(int row, int chunk) { return row * 4 + (chunk ^ ((row >> 2) & 3)); }
+// 16-B chunk index of (row, chunk) in a [R][32]-bf16 image: the chunks of row r are permuted by
+// chunk ^ h((r >> 2) & 3) with h = (0, 2, 3, 1), which keeps both MFMA fragment reads conflict-free
+// -- 32x32x16 (lane = row, lane >> 5 = chunk within the k16 half) and 16x16x32 (lane & 15 = row,
+// lane >> 4 = chunk) -- and the row-major unit stores (any per-row permutation is). (Round 4's
+// h = identity left the 16x16x32 reads 2-way conflicted.)
+__device__ __forceinline__ int x6_pos(int row, int chunk) {
+    return row * 4 + (chunk ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3));
+}
 
 // One staging unit = 8 consecutive k of one row r (r = m or n) of the tile.
 //   KCONTIG = 1: element (r, k) at P[r * ld + k];   unit idx -> r = idx / 4, chunk = idx % 4
@@ -324,16 +331,37 @@ __device__ __forceinline__ void x6_mma(floatx16 (&acc)[TM][TN], const uint4 (&fa
             floatx16 t = acc[i][j];
             if constexpr (PREC == 2) {   // bf16 operands: one product
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[i][0]), as_bf16x8(fb[j][0]), t, 0, 0, 0);
-                continue;
+            } else {   // f16x3: the two cross terms, then the leading product
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][0]), t, 0, 0, 0);
+                acc[i][j] = t;
             }
-            // f16x3: the two cross terms, then the leading product
-            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][1]), t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][1]), as_f16x8(fb[j][0]), t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_f16x8(fa[i][0]), as_f16x8(fb[j][0]), t, 0, 0, 0);
-            acc[i][j] = t;
         }
 }
 
+
+// Interleaved schedule of one steady-state pipeline step of the pre-split-B GEMM (PPV bit 4):
+// the step's instructions form one basic block -- the LDS fragment reads of both k16 halves of
+// slice kt, the split and LDS writes of slice kt+1, the global loads of slice kt+1+PF and the
+// MFMAs of slice kt -- and sched_group_barrier spreads the staging between the MFMAs (per MFMA:
+// up to one fragment read of the second half, VPM VALU, one LDS write, one global load), so a
+// wave's MFMA stream carries its own staging instead of leaving the matrix pipe to the partner
+// wave while it stages (one MFMA gap hides about five single-issue instructions; guide
+// MI355X_MICROARCH.md, cycle constants).
+template <int I, int NR, int NW, int NV, int VPM>
+__device__ __forceinline__ void x6_il_one() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                    // one MFMA
+    if constexpr (I < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // a fragment read
+    __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);                  // VALU (the split)
+    if constexpr (I >= 2 && I - 2 < NW) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // LDS write
+    if constexpr (I >= NR && I - NR < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0); // global load
+}
+template <int NR0, int NR, int NW, int NV, int VPM, int... I>
+__device__ __forceinline__ void x6_il_schedule(std::integer_sequence<int, I...>) {
+    __builtin_amdgcn_sched_group_barrier(0x100, NR0, 0);   // the first half's fragment reads
+    (x6_il_one<I, NR, NW, NV, VPM>(), ...);
+}
 
 // ABL (timing ablations only, wrong results): 1 = no split arithmetic (piece 0 stored in
 // every piece slot), 2 = no global loads, 3 = no staging at all (LDS reads + MFMA +
@@ -364,6 +392,18 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
     // PPV bit 2: B arrives pre-split (bgnn_gemm_wsplit): its LDS image is copied, not split
     constexpr bool kWB = (PPV & 4) != 0;
+    // PPV bit 4 (with bit 2): the steady-state steps run the interleaved schedule (x6_il_schedule)
+    constexpr bool kIL = (PPV & 16) != 0;
+    // f16x3 main loops run 16x16x32 MFMAs (four per 32x32 block, one per 32-deep slice; round 5):
+    // the same cycles per FLOP as 32x32x16, but the chip holds a higher clock under them (guide
+    // MI355X_MICROARCH.md, DVFS item 7): isolated dgrad 274 -> 258 us, drop-add dgrad 314 -> 303,
+    // forward 277 -> 263 (profiles/r05_ab_gemm_m16.txt). The 8-wave tiles of the large GEMMs only:
+    // the 4-wave 128x128 tile of the small products (the folded encoder's weight products, the
+    // EA_GNN node blocks at small N) keeps 32x32x16 and its rounding (tests/test_gpu_fold.py
+    // measures the folded path's gradients against fp64 relative to the unfolded path's). PPV bit 5
+    // keeps 32x32x16 (A/B), as do the ping-pong, line-major, interleaved and B-in-registers variants.
+    constexpr bool kM16 = PREC == 1 && NT == 512 && (PPV & 32) == 0 && (PPV & (1 | 2 | 8 | 16)) == 0;
+
     // (pre-split B: A may have a unit count that is no multiple of NT, x6_nu's guarded last unit)
     static_assert((BM * 4 % NT == 0 || kWB) && BN * 4 % NT == 0, "staging units must divide evenly");
     // PPV bit 3: B's MFMA fragments are loaded straight from the pre-split image into registers
@@ -371,6 +411,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr bool kWR = (PPV & 8) != 0;
     static_assert(!kWR || (PREC == 1 && AK && BKc && !A16 && !B16 && (PPV & 7) == 0 && ABL != 7),
                   "B in registers: f16x3 NT on a pre-split image");
+
     // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
     // epilogue as one [TM*32][32] f32 stage per wave
     constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
@@ -407,13 +448,21 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         h3_scale(*g.b_amax, sb, ib);
     }
 
-    floatx16 acc[TM][TN];
+    floatx16 acc[kM16 ? 1 : TM][kM16 ? 1 : TN];
+    floatx4 acc4[kM16 ? 2 * TM : 1][kM16 ? 2 * TN : 1];
+    if constexpr (kM16) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < 2 * TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+            for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
 
     constexpr bool KQ = !AK && !BKc && PREC >= 1 && ABL != 7 && BM + BN <= NT && BM % 64 == 0 && BN % 64 == 0 &&
                         BM * BN >= 256 * 128;   // (128x128: measured slower than the dword path)
@@ -459,7 +508,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
                 if (t < BM) kq_load<BM, FULL, A16, KT>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
                 else if (t < BM + BN) kq_load<BN, FULL, B16, KT>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
             } else if constexpr (kWB) {   // B: the image of slice k0 / 32 of column tile tn
-                x6_load<1, BM, NT, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
+                // (bgnn_gemm_f32_w passes a dense A: no plane split, no branch in the step)
+                x6_load<1, BM, NT, FULL>(g.A, g.lda, g.M, m0, k0, ke, a_vec, r.a, t);
                 const uint4* img = reinterpret_cast<const uint4*>(g.B) + (tn * (g.K / X6_BK) + k0 / X6_BK) * (BN * 8);
 #pragma unroll
                 for (int q = 0; q < BN * 8 / NT; ++q) r.b[q] = img[t + NT * q];
@@ -492,6 +542,41 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         };
         const int li = lane & 31, lh = lane >> 5;
         auto mma_slice = [&](int cur, int64_t kt) {
+            if constexpr (kM16) {   // one 32-deep step: 16-row fragments, chunk = lane >> 4
+                // the side with fewer 16-row blocks is held whole, the other streamed block by block
+                // (both whole would need 24 fragments = 96 VGPRs at 256x256 and spill)
+                const int l16 = lane & 15, lq = lane >> 4;
+                auto fa = [&](int i, int p) { return As[cur][p * BM * 4 + x6_pos(wm * (BM / WM) + i * 16 + l16, lq)]; };
+                auto fb = [&](int j, int p) { return Bs[cur][p * BN * 4 + x6_pos(wn * (BN / WN) + j * 16 + l16, lq)]; };
+                auto mma3 = [&](floatx4& t, const uint4 (&a)[2], const uint4 (&b)[2]) {
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[1]), t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[1]), as_f16x8(b[0]), t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[0]), t, 0, 0, 0);
+                };
+                if constexpr (TM <= TN) {
+                    uint4 a[2 * TM][2];
+#pragma unroll
+                    for (int i = 0; i < 2 * TM; ++i) { a[i][0] = fa(i, 0); a[i][1] = fa(i, 1); }
+#pragma unroll
+                    for (int j = 0; j < 2 * TN; ++j) {
+                        const uint4 b[2] = {fb(j, 0), fb(j, 1)};
+#pragma unroll
+                        for (int i = 0; i < 2 * TM; ++i)
+                            if constexpr (ABL != 11) mma3(acc4[i][j], a[i], b);
+                    }
+                } else {
+                    uint4 b[2 * TN][2];
+#pragma unroll
+                    for (int j = 0; j < 2 * TN; ++j) { b[j][0] = fb(j, 0); b[j][1] = fb(j, 1); }
+#pragma unroll
+                    for (int i = 0; i < 2 * TM; ++i) {
+                        const uint4 a[2] = {fa(i, 0), fa(i, 1)};
+#pragma unroll
+                        for (int j = 0; j < 2 * TN; ++j)
+                            if constexpr (ABL != 11) mma3(acc4[i][j], a, b[j]);
+                    }
+                }
+            } else {
 #pragma unroll
             for (int kk = 0; kk < X6_BK / 16; ++kk) {
                 uint4 a[TM][NP], b[TN][NP];
@@ -516,6 +601,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
                 if constexpr (ABL != 11) x6_mma<TM, TN, PREC, NP>(acc, a, b);
                 else if (kt < 0) x6_mma<TM, TN, PREC, NP>(acc, a, b);   // (keeps the reads live)
             }
+            }
         };
         // one pipeline step: split slice kt+1 (register set S) into LDS buffer (kt+1)&1, refill
         // set S with slice kt+1+PF, multiply slice kt, barrier. S = (kt+1) & 1 for PF = 2.
@@ -528,6 +614,42 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             mma_slice(cur, kt);
             __syncthreads();
         };
+        // steady-state step of the interleaved schedule (kIL): slice kt+1 is stored and slice
+        // kt+1+PF loaded unconditionally, one basic block; the four buffers are restrict-qualified
+        // so the writes to buffer cur^1 may move among the reads of buffer cur
+        auto step_il = [&](const uint4* __restrict__ ard, const uint4* __restrict__ brd, uint4* __restrict__ awr,
+                           uint4* __restrict__ bwr, int64_t k_next, Regs& r) {
+            if constexpr (kWB && kIL) {
+                uint4 fa[2][TM][NP], fb[2][TN][NP];
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            fa[kk][i][p] = ard[p * BM * 4 + x6_pos(wm * (BM / WM) + i * 32 + li, 2 * kk + lh)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int p = 0; p < NP; ++p)
+                            fb[kk][j][p] = brd[p * BN * 4 + x6_pos(wn * (BN / WN) + j * 32 + li, 2 * kk + lh)];
+                }
+                x6_store<1, BM, NT, PREC, ABL>(awr, r.a, t, sa);
+#pragma unroll
+                for (int q = 0; q < BN * 8 / NT; ++q) bwr[t + NT * q] = r.b[q];
+                load_ab(k_next, r);
+                x6_mma<TM, TN, PREC, NP>(acc, fa[0], fb[0]);
+                x6_mma<TM, TN, PREC, NP>(acc, fa[1], fb[1]);
+                constexpr int NM = 2 * TM * TN * 3, NR0 = (TM + TN) * NP;
+                constexpr int NW = x6_nu(BM, NT) * 2 + BN * 8 / NT, NV = x6_nu(BM, NT) * 2 + BN * 8 / NT;
+                x6_il_schedule<NR0, NR0, NW, NV, 2>(std::make_integer_sequence<int, NM>{});
+            }
+        };
+        auto il = [&](int64_t kt, Regs& r) {
+            const int cur = (int)(kt & 1);
+            step_il(As[cur], Bs[cur], As[cur ^ 1], Bs[cur ^ 1], kb + (kt + 1 + PF) * X6_BK, r);
+            __syncthreads();
+        };
         if (nk > 0) {
             load_ab(kb, rs[0]);
             store_ab(0, rs[0]);
@@ -537,13 +659,23 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         __syncthreads();
         if constexpr (PF == 2) {
             int64_t kt = 0;
+            if constexpr (kWB && kIL) {
+                for (; kt + 2 + PF < nk; kt += 2) {
+                    il(kt, rs[1]);
+                    il(kt + 1, rs[0]);
+                }
+            }
             for (; kt + 1 < nk; kt += 2) {
                 step(kt, rs[1]);
                 step(kt + 1, rs[0]);
             }
             if (kt < nk) step(kt, rs[1]);
         } else {
-            for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
+            int64_t kt = 0;
+            if constexpr (kWB && kIL) {
+                for (; kt + 1 + PF < nk; ++kt) il(kt, rs[1]);
+            }
+            for (; kt < nk; ++kt) step(kt, rs[1]);
         }
     };
     if constexpr (kWR) {
@@ -704,13 +836,32 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     }
     // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
-    x6_epilogue<TM, TN, ABL, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
+    if constexpr (kM16)
+        x6_epilogue<TM, TN, ABL, C16>(g, acc4, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
+    else
+        x6_epilogue<TM, TN, ABL, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
 }
 
 template <int PREC, int TA, int TB, int ABL>
 inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if constexpr (PREC == 1 && TA == 0 && TB == 1 && (ABL == 0 || ABL == 8)) {
         if (g.wb) {   // pre-split B image (bgnn_gemm_f32_w): tiles with BN = the image's column tile
+            if (gemm_pp() == 6) {   // 32x32x16 MFMAs, the form before round 5's default (BGNN_TUNE_GEMM_PP = 6)
+                switch (cfg) {
+                    case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 36>), grid, dim3(512), 0, s, g); return;
+                    case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 36>), grid, dim3(512), 0, s, g); return;
+                    case 3: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL, 36>), grid, dim3(512), 0, s, g); return;
+                    case 4: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 36>), grid, dim3(512), 0, s, g); return;
+                    default: break;
+                }
+            }
+            if (gemm_pp() == 5) {   // interleaved schedule (BGNN_TUNE_GEMM_PP = 5; 256x256: spills)
+                switch (cfg) {
+                    case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 20>), grid, dim3(512), 0, s, g); return;
+                    case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 20>), grid, dim3(512), 0, s, g); return;
+                    default: break;
+                }
+            }
             if (gemm_pp() == 4) {   // B fragments in registers (BGNN_TUNE_GEMM_PP = 4)
                 if (cfg == 1) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 8>), grid, dim3(512), 0, s, g); return; }
                 if (cfg == 2) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 8>), grid, dim3(512), 0, s, g); return; }

@@ -1342,7 +1342,7 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
         case BGNN_TUNE_GEMM_PP:
-            BGNN_REQUIRE(value >= 0 && value <= 4, "set_tuning: gemm staging variant must be 0..4");
+            BGNN_REQUIRE(value >= 0 && value <= 6, "set_tuning: gemm staging variant must be 0..6");
             set_gemm_pp(value);
             return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:

@@ -89,7 +89,11 @@ const char* bgnn_last_error_string(void);
                                     both measured slower, profiles/r05_ab_gemm_*); 4 = the
                                     pre-split weight path (bgnn_gemm_f32_w) on 128x256 / 256x128
                                     tiles loads B's MFMA fragments straight from the image into
-                                    registers instead of through LDS. Bit-identical. */
+                                    registers instead of through LDS, 5 = an interleaved
+                                    steady-state schedule (staging spread between the MFMAs),
+                                    6 = 32x32x16 MFMAs instead of the 16x16x32 default. 0..5 are
+                                    bit-identical to each other; 6 differs within the f16x3 error
+                                    class (another summation order inside the matrix core). */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose

@@ -10,7 +10,8 @@ the automatic plan); "pC" the same with the ping-pong main loop (BGNN_TUNE_GEMM_
 line-major staging loads (2), "qC" with both (3); "w" the pre-split weight path (bgnn_gemm_wsplit +
 bgnn_gemm_f32_w, the weight image copied into LDS), "d" the same with the drop-add epilogue (src = a
 [M, N] gradient, p = 0.1: the skip layers' dgrad); "r" / "s" as "w" / "d" with B's MFMA fragments
-loaded from the image into registers (BGNN_TUNE_GEMM_PP = 4).
+loaded from the image into registers (BGNN_TUNE_GEMM_PP = 4); "i" / "j" as "w" / "d" with the interleaved
+steady-state schedule (BGNN_TUNE_GEMM_PP = 5); "m" / "n" with 16x16x32 MFMAs (BGNN_TUNE_GEMM_PP = 6).
 """
 import argparse
 import os
@@ -46,9 +47,9 @@ def main():
         ref = None
         for vs in args.variants.split(","):
             wimg = None
-            if vs[0] in "wdrs":   # pre-split weight image + bgnn_gemm_f32_w ("wC": tile config C)
+            if vs[0] in "wdrsijmn":   # pre-split weight image + bgnn_gemm_f32_w ("wC": tile config C)
                 _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if len(vs) > 1 else -1)
-                _lib.call("bgnn_set_tuning", 14, 4 if vs[0] in "rs" else 0)
+                _lib.call("bgnn_set_tuning", 14, {"r": 4, "s": 4, "i": 5, "j": 5, "m": 6, "n": 6}.get(vs[0], 0))
                 bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
                 wimg = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
                 _lib.call("bgnn_gemm_wsplit", b.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, wimg.data_ptr(),
@@ -65,7 +66,7 @@ def main():
                 if wimg is not None:
                     _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, wimg.data_ptr(), bn, out.data_ptr(), N,
                               None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None,
-                              src.data_ptr() if vs[0] in "ds" else None, N, 0.1, 1234, fused._stream())
+                              src.data_ptr() if vs[0] in "dsjn" else None, N, 0.1, 1234, fused._stream())
                 else:
                     fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 e1.record()
