@@ -142,6 +142,8 @@ SIGNATURES = {
                               c_sz, c_p]),
     "bgnn_gemm_f32_dropadd": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p,
                                       c_p, c_p, c_i64, c_f32, c_u64, c_p, c_sz, c_p]),
+    "bgnn_gemm_f32_dropadd_cols": (c_i32, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p,
+                                           c_i64, c_i64, c_f32, c_u64, c_p, c_sz, c_p]),
     "bgnn_add_dropout": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p, c_p]),
     "bgnn_gemm_f32": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,
                               c_p, c_sz, c_p]),

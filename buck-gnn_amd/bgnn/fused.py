@@ -54,6 +54,9 @@ BF16_PREP = True
 ABSMAX_ITEMS = True
 # [W_l;W_r] of all layers packed by a multi-tensor copy into a persistent buffer (not torch.cat)
 PERSISTENT_WPACK = True
+# max aggregation: the two input-gradient products as one GEMM [dh W_l | dh W_r (+ drop(g))] and
+# the two weight gradients as one [agg | x]^T dh (A/B switch)
+MAX_MERGED = True
 # forward / input-gradient GEMMs of the K = H layers take [W_l;W_r] (and its transpose) as images
 # pre-split once per step (bgnn_gemm_wsplit), staged by LDS-DMA in the GEMM (bgnn_gemm_f32_w);
 # bit-identical to the register-staged path (A/B switch)
@@ -902,13 +905,39 @@ def _max_backward(dh, dz_amax, wcat_t, x, agg, arg, graph: Graph, x_amax, w_amax
     wcat_t = [W_l ; W_r]^T ([C, 2H]); addend_beta_src: the skip connection's incoming gradient g
     (added through its dropout mask in the dW_r product's epilogue) or None."""
     N, H = dh.shape
+    C = x.size(1)
     dev = dh.device
     dx = None
-    if need_dx:
+    hip16 = GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) == 2
+    if need_dx and MAX_MERGED and hip16 and C % 256 == 0:
+        # one GEMM [dagg | t] = dh [W_l | W_r] (B^T = [W_l^T ; W_r^T], [2C, H]), the skip layers'
+        # drop(g) added to the t columns only (bgnn_gemm_f32_dropadd_cols): one launch at N = 2C
+        # instead of two at N = C
+        wkt = torch.cat([wcat_t[:, :H], wcat_t[:, H:]], 0)          # [W_l^T ; W_r^T]
+        with _timed("gemm_dgrad"):
+            dt = torch.empty(N, 2 * C, dtype=torch.float32, device=dev)
+            if addend_beta_src is not None:
+                ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", N, 2 * C, H, 0, 1, 0)
+                ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
+                _lib.call("bgnn_gemm_f32_dropadd_cols", N, 2 * C, H, dh.data_ptr(), dh.stride(0), wkt.data_ptr(), H,
+                          dt.data_ptr(), 2 * C, dz_amax.data_ptr(), w_amax.data_ptr(), addend_beta_src.data_ptr(),
+                          addend_beta_src.stride(0), C, float(p), seed, _ptr(ws), ws_bytes, _stream())
+            else:
+                gemm(dh, wkt, trans_a=False, trans_b=True, out=dt, a_amax=dz_amax, b_amax=w_amax)
+        dagg, t = dt[:, :C], dt[:, C:]
+        dx = torch.empty(N, C, dtype=torch.float32, device=dev)
+        bw = graph.bwd
+        part = torch.empty(bw.plan.n_chunks * C, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
+        with _timed("spmm_bwd"):
+            _lib.call("bgnn_spmm_bwd_max", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(), N,
+                      dagg.data_ptr(), 2 * C, C, arg.data_ptr(), t.data_ptr(), 2 * C,
+                      dx.data_ptr(), dx.stride(0), _ptr(part), None, _stream())
+        del dt, dagg, t
+    elif need_dx:
         wl_t, wr_t = wcat_t[:, :H], wcat_t[:, H:]                    # W_l^T, W_r^T: [C, H], ld 2H
         with _timed("gemm_dgrad"):
             dagg = gemm(dh, wl_t, trans_a=False, trans_b=True, a_amax=dz_amax, b_amax=w_amax)
-            if addend_beta_src is not None and GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) == 2:
+            if addend_beta_src is not None and hip16:
                 t = torch.empty(N, wcat_t.size(0), dtype=torch.float32, device=dev)
                 ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", N, t.size(1), H, 0, 1, 0)
                 ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev) if ws_bytes else None
@@ -928,8 +957,15 @@ def _max_backward(dh, dz_amax, wcat_t, x, agg, arg, graph: Graph, x_amax, w_amax
                       dagg.data_ptr(), dagg.stride(0), x.size(1), arg.data_ptr(), t.data_ptr(), t.stride(0),
                       dx.data_ptr(), dx.stride(0), _ptr(part), None, _stream())
     with _timed("gemm_wgrad"):
-        dw_l = gemm(dh, agg, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
-        dw_r = gemm(dh, x, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
+        if (MAX_MERGED and GEMM_BACKEND == "hip" and C % 256 == 0 and agg.shape == x.shape
+                and agg.stride() == x.stride() and (x.data_ptr() - agg.data_ptr()) % 16 == 0):
+            # [dW_l^T ; dW_r^T] = [agg | x]^T dh in one GEMM ([agg | x] read in place as two planes
+            # of the M dimension; max|[agg | x]| = max|x|)
+            dwt = gemm(Pair(agg, x), dh, trans_a=True, trans_b=False, a_amax=x_amax, b_amax=dz_amax)   # [2C, H]
+            dw_l, dw_r = dwt[:C].t(), dwt[C:].t()
+        else:
+            dw_l = gemm(dh, agg, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
+            dw_r = gemm(dh, x, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)
     return dx, dw_l, dw_r
 
 

@@ -516,6 +516,7 @@ struct BetaSrc {
     int64_t ld;
     uint64_t seed;
     float p;
+    int64_t c0;   // first column that takes it (bgnn_gemm_f32_dropadd_cols)
 };
 
 static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha,
@@ -533,7 +534,7 @@ extern "C" int bgnn_gemm_f32_scaled(int32_t ta, int32_t tb, int64_t M, int64_t N
                                     size_t ws_bytes, void* stream) {
     return gemm_scaled_impl(ta, tb, M, N, K, alpha, A, lda, a_blk, a_pstride, B, ldb, beta, C, ldc, c_blk,
                             c_pstride, bias, relu, a_amax, b_amax, c_amax, precision, ws, ws_bytes, stream,
-                            BetaSrc{nullptr, 0, 0, 0.f});
+                            BetaSrc{nullptr, 0, 0, 0.f, 0});
 }
 
 extern "C" int bgnn_gemm_f32_dropadd(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
@@ -545,7 +546,23 @@ extern "C" int bgnn_gemm_f32_dropadd(int32_t ta, int32_t tb, int64_t M, int64_t 
     BGNN_REQUIRE(gemm_mode() == 2 && ta == 0 && tb == 1,
                  "gemm_dropadd: built for the f16x3 family (BGNN_TUNE_GEMM_MODE 2) and C = A B^T only");
     return gemm_scaled_impl(ta, tb, M, N, K, 1.f, A, lda, 0, 0, B, ldb, 1.f, C, ldc, 0, 0, nullptr, 0, a_amax,
-                            b_amax, nullptr, 0, ws, ws_bytes, stream, BetaSrc{src, ld_src, seed, p});
+                            b_amax, nullptr, 0, ws, ws_bytes, stream, BetaSrc{src, ld_src, seed, p, 0});
+}
+
+extern "C" int bgnn_gemm_f32_dropadd_cols(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                          const float* B, int64_t ldb, float* C, int64_t ldc, const float* a_amax,
+                                          const float* b_amax, const float* src, int64_t ld_src, int64_t src_col0,
+                                          float p, uint64_t seed, void* ws, size_t ws_bytes, void* stream) {
+    BGNN_REQUIRE(src != nullptr && src_col0 >= 0 && src_col0 < N && ld_src >= N - src_col0 && ld_src % 4 == 0 &&
+                     N % 4 == 0 && ((uintptr_t)src & 15) == 0,
+                 "gemm_dropadd_cols: src must be 16-byte aligned, cover columns [src_col0, N), ld_src % 4 == 0");
+    BGNN_REQUIRE(gemm_mode() == 2, "gemm_dropadd_cols: built for the f16x3 family (BGNN_TUNE_GEMM_MODE 2)");
+    const Plan pl = make_plan(M, N, K, 0, 1, 0, 0);
+    BGNN_REQUIRE(pl.x6 && pl.split == 1 && src_col0 % pl.bn == 0,
+                 "gemm_dropadd_cols: src_col0 %lld must be a multiple of the column tile %d (no split-K)",
+                 (long long)src_col0, pl.bn);
+    return gemm_scaled_impl(0, 1, M, N, K, 1.f, A, lda, 0, 0, B, ldb, 1.f, C, ldc, 0, 0, nullptr, 0, a_amax, b_amax,
+                            nullptr, 0, ws, ws_bytes, stream, BetaSrc{src, ld_src, seed, p, src_col0});
 }
 
 extern "C" int32_t bgnn_gemm_w_tile(int64_t M, int64_t N, int64_t K) {
@@ -606,7 +623,15 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
     BGNN_REQUIRE(a_blk >= 0 && c_blk >= 0, "gemm: negative plane block");
     BGNN_REQUIRE(precision == 0 || precision == 1, "gemm: precision must be 0 (f32-accurate) or 1 (bf16)");
     if (M == 0 || N == 0) return BGNN_OK;
-    const Plan pl = make_plan(M, N, K, ta, tb, a_blk, c_blk, precision);
+    Plan pl = make_plan(M, N, K, ta, tb, a_blk, c_blk, precision);
+    // the drop-add epilogue preloads its whole masked tile (32 float4 per lane at 256x256, where the
+    // accumulators already fill the VGPRs: it spilled, 365 us for the max layer's N = 1024 merged
+    // dgrad): 128x256 tiles, as the SAGE dgrad's
+    if (bs.src && pl.x6 && pl.prec == 1 && (pl.cfg == 3 || pl.cfg == 4) && g_gemm_cfg < 0) {
+        pl.cfg = 2;
+        pl.bm = kX6Cfgs[2].bm;
+        pl.bn = kX6Cfgs[2].bn;
+    }
     BGNN_REQUIRE((a_blk == 0 || a_blk % (ta ? pl.bm : pl.bk) == 0) && (c_blk == 0 || c_blk % pl.bn == 0),
                  "gemm: plane blocks (a_blk %lld, c_blk %lld) must be multiples of the %dx%dx%d tile",
                  (long long)a_blk, (long long)c_blk, pl.bm, pl.bn, pl.bk);
@@ -660,6 +685,7 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
         g.dseed = bs.seed;
         g.dthr = dropout_threshold(bs.p);
         g.dkeep = g.dthr ? 1.f / (1.f - bs.p) : 1.f;
+        g.bsrc_c0 = bs.c0;
     }
     // max |C| for the next GEMM's operand scale: in the split kernels' epilogue, else one pass
     const bool c_amax_fused = c_amax != nullptr && pl.x6 && split == 1;

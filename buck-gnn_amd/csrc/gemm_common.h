@@ -37,13 +37,16 @@ struct GemmArgs {
     // pointers then address bf16 elements and lda / ldb / ldc count bf16 elements
     int st;
     // f16x3 C = A B^T only: B points to a pre-split image of B^T (bgnn_gemm_wsplit, column tile =
-    // the launch tile's BN) instead of f32 rows; the kernel stages it by LDS-DMA
+    // the launch tile's BN) instead of f32 rows; the kernel copies its LDS image
     int wb;
+    // drop-add epilogue: only columns >= bsrc_c0 take the beta operand, column c reading bsrc column
+    // c - bsrc_c0 (a multiple of the tile width; the max layer's merged dgrad [dh W_l | dh W_r])
+    int64_t bsrc_c0;
 };
 
 // the beta operand of 4 consecutive columns (col % 4 == 0) of row `row`: masked bsrc
 __device__ __forceinline__ void beta_src4(const GemmArgs& g, int64_t row, int64_t col, float (&pv)[4]) {
-    const int64_t i = row * g.ld_bsrc + col;
+    const int64_t i = row * g.ld_bsrc + col - g.bsrc_c0;
     const float4 t = *reinterpret_cast<const float4*>(g.bsrc + i);
     const uint32_t m = g.dthr ? keep_bits4(g.dseed, (uint64_t)(i >> 2), g.dthr) : 0xFu;
     const float kf = g.dthr ? g.dkeep : 1.f;
@@ -56,7 +59,7 @@ __device__ __forceinline__ void beta_src4(const GemmArgs& g, int64_t row, int64_
 // beta_src4 on an already loaded float4 t of bsrc at (row, col) (the drop-add epilogue's prefetch)
 __device__ __forceinline__ void beta_mask4(const GemmArgs& g, int64_t row, int64_t col, const float4& t,
                                            float (&pv)[4]) {
-    const int64_t i = row * g.ld_bsrc + col;
+    const int64_t i = row * g.ld_bsrc + col - g.bsrc_c0;
     const uint32_t m = g.dthr ? keep_bits4(g.dseed, (uint64_t)(i >> 2), g.dthr) : 0xFu;
     const float kf = g.dthr ? g.dkeep : 1.f;
     pv[0] = (m & 1u) ? t.x * kf : 0.f;

@@ -136,7 +136,7 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const Acc& acc, i
 #pragma unroll
                 for (int q = 0; q < TM * 4; ++q)
                     gpre[j][q] = *reinterpret_cast<const float4*>(g.bsrc + (r0 + q * 8 + rq) * g.ld_bsrc + c0 + j * 32 +
-                                                                  c4);
+                                                                  c4 - g.bsrc_c0);
         }
     }
 #pragma unroll

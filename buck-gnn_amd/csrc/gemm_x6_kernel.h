@@ -836,6 +836,15 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     }
     // (the loop's last barrier has retired every wave's LDS reads of the operand tiles)
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
+    if (ABL == 8 && n0 < g.bsrc_c0) {   // drop-add GEMM, a column tile left of the beta operand
+        GemmArgs ge = g;
+        ge.beta = 0.f;
+        if constexpr (kM16)
+            x6_epilogue<TM, TN, ABL, C16>(ge, acc4, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
+        else
+            x6_epilogue<TM, TN, ABL, C16>(ge, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
+        return;
+    }
     if constexpr (kM16)
         x6_epilogue<TM, TN, ABL, C16>(g, acc4, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, ks, lane, ia, ib, stage);
     else

@@ -412,6 +412,15 @@ int bgnn_gemm_f32_dropadd(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N
                           const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                           const float* a_amax, const float* b_amax, const float* src, int64_t ld_src,
                           float p, uint64_t seed, void* ws, size_t ws_bytes, void* stream);
+/* bgnn_gemm_f32_dropadd (trans_a = 0, trans_b = 1) whose masked addend covers only the columns
+ * [src_col0, N) of C -- column c takes src column c - src_col0, with the mask index of that src
+ * element -- and the columns left of src_col0 are a plain product: the max aggregation layer's
+ * merged input gradient [dh W_l | dh W_r + drop(g)] in one launch (round 5, ABI 10). src_col0 must
+ * be a multiple of the planned column tile (256 for the SAGE shapes). */
+int bgnn_gemm_f32_dropadd_cols(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                               int64_t ldb, float* C, int64_t ldc, const float* a_amax, const float* b_amax,
+                               const float* src, int64_t ld_src, int64_t src_col0, float p, uint64_t seed, void* ws,
+                               size_t ws_bytes, void* stream);
 #define BGNN_WSPLIT_FRAG 0x10000
 /* Pre-split weights (round 5). The f16x3 GEMM C = A W^T of the SAGE layers (forward z = x
  * [W_l;W_r]^T, input gradient dx = dz [W_l;W_r]) takes its weight operand W [N, K] as a

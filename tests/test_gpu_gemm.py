@@ -317,3 +317,36 @@ def test_gemm_presplit_rejects_mismatched_tile(dev):
     with pytest.raises(_lib.BgnnError):
         _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), wrong, out.data_ptr(), N, None, 0,
                   am.data_ptr(), am.data_ptr(), None, None, 0, 0.0, 0, fused._stream())
+
+
+@pytest.mark.parametrize("M", [80656, 1000])
+def test_gemm_dropadd_cols_bit_identical(dev, M):
+    """bgnn_gemm_f32_dropadd_cols (the max layer's merged input gradient [dh W_l | dh W_r + drop(g)]):
+    the columns left of src_col0 are exactly the plain product and the rest exactly
+    bgnn_gemm_f32_dropadd of the right block with src (its own mask indices)."""
+    torch.manual_seed(M)
+    C, H = 512, 512
+    a = torch.randn(M, H, device=dev)
+    w = torch.randn(2 * C, H, device=dev) * 0.03
+    src = torch.randn(M, C, device=dev)
+    am = torch.stack([a.abs().max(), w.abs().max()]).contiguous()
+    out = torch.full((M, 2 * C), float("nan"), device=dev)
+    ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, 2 * C, H, 0, 1, 0)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    _lib.call("bgnn_gemm_f32_dropadd_cols", M, 2 * C, H, a.data_ptr(), H, w.data_ptr(), H, out.data_ptr(), 2 * C,
+              am[0:1].data_ptr(), am[1:2].data_ptr(), src.data_ptr(), C, C, 0.1, 77, ws.data_ptr(), ws_bytes,
+              fused._stream())
+    left = fused.gemm(a, w[:C].contiguous(), False, True, a_amax=am[0:1], b_amax=am[1:2])
+    right = torch.empty(M, C, device=dev)
+    ws2_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, C, H, 0, 1, 0)
+    ws2 = torch.empty(max(ws2_bytes, 1), dtype=torch.uint8, device=dev)
+    wr = w[C:].contiguous()
+    _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M, C, H, a.data_ptr(), H, wr.data_ptr(), H, right.data_ptr(), C,
+              am[0:1].data_ptr(), am[1:2].data_ptr(), src.data_ptr(), C, 0.1, 77, ws2.data_ptr(), ws2_bytes,
+              fused._stream())
+    assert torch.equal(out[:, :C], left)
+    assert torch.equal(out[:, C:], right)
+    with pytest.raises(_lib.BgnnError):   # the addend must start on a column tile
+        _lib.call("bgnn_gemm_f32_dropadd_cols", M, 2 * C, H, a.data_ptr(), H, w.data_ptr(), H, out.data_ptr(),
+                  2 * C, am[0:1].data_ptr(), am[1:2].data_ptr(), src.data_ptr(), C, 100, 0.1, 77, ws.data_ptr(),
+                  ws_bytes, fused._stream())
