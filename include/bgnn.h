@@ -94,6 +94,10 @@ const char* bgnn_last_error_string(void);
                                     6 = 32x32x16 MFMAs instead of the 16x16x32 default. 0..5 are
                                     bit-identical to each other; 6 differs within the f16x3 error
                                     class (another summation order inside the matrix core). */
+#define BGNN_TUNE_MAX_GROUP 15  /* max aggregation (forward) on the row-group kernel where the CSR
+                                    has a 4-row plan (1) or on the sweep kernel (0, default: the
+                                    group form measured 168 against 156 us on cfg2); the same
+                                    values and argmax state */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose
