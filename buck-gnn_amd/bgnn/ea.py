@@ -81,7 +81,7 @@ class _LinearGatherReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, e, W, b, p1, seg1: SegmentIndex, p2, seg2: SegmentIndex, bf16: bool, out_bf16: bool = False,
-                slot=None):
+                slot=None, dp=None):
         e = e.contiguous()
         Wc = W.contiguous()
         M, K = e.shape
@@ -111,6 +111,7 @@ class _LinearGatherReLU(torch.autograd.Function):
         ctx.seg1, ctx.seg2, ctx.has2, ctx.bf16, ctx.has_bias = seg1, seg2, p2 is not None, bf16, b is not None
         ctx.storage = storage
         ctx.slot = slot
+        ctx.dp = dp   # (ColGrad, block of p1, block of p2): the segment sums go into its columns
         ctx.save_for_backward(e, W, out)
         return out
 
@@ -128,9 +129,15 @@ class _LinearGatherReLU(torch.autograd.Function):
             if de is not None and ctx.slot is not None:
                 de = ctx.slot.add_to(de)   # + the skip + dropout's share of e's gradient, one pass
             dW = gemm_bf16(g, e, True, False)
-            d1 = segment_reduce(g, ctx.seg1, "sum")
-            d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
-            return de, dW, db, d1, None, d2, None, None, None, None
+            if ctx.dp is not None:
+                cg, i1, i2 = ctx.dp
+                H = g.size(1)
+                d1 = _segment_sum_into(g, ctx.seg1, cg.block(i1, H))
+                d2 = _segment_sum_into(g, ctx.seg2, cg.block(i2, H)) if ctx.has2 else None
+            else:
+                d1 = segment_reduce(g, ctx.seg1, "sum")
+                d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
+            return de, dW, db, d1, None, d2, None, None, None, None, None
         # ReLU mask, bias gradient and max|g'| (the f16x3 operand scale of both GEMMs) in one pass
         g, db, g_amax = relu_bias_grad(g, out, ctx.has_bias)
         bf16 = ctx.bf16
@@ -141,7 +148,16 @@ class _LinearGatherReLU(torch.autograd.Function):
         dW = gemm(g, e, trans_a=True, trans_b=False, a_amax=g_amax, bf16=bf16)
         d1 = segment_reduce(g, ctx.seg1, "sum")
         d2 = segment_reduce(g, ctx.seg2, "sum") if ctx.has2 else None
-        return de, dW, db, d1, None, d2, None, None, None, None
+        return de, dW, db, d1, None, d2, None, None, None, None, None
+
+
+def _segment_sum_into(g: torch.Tensor, seg: SegmentIndex, out: torch.Tensor) -> torch.Tensor:
+    """Segment sums of the bf16 rows of g by seg into the f32 view out (a column block of a
+    ColGrad buffer): bgnn_segment_sum_bf16 with out's row stride."""
+    g = g.contiguous()
+    _lib.call("bgnn_segment_sum_bf16", seg.fwd.rowptr.data_ptr(), seg.fwd.col.data_ptr(), seg.num_rows, g.data_ptr(),
+              g.stride(0), g.size(1), 0, out.data_ptr(), out.stride(0), _stream())
+    return out
 
 
 def _epilogue_gather_available() -> bool:
@@ -151,12 +167,12 @@ def _epilogue_gather_available() -> bool:
     return fused.GEMM_BACKEND == "hip" and _lib.query("bgnn_get_tuning", 5) != 0
 
 
-def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False, out_bf16=False, slot=None):
+def linear_gather_relu(e, W, b, p1, seg1, p2=None, seg2=None, bf16=False, out_bf16=False, slot=None, dp=None):
     if not _epilogue_gather_available():
         if e.dtype == torch.bfloat16 or out_bf16:
             raise ValueError("linear_gather_relu: bf16 storage needs the epilogue gather (split GEMM family)")
         return gather_add(linear(e, W, b, False, bf16=bf16), p1, seg1, p2, seg2, relu=True)
-    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16, out_bf16, slot)
+    return _LinearGatherReLU.apply(e, W, b, p1, seg1, p2, seg2, bf16, out_bf16, slot, dp)
 
 
 class GradSlot:
@@ -206,13 +222,30 @@ class _SkipDropoutToSlot(torch.autograd.Function):
         return None, None, None, None, None
 
 
+class ColGrad:
+    """One [N, k*H] f32 gradient buffer shared by the k column blocks of P (_ColumnBlocks): the
+    consumers' backward writes each block's segment sums straight into its columns (one block each),
+    so _ColumnBlocks' backward returns the buffer instead of concatenating k [N, H] gradients (EA_GNN
+    cfg5: a 2 GB copy per block per step)."""
+    __slots__ = ("shape", "device", "buf")
+
+    def __init__(self, shape, device):
+        self.shape, self.device, self.buf = shape, device, None
+
+    def block(self, i: int, H: int) -> torch.Tensor:
+        if self.buf is None:
+            self.buf = torch.empty(self.shape, dtype=torch.float32, device=self.device)
+        return self.buf[:, i * H:(i + 1) * H]
+
+
 class _ColumnBlocks(torch.autograd.Function):
     """Split [N, k*H] into k column views whose backward is ONE concatenation of the k
-    gradients (autograd's slice backward would zero-fill and add k full [N, k*H] buffers)."""
+    gradients (autograd's slice backward would zero-fill and add k full [N, k*H] buffers), or no
+    copy at all when the k gradients are the blocks of the layer's ColGrad buffer."""
 
     @staticmethod
-    def forward(ctx, P, k: int):
-        ctx.k = k
+    def forward(ctx, P, k: int, cg=None):
+        ctx.k, ctx.cg = k, cg
         ctx.set_materialize_grads(False)   # unused blocks arrive as None: no zero-filled buffers
         H = P.size(1) // k
         return tuple(P[:, i * H:(i + 1) * H] for i in range(k))
@@ -221,13 +254,22 @@ class _ColumnBlocks(torch.autograd.Function):
     def backward(ctx, *gs):
         ref = next((g for g in gs if g is not None), None)
         if ref is None:
-            return None, None
+            return None, None, None
+        cg = ctx.cg
+        if cg is not None and cg.buf is not None:
+            H = cg.buf.size(1) // ctx.k
+            if all(g is not None and g.data_ptr() == cg.buf[:, i * H:].data_ptr() and g.stride() == cg.buf.stride()
+                   for i, g in enumerate(gs)):
+                buf, cg.buf = cg.buf, None
+                return buf, None, None
         gs = [torch.zeros_like(ref) if g is None else g for g in gs]
-        return torch.cat(gs, 1), None
+        return torch.cat(gs, 1), None, None
 
 
 # the two-step form (linear, then _GatherAdd) is kept for A/B measurement
 FUSED_GATHER = True
+# bf16 storage: the P column blocks' gradients written into one shared buffer (ColGrad, A/B switch)
+COLGRAD = True
 # EA_GNN's skip add + dropout over [E, H] / [N, H] as one pass (bgnn_add_dropout)
 FUSED_SKIP_DROPOUT = True
 # bf16 configuration (model.ea_bf16): the per-edge activations (edge encoder output, h1, e',
@@ -294,18 +336,20 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
     x = x.contiguous()
     # node-level blocks of the two concatenation Linears, one GEMM
     P = linear(x, torch.cat([W1[:, :H], W1[:, H:2 * H], Wp[:, :H]], 0), None, False, bf16=bf16)
-    P_row, P_col, Q = _ColumnBlocks.apply(P, 3)
     # the four per-edge K = H forward products, timed for the bench's EA_GNN roofline (each reads
     # an [E, H] f32 operand and writes an [E, H] f32 result)
     st = bf16 and BF16_STORAGE and FUSED_GATHER and _epilogue_gather_available() and H % 8 == 0
+    cg = ColGrad(P.shape, P.device) if (st and COLGRAD) else None
+    P_row, P_col, Q = _ColumnBlocks.apply(P, 3, cg)
     if st:   # bf16 edge activations end to end
         with fused._timed("ea_edge_fwd"):
             h1 = linear_gather_relu(e, W1[:, 2 * H:], b1, P_row, seg_row, P_col, seg_col, bf16=True, out_bf16=True,
-                                    slot=slot if slot_in else None)
+                                    slot=slot if slot_in else None, dp=(cg, 0, 1) if cg is not None else None)
         with fused._timed("ea_edge_fwd"):
             e_out = linear_bf16(h1, W2, b2, False, True)
         with fused._timed("ea_edge_fwd"):
-            m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=True, out_bf16=True, slot=slot)
+            m1 = linear_gather_relu(e_out, Wp[:, H:], bp, Q, seg_col, bf16=True, out_bf16=True, slot=slot,
+                                    dp=(cg, 2, None) if cg is not None else None)
         with fused._timed("ea_edge_fwd"):
             msg = linear_bf16(m1, Wp2, bp2, False, True)
         agg = segment_reduce(msg, seg_row, "mean")
