@@ -116,6 +116,7 @@ SIGNATURES = {
     "bgnn_gemm_b16_variant": (c_i32, [c_i32]),
     "bgnn_add_dropout_bf16": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p, c_p]),
     "bgnn_segment_sum_bf16": (c_i32, [c_p, c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p]),
+    "bgnn_segment_bcast_bf16": (c_i32, [c_p, c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p]),
     "bgnn_gemm_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
     "bgnn_gemm_set_cfg": (c_i32, [c_i32]),
     "bgnn_gemm_f32_planes": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_i64, c_i64, c_p, c_i64,

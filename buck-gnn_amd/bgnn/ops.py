@@ -163,6 +163,13 @@ class _SegmentReduceBf16(torch.autograd.Function):
     def backward(ctx, g):
         seg = ctx.seg
         g = g.contiguous()
+        H = g.size(1)
+        if g.dtype == torch.float32 and g.is_cuda and H % 8 == 0 and H <= 512 and g.data_ptr() % 16 == 0:
+            # one pass: scale, bf16 rounding and the broadcast to every position (bgnn_segment_bcast_bf16)
+            out = torch.empty(seg.n, H, dtype=torch.bfloat16, device=g.device)
+            _lib.call("bgnn_segment_bcast_bf16", seg.fwd.rowptr.data_ptr(), seg.fwd.col.data_ptr(), seg.num_rows,
+                      g.data_ptr(), g.stride(0), H, int(ctx.mean), out.data_ptr(), out.stride(0), _stream())
+            return out, None, None
         if ctx.mean:
             g = g / seg.fwd.degree().clamp_min(1).to(g.dtype).unsqueeze(1)
         return g.to(torch.bfloat16).index_select(0, seg.index), None, None

@@ -124,6 +124,35 @@ __global__ __launch_bounds__(256) void k_seg_sum_bf16(const int32_t* __restrict_
     }
 }
 
+// Backward of k_seg_sum_bf16: every position p of segment r receives bf16(g[r] (/ max(deg, 1) for
+// mean)), f32 division then one round-to-nearest-even -- torch's (g / cnt).to(bfloat16)
+// .index_select(0, index) in one pass (EA_GNN's scatter_mean backward, Models/BuckGNN.py:561).
+// One wave per segment, 8 columns (16 B of bf16) per lane; each position's row is written once.
+__global__ __launch_bounds__(256) void k_seg_bcast_bf16(const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ col, int64_t R,
+                                                        const float* __restrict__ g, int64_t ldg, int H, int mean,
+                                                        uint16_t* __restrict__ out, int64_t ldo) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    const int c = lane * 8;
+    const bool ok = c < H;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < R; r += nw) {
+        const int32_t b = rowptr[r], e = rowptr[r + 1];
+        if (b == e || !ok) continue;
+        const float4 v0 = *reinterpret_cast<const float4*>(g + r * ldg + c);
+        const float4 v1 = *reinterpret_cast<const float4*>(g + r * ldg + c + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (mean) {
+            const float cnt = (float)(e - b);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = __fdiv_rn(v[k], cnt);
+        }
+        const uint4 q = make_uint4(bf16_pack2(v[0], v[1]), bf16_pack2(v[2], v[3]), bf16_pack2(v[4], v[5]),
+                                   bf16_pack2(v[6], v[7]));
+        for (int32_t p = b; p < e; ++p) *reinterpret_cast<uint4*>(out + (int64_t)col[p] * ldo + c) = q;
+    }
+}
+
 inline unsigned elem_blocks(int64_t n4) {
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 8192) blocks = 8192;   // grid-stride beyond 32 blocks per CU
@@ -263,6 +292,21 @@ extern "C" int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, 
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_seg_sum_bf16, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), rowptr, col, n_rows,
                        static_cast<const uint16_t*>(x), ldx, H, mean, out, ldo);
+    BGNN_CHECK_LAUNCH();
+    return BGNN_OK;
+}
+
+extern "C" int bgnn_segment_bcast_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* g,
+                                       int64_t ldg, int32_t H, int32_t mean, void* out, int64_t ldo, void* stream) {
+    BGNN_REQUIRE(rowptr && (n_rows == 0 || (col && g && out)), "segment_bcast_bf16: null pointer");
+    BGNN_REQUIRE(H > 0 && H <= 512 && H % 8 == 0 && ldg % 4 == 0 && ldg >= H && ldo >= H && ldo % 8 == 0,
+                 "segment_bcast_bf16: H must be a multiple of 8 up to 512, rows 16-B aligned");
+    BGNN_REQUIRE(aligned16(g) && aligned16(out), "segment_bcast_bf16: 16-byte aligned g / out required");
+    if (n_rows == 0) return BGNN_OK;
+    int64_t blocks = (n_rows + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_seg_bcast_bf16, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), rowptr, col, n_rows,
+                       g, ldg, H, mean, static_cast<uint16_t*>(out), ldo);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

@@ -356,6 +356,11 @@ int bgnn_add_dropped_bf16(const void* a, const void* b, int64_t n, float p, uint
                           void* stream);
 int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
                           int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream);
+/* Backward of bgnn_segment_sum_bf16 (ABI 10): every position p of segment r (the CSR's col lists
+ * the positions of each segment) gets bf16(g[r] / max(deg, 1) for mean, else g[r]) -- f32 division,
+ * one round-to-nearest-even -- in one pass (torch: a divide, a bf16 cast and an index_select). */
+int bgnn_segment_bcast_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* g, int64_t ldg,
+                            int32_t H, int32_t mean, void* out, int64_t ldo, void* stream);
 
 /* ------------------------------------------------------------------------
  * fp32 GEMM (f32 operands, f32 result, f32 accumulation):

@@ -95,6 +95,10 @@ def test_segment_reduce_bf16(dev, reduce):
     ref.backward(g.double())
     assert x.grad.dtype == torch.bfloat16
     torch.testing.assert_close(x.grad.float(), xr.grad.float().to(torch.bfloat16).float(), rtol=1e-2, atol=1e-6)
+    # the backward kernel (bgnn_segment_bcast_bf16) is torch's (g / cnt).to(bfloat16).index_select,
+    # bit for bit (f32 division, one round-to-nearest-even)
+    gg = g / seg.fwd.degree().clamp_min(1).to(g.dtype).unsqueeze(1) if reduce == "mean" else g
+    assert torch.equal(x.grad, gg.to(torch.bfloat16).index_select(0, seg.index))
 
 
 @pytest.fixture
