@@ -22,13 +22,13 @@ from collections import defaultdict
 
 # bench roofline kernels: key -> kernel-name substrings (either matches)
 KERNELS = {
-    "gemm_fwd_h3": ("k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>",),   # f16x3 forward GEMM (256x256 tiles)
-    "gemm_dgrad": ("k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8>", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0>"),   # dgrad
-    "gemm_wgrad": ("k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0>",),   # wgrad (split-K partial products)
+    "gemm_fwd_h3": ("k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0,",),   # f16x3 forward GEMM (256x256 tiles)
+    "gemm_dgrad": ("k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8,", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0,"),   # dgrad
+    "gemm_wgrad": ("k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0,",),   # wgrad (split-K partial products)
     "sage_fwd": ("k_seg_group<2, 0, 1,", "k_seg_sweep<2, 0, 1,"),   # fused SAGE forward aggregation
     "spmm_bwd": ("k_seg_group<2, 0, 0,", "k_seg_sweep<2, 0, 0,"),   # transpose aggregation
     "ea_edge_b16": ("k_gemm_b16<",),   # EA_GNN bf16 per-edge Linears (gathered and plain epilogues)
-    "ea_wgrad_b16": ("k_gemm_x6<2, 1, 0, 256, 256, 4, 2, 19>",),   # EA_GNN bf16 per-edge weight gradients
+    "ea_wgrad_b16": ("k_gemm_x6<2, 1, 0, 256, 256, 4, 2, 19,",),   # EA_GNN bf16 per-edge weight gradients
 }
 
 
