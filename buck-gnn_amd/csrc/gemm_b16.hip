@@ -76,19 +76,104 @@ __device__ __forceinline__ void b16_mma(const uint4* __restrict__ S, floatx16 (&
     }
 }
 
+// The same slice on 16x16x32 MFMAs (round 5: the chip holds a higher clock under them; the
+// k_gemm_x6 bf16 kernels use them too, so both give the same bits): per k32 step the fragments of
+// 16 rows (lane & 15) x 8 k (chunk 4 s + (lane >> 4)); the side with fewer 16-row blocks is held,
+// the other streamed. The swizzle keeps these reads conflict-free (lane groups of ds_read_b128).
+template <int BM, int BN, int BK, int WM, int WN>
+__device__ __forceinline__ void b16_mma(const uint4* __restrict__ S, floatx4 (&acc)[2 * (BM / WM / 32)][2 * (BN / WN / 32)],
+                                        int wm, int wn, int lane) {
+    using L = B16Slice<BK>;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int st = 0; st < BK / 32; ++st) {
+        const int kg = 4 * st + lq;
+        if constexpr (TM <= TN) {
+            uint4 a[2 * TM];
+#pragma unroll
+            for (int i = 0; i < 2 * TM; ++i) a[i] = S[L::at(wm * (BM / WM) + i * 16 + l16, kg)];
+#pragma unroll
+            for (int j = 0; j < 2 * TN; ++j) {
+                const uint4 b = S[L::at(BM + wn * (BN / WN) + j * 16 + l16, kg)];
+#pragma unroll
+                for (int i = 0; i < 2 * TM; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[i]), as_bf16x8(b), acc[i][j], 0, 0, 0);
+            }
+        } else {
+            uint4 b[2 * TN];
+#pragma unroll
+            for (int j = 0; j < 2 * TN; ++j) b[j] = S[L::at(BM + wn * (BN / WN) + j * 16 + l16, kg)];
+#pragma unroll
+            for (int i = 0; i < 2 * TM; ++i) {
+                const uint4 a = S[L::at(wm * (BM / WM) + i * 16 + l16, kg)];
+#pragma unroll
+                for (int j = 0; j < 2 * TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b[j]), acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// accumulator helpers for either MFMA shape: zero; the 32x32 block (i, j) into an LDS stage (rows
+// row0.., columns coff.., row stride ld) with the C/D map of the MFMA; one probe value
+template <int TM, int TN>
+__device__ __forceinline__ void b16_acc_zero(floatx16 (&acc)[TM][TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+}
+template <int TM2, int TN2>
+__device__ __forceinline__ void b16_acc_zero(floatx4 (&acc)[TM2][TN2]) {
+#pragma unroll
+    for (int i = 0; i < TM2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+}
+template <int TM, int TN>
+__device__ __forceinline__ void b16_stage_block(float* __restrict__ stage, int ld, int coff, int row0,
+                                                const floatx16 (&acc)[TM][TN], int i, int j, int lane) {
+    const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) stage[(row0 + (r & 3) + 8 * (r >> 2) + 4 * lh) * ld + coff + li] = acc[i][j][r];
+}
+template <int TM2, int TN2>
+__device__ __forceinline__ void b16_stage_block(float* __restrict__ stage, int ld, int coff, int row0,
+                                                const floatx4 (&acc)[TM2][TN2], int i, int j, int lane) {
+    const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+    for (int si = 0; si < 2; ++si)
+#pragma unroll
+        for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                stage[(row0 + si * 16 + 4 * lq + r) * ld + coff + sj * 16 + l16] = acc[2 * i + si][2 * j + sj][r];
+}
+template <int TM, int TN>
+__device__ __forceinline__ float b16_acc_probe(const floatx16 (&acc)[TM][TN], int i, int j) {
+    return acc[i][j][0] + acc[i][j][15];
+}
+template <int TM2, int TN2>
+__device__ __forceinline__ float b16_acc_probe(const floatx4 (&acc)[TM2][TN2], int i, int j) {
+    return acc[2 * i][2 * j][0] + acc[2 * i + 1][2 * j + 1][3];
+}
+
 // Epilogue (alpha 1, beta 0, no split-K): per 32-column block, the wave's TM x 32 x 32
 // accumulators go through its LDS stage (x6_epilogue's C/D map and stage layout) and leave as
 // 16-B non-temporal row stores -- f32 C: 4 columns per lane (8 lanes per 128-B row segment), bf16
 // C: 8 columns per lane (4 lanes per 64-B row segment; x6_epilogue stores 8 B). Per element the
 // arithmetic and its order are x6_epilogue's: acc, + bias, + ga0[gi0[row]], + ga1[gi1[row]],
 // ReLU, one bf16 rounding (RNE). Edge blocks fall back to x6_epilogue's element-guarded path.
-template <int TM, int TN, bool C16, bool WIDE = false>
-__device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
+template <int TM, int TN, bool C16, bool WIDE = false, typename Acc>
+__device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
                                              int64_t c0, int lane, float* __restrict__ stage) {
     constexpr int CPL = C16 ? 8 : 4;        // columns per lane
     constexpr int LPR = 32 / CPL;           // lanes per 32-column row segment
     constexpr int RPP = 64 / LPR;           // rows per pass
-    const int li = lane & 31, lh = lane >> 5;
+
     const int rq = lane / LPR, cq = (lane % LPR) * CPL;
     const bool gvec = (!g.ga0 || ((((uintptr_t)g.ga0 & 15) == 0) && g.ldg0 % 4 == 0)) &&
                       (!g.ga1 || ((((uintptr_t)g.ga1 & 15) == 0) && g.ldg1 % 4 == 0));
@@ -119,10 +204,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        stage[((r & 3) + 8 * (r >> 2) + 4 * lh) * LDW + h * 32 + li] = acc[i][j + h][r];
+                for (int h = 0; h < 2; ++h) b16_stage_block(stage, LDW, h * 32, 0, acc, i, j + h, lane);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -173,9 +255,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const floatx16 (
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+        for (int i = 0; i < TM; ++i) b16_stage_block(stage, 32, 0, i * 32, acc, i, j, lane);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const int64_t col = c0 + j * 32 + cq;
         float bv[CPL];
@@ -288,13 +368,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
                                              (lds_void_t*)(slot + dst[q]), 16, 0, 0);
     };
 
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    floatx4 acc[2 * TM][2 * TN];   // 16x16x32 MFMA tiles (b16_mma)
+    b16_acc_zero(acc);
 
     // slice m lives in slot m % NS: wait for this wave's part of slice m (the NS - 2 newer
     // slices stay in flight), one barrier (every wave's part landed, every wave done with slice
@@ -312,7 +387,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) t0 += acc[i][j][0] + acc[i][j][15];
+            for (int j = 0; j < TN; ++j) t0 += b16_acc_probe(acc, i, j);
         if (lane == 0) reinterpret_cast<float*>(g.C)[wave] = t0;
         return;
     }
@@ -325,13 +400,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
 // wave-private 4 KiB LDS stage (separate from the operand slots, so the next tile's slices can be
 // in flight meanwhile), out as 16-B non-temporal row stores (f32: 4 columns per lane, bf16: 8);
 // x6_epilogue's per-element arithmetic and order; edge blocks store element-wise within bounds.
-template <int TM, int TN, bool C16>
-__device__ __forceinline__ void b16p_epilogue(const GemmArgs& g, const floatx16 (&acc)[TM][TN], int64_t r0,
+template <int TM, int TN, bool C16, typename Acc>
+__device__ __forceinline__ void b16p_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
                                               int64_t c0, int lane, float* __restrict__ stage) {
     constexpr int CPL = C16 ? 8 : 4;
     constexpr int LPR = 32 / CPL;
     constexpr int RPP = 64 / LPR;
-    const int li = lane & 31, lh = lane >> 5;
+
     const int rq = lane / LPR, cq = (lane % LPR) * CPL;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -342,8 +417,7 @@ __device__ __forceinline__ void b16p_epilogue(const GemmArgs& g, const floatx16 
         for (int k = 0; k < CPL; ++k) bv[k] = (g.bias && (cfull || col + k < g.N)) ? g.bias[col + k] : 0.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[i][j][r];
+            b16_stage_block(stage, 32, 0, 0, acc, i, j, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             const bool full = cfull && r0 + i * 32 + 32 <= g.M;
 #pragma unroll
@@ -483,13 +557,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_b16p(GemmArgs g) {
                                              (lds_void_t*)(slot + dst[q]), 16, 0, 0);
     };
 
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    floatx4 acc[2 * TM][2 * TN];   // 16x16x32 MFMA tiles (b16_mma)
+    b16_acc_zero(acc);
     float* stage = reinterpret_cast<float*>(smem + NS * SLICE_U4) + wave * (32 * 32);
 
     for (int S = 0; S < NS - 1; ++S) issue(S);
@@ -503,12 +572,7 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_b16p(GemmArgs g) {
             const int64_t lt = first + (S / nm) * stride;
             const int64_t m0 = (lt / ntn) * BM, n0 = (lt % ntn) * BN;
             b16p_epilogue<TM, TN, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            b16_acc_zero(acc);
         }
     }
 }

@@ -402,7 +402,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // EA_GNN node blocks at small N) keeps 32x32x16 and its rounding (tests/test_gpu_fold.py
     // measures the folded path's gradients against fp64 relative to the unfolded path's). PPV bit 5
     // keeps 32x32x16 (A/B), as do the ping-pong, line-major, interleaved and B-in-registers variants.
-    constexpr bool kM16 = PREC == 1 && NT == 512 && (PPV & 32) == 0 && (PPV & (1 | 2 | 8 | 16)) == 0;
+    // (bf16 operands, PREC 2: every tile, as the LDS-DMA bf16 kernels of gemm_b16.hip, which must
+    // give the same bits)
+    constexpr bool kM16 = (PREC == 2 || (PREC == 1 && NT == 512)) && (PPV & 32) == 0 &&
+                          (PPV & (1 | 2 | 8 | 16)) == 0;
 
     // (pre-split B: A may have a unit count that is no multiple of NT, x6_nu's guarded last unit)
     static_assert((BM * 4 % NT == 0 || kWB) && BN * 4 % NT == 0, "staging units must divide evenly");
@@ -546,12 +549,22 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
                 // the side with fewer 16-row blocks is held whole, the other streamed block by block
                 // (both whole would need 24 fragments = 96 VGPRs at 256x256 and spill)
                 const int l16 = lane & 15, lq = lane >> 4;
-                auto fa = [&](int i, int p) { return As[cur][p * BM * 4 + x6_pos(wm * (BM / WM) + i * 16 + l16, lq)]; };
-                auto fb = [&](int j, int p) { return Bs[cur][p * BN * 4 + x6_pos(wn * (BN / WN) + j * 16 + l16, lq)]; };
+                auto fa = [&](int i, int p) {
+                    return (p < NP) ? As[cur][p * BM * 4 + x6_pos(wm * (BM / WM) + i * 16 + l16, lq)]
+                                    : make_uint4(0, 0, 0, 0);
+                };
+                auto fb = [&](int j, int p) {
+                    return (p < NP) ? Bs[cur][p * BN * 4 + x6_pos(wn * (BN / WN) + j * 16 + l16, lq)]
+                                    : make_uint4(0, 0, 0, 0);
+                };
                 auto mma3 = [&](floatx4& t, const uint4 (&a)[2], const uint4 (&b)[2]) {
-                    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[1]), t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[1]), as_f16x8(b[0]), t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[0]), t, 0, 0, 0);
+                    if constexpr (PREC == 2) {   // bf16 operands: one product
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[0]), as_bf16x8(b[0]), t, 0, 0, 0);
+                    } else {
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[1]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[1]), as_f16x8(b[0]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[0]), t, 0, 0, 0);
+                    }
                 };
                 if constexpr (TM <= TN) {
                     uint4 a[2 * TM][2];
