@@ -4,10 +4,8 @@
 
     python tools/gemm_launches.py gpurun_out/prof_TAG/.../run_kernel_trace.csv [N] [out.json]
 
-The forward GEMM instantiation serves both the folded first layer (K = 128) and the five K = 512
-layers; in dispatch order every step issues them as [layer 0, layers 1..5], so launch i of that
-instantiation is the folded one when i % 6 == 0 (checked against the duration split: a K = 128
-launch takes well under half of a K = 512 one). N = nodes per batch (default cfg2: 80,656).
+The folded first layer's forward (K = 128) and the five K = 512 layers' forward run different
+instantiations (the latter with the pre-split weights). N = nodes per batch (default cfg2: 80,656).
 """
 import csv
 import json
@@ -17,12 +15,15 @@ import sys
 H, K_IN = 512, 128
 PEAK = 2500.0 / 3   # f16x3 f32-equivalent ceiling, TF
 
+# (round 5: the names carry the variant parameter; the K = 512 forward and dgrad run the
+# pre-split-weight instantiation, PPV 4, the folded layer's the plain one)
 FAMS = {
-    "gemm_fwd": ["k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0>"],
-    "gemm_dgrad": ["k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8>", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0>"],
-    "gemm_wgrad": ["k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0>"],
-    "gemm_dgrad_fold": ["k_gemm_x6<1, 0, 1, 256, 128, 4, 2, 0>"],
-    "gemm_wgrad_fold": ["k_gemm_x6<1, 1, 0, 256, 128, 4, 2, 0>"],
+    "gemm_fwd": ["k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0, 4>"],
+    "gemm_fwd_fold": ["k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0, 0>"],
+    "gemm_dgrad": ["k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8, 4>", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0, 4>"],
+    "gemm_wgrad": ["k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0, 0>"],
+    "gemm_dgrad_fold": ["k_gemm_x6<1, 0, 1, 256, 128, 4, 2, 0, 0>"],
+    "gemm_wgrad_fold": ["k_gemm_x6<1, 1, 0, 256, 128, 4, 2, 0, 0>"],
 }
 
 
@@ -31,18 +32,12 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 80656
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Dispatch_Id"]))
     dur = {k: [] for k in FAMS}
-    dur["gemm_fwd_fold"] = []
-    fwd_i = 0
     for r in rows:
         name = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3   # us
         for fam, pats in FAMS.items():
             if any(p in name for p in pats):
-                if fam == "gemm_fwd":
-                    (dur["gemm_fwd_fold"] if fwd_i % 6 == 0 else dur["gemm_fwd"]).append(d)
-                    fwd_i += 1
-                else:
-                    dur[fam].append(d)
+                dur[fam].append(d)
                 break
     flop = {"gemm_fwd": 2.0 * n * 2 * H * H, "gemm_dgrad": 2.0 * n * H * 2 * H, "gemm_wgrad": 2.0 * 2 * H * H * n,
             "gemm_fwd_fold": 2.0 * n * 2 * H * K_IN, "gemm_dgrad_fold": 2.0 * n * K_IN * 2 * H,
