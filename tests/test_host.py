@@ -151,8 +151,26 @@ def test_column_blocks_unused_blocks_get_no_buffers():
     x, y = _ColumnBlocks.apply(Q, 2)
     z = torch.randn(1, requires_grad=True)
     (z * 2).sum().backward(inputs=[z])
-    out = _ColumnBlocks.backward(type("Ctx", (), {"k": 2})(), None, None)
-    assert out == (None, None)
+    out = _ColumnBlocks.backward(type("Ctx", (), {"k": 2, "cg": None})(), None, None)
+    assert out == (None, None, None)
+
+
+def test_column_blocks_shared_buffer_returned_without_copy():
+    """EA_GNN's ColGrad: when every block's gradient is that block of the shared buffer, the
+    backward hands the buffer on (no concatenation); otherwise it concatenates."""
+    from bgnn.ea import ColGrad, _ColumnBlocks
+    cg = ColGrad((4, 6), torch.device("cpu"))
+    b0, b1 = cg.block(0, 3), cg.block(1, 3)
+    b0.fill_(1.0)
+    b1.fill_(2.0)
+    buf = cg.buf
+    out = _ColumnBlocks.backward(type("Ctx", (), {"k": 2, "cg": cg})(), b0, b1)
+    assert out[0] is buf and cg.buf is None
+    cg2 = ColGrad((4, 6), torch.device("cpu"))
+    g0 = cg2.block(0, 3)
+    g1 = torch.full((4, 3), 5.0)   # not the buffer's block: concatenated
+    out = _ColumnBlocks.backward(type("Ctx", (), {"k": 2, "cg": cg2})(), g0, g1)
+    assert out[0] is not cg2.buf and torch.equal(out[0][:, 3:], g1)
 
 
 def test_relu_mask_matches_reference_form():
