@@ -169,7 +169,9 @@ __device__ __forceinline__ float b16_acc_probe(const floatx4 (&acc)[TM2][TN2], i
 // ReLU, one bf16 rounding (RNE). Edge blocks fall back to x6_epilogue's element-guarded path.
 template <int TM, int TN, bool C16, bool WIDE = false, typename Acc>
 __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
-                                             int64_t c0, int lane, float* __restrict__ stage) {
+                                             int64_t c0, int lane, float* __restrict__ stage,
+                                             const int64_t* __restrict__ li0 = nullptr,
+                                             const int64_t* __restrict__ li1 = nullptr) {
     constexpr int CPL = C16 ? 8 : 4;        // columns per lane
     constexpr int LPR = 32 / CPL;           // lanes per 32-column row segment
     constexpr int RPP = 64 / LPR;           // rows per pass
@@ -217,14 +219,15 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                         e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
                     }
                     if (g.ga0) {
-                        const float* s0 = g.ga0 + g.gi0[row] * g.ldg0 + col;
+                        // the gather rows' indices from the tile's LDS copy when the kernel made one
+                        const float* s0 = g.ga0 + (li0 ? li0[i * 32 + rr] : g.gi0[row]) * g.ldg0 + col;
 #pragma unroll
                         for (int k = 0; k < 8; k += 4) {
                             const float4 t = *reinterpret_cast<const float4*>(s0 + k);
                             x0[k] = t.x; x0[k + 1] = t.y; x0[k + 2] = t.z; x0[k + 3] = t.w;
                         }
                         if (g.ga1) {
-                            const float* s1 = g.ga1 + g.gi1[row] * g.ldg1 + col;
+                            const float* s1 = g.ga1 + (li1 ? li1[i * 32 + rr] : g.gi1[row]) * g.ldg1 + col;
 #pragma unroll
                             for (int k = 0; k < 8; k += 4) {
                                 const float4 t = *reinterpret_cast<const float4*>(s1 + k);
@@ -326,8 +329,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     static_assert((NS - 2) * G < 64, "vmcnt range");
     constexpr int EPI_U4 = NW * TM * 32 * 32 / 4;
     constexpr int SMEM_U4 = NS * SLICE_U4 > EPI_U4 ? NS * SLICE_U4 : EPI_U4;
-    static_assert(SMEM_U4 * 16 <= 160 * 1024, "LDS over 160 KiB");
-    __shared__ uint4 smem[SMEM_U4];   // one array (a second __shared__ object costs a vmcnt(0) per slice)
+    // WIDE bf16 C with gathered rows: the tile's gi0 / gi1 (BM int64 each) copied to LDS by the
+    // waves' first loads, so the epilogue's gather addresses wait on LDS instead of a dependent
+    // global load per 32-row block (one row of 32 per wave: NW * 32 == BM)
+    constexpr bool kIdx = WIDE && C16 && NW * 32 == BM;
+    constexpr int IDX_U4 = kIdx ? BM : 0;
+    static_assert((SMEM_U4 + IDX_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
+    __shared__ uint4 smem[SMEM_U4 + IDX_U4];   // one array (a second __shared__ object costs a vmcnt(0) per slice)
 
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -356,6 +364,18 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
         if (r > rmax) r = (int)rmax;
         off[q] = (uint32_t)((r * (isa ? g.lda : g.ldb) + 8 * c) * 2);
         dst[q] = ((isa ? 0 : BM) + r0) * L::CPR;
+    }
+    // the index copies go first: the slice waits' in-order vmcnt covers them
+    const bool lidx = kIdx && g.ga0 != nullptr && g.gidx_lds;
+    if (lidx) {
+        int64_t row = m0 + wave * 32 + (lane >> 1);
+        if (row > g.M - 1) row = g.M - 1;
+        uint4* dsti = smem + SMEM_U4 + wave * 16;   // 32 rows x 8 B per wave, lane l -> bytes 4 l
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(reinterpret_cast<const char*>(g.gi0 + row) + (lane & 1) * 4),
+                                         (lds_void_t*)dsti, 4, 0, 0);
+        if (g.ga1)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(reinterpret_cast<const char*>(g.gi1 + row) + (lane & 1) * 4),
+                                             (lds_void_t*)(dsti + BM / 2), 4, 0, 0);
     }
     const int64_t nm = g.K / BK;
     auto issue = [&](int64_t m) {
@@ -393,7 +413,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     }
     __syncthreads();   // every wave's fragment reads done before the epilogue reuses the LDS
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
-    b16_epilogue<TM, TN, C16, WIDE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
+    const int64_t* li = reinterpret_cast<const int64_t*>(smem + SMEM_U4) + wm * (BM / WM);
+    b16_epilogue<TM, TN, C16, WIDE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage,
+                                    lidx ? li : nullptr, lidx && g.ga1 ? li + BM : nullptr);
 }
 
 // Epilogue of one wave's TM x TN blocks for the persistent kernel: each 32x32 block through a
@@ -630,7 +652,9 @@ static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
             hipLaunchKernelGGL((k_gemm_b16p<256, 256, 32, 3, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
         case 10:  // persistent 128x256, k32 x 4 slots (96 + 32 KiB)
             hipLaunchKernelGGL((k_gemm_b16p<128, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 11:  // variant 7 with whole-line bf16 C stores (b16_epilogue WIDE)
+        case 13:  // variant 11 with the gather indices read from global memory per row (A/B)
+        case 11:  // variant 7 with whole-line bf16 C stores (b16_epilogue WIDE); gathered rows'
+                  // indices staged in LDS
             hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
         case 12:  // variant 1 with whole-line bf16 C stores
             hipLaunchKernelGGL((k_gemm_b16<256, 256, 32, 4, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
@@ -639,9 +663,11 @@ static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
     }
 }
 
-void launch_b16(hipStream_t s, const GemmArgs& g) {
-    const int v = b16_pick(g);
-    const dim3 grid((unsigned)b16_grid(v, g.M, g.N));
+void launch_b16(hipStream_t s, const GemmArgs& g0) {
+    const int v = b16_pick(g0);
+    const dim3 grid((unsigned)b16_grid(v, g0.M, g0.N));
+    GemmArgs g = g0;
+    g.gidx_lds = v != 13;
     if (g.st & 4) launch_b16_t<true>(v, grid, s, g);
     else launch_b16_t<false>(v, grid, s, g);
 }
@@ -649,7 +675,7 @@ void launch_b16(hipStream_t s, const GemmArgs& g) {
 }  // namespace bgnn
 
 extern "C" int bgnn_gemm_b16_variant(int32_t variant) {
-    BGNN_REQUIRE(variant >= -1 && variant <= 12, "gemm_b16_variant: must be -1 (off) or 0..12");
+    BGNN_REQUIRE(variant >= -1 && variant <= 13, "gemm_b16_variant: must be -1 (off) or 0..13");
     bgnn::g_b16_variant = variant;
     return BGNN_OK;
 }

@@ -42,6 +42,9 @@ struct GemmArgs {
     // drop-add epilogue: only columns >= bsrc_c0 take the beta operand, column c reading bsrc column
     // c - bsrc_c0 (a multiple of the tile width; the max layer's merged dgrad [dh W_l | dh W_r])
     int64_t bsrc_c0;
+    // LDS-DMA bf16 kernel (gemm_b16.hip), whole-line bf16 C with gathered rows: the tile's gi0 / gi1
+    // staged in LDS before the epilogue (1) or read from global memory per row (0, A/B variant 13)
+    int gidx_lds;
 };
 
 // the beta operand of 4 consecutive columns (col % 4 == 0) of row `row`: masked bsrc

@@ -53,6 +53,8 @@ P1 = torch.randn(NN, H, device=dev)
 P2 = torch.randn(NN, H, device=dev)
 i1 = torch.sort(torch.randint(0, NN, (E,), device=dev))[0]
 i2 = torch.randint(0, NN, (E,), device=dev)
+if os.environ.get("AB_MESH_IDX"):   # mesh-like locality: i2 near i1 (a neighbour within a few rows)
+    i2 = (i1 + torch.randint(-80, 81, (E,), device=dev)).clamp(0, NN - 1)
 
 
 def gather7():
@@ -95,6 +97,7 @@ cases = {
     "gather st7 b16 v10": v(10, lambda: gather7()),
     "gather st7 b16 v11": v(11, lambda: gather7()),
     "gather st7 b16 v12": v(12, lambda: gather7()),
+    "gather st7 b16 v13 (v11, idx global)": v(13, lambda: gather7()),
     "TN st0 (f32 g, f32 e)": lambda: fused.gemm_bf16(g32, x32, True, False),
     "TN st3 (bf16 g, bf16 e)": lambda: fused.gemm_bf16(g16, x16, True, False),
 }
@@ -108,7 +111,7 @@ print(f"{'NT st3 b16 v0':28s} bit-identical to x6: {torch.equal(cases['NT st3 b1
 print(f"{'NT st3 b16 v6':28s} bit-identical to x6: {torch.equal(cases['NT st3 b16 v6'](), ref3)}", flush=True)
 refg = cases["gather st7 x6"]()
 for k in ("gather st7 b16 v0", "gather st7 b16 v2", "gather st7 b16 v6", "gather st7 b16 v8", "gather st7 b16 v9",
-          "gather st7 b16 v10", "gather st7 b16 v11", "gather st7 b16 v12"):
+          "gather st7 b16 v10", "gather st7 b16 v11", "gather st7 b16 v12", "gather st7 b16 v13 (v11, idx global)"):
     print(f"{k:28s} bit-identical to x6: {torch.equal(cases[k](), refg)}", flush=True)
 del ref7, ref3, refg
 POISON[0] = False
