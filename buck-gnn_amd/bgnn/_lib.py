@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lock = threading.Lock()
 _lib = None
@@ -103,6 +103,8 @@ SIGNATURES = {
     "bgnn_linear_bwd_prep_bf16": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p]),
     "bgnn_absmax_items_f32": (c_i32, [c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p]),
     "bgnn_add_dropped_bf16": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p, c_p]),
+    "bgnn_gemm_bf16_dropadd": (c_i32, [c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f32,
+                                       c_u64, c_p]),
     "bgnn_rel_error_loss": (c_i32, [c_p, c_p, c_i64, c_f32, c_f32, c_f32, c_p, c_p, c_p]),
     "bgnn_small_linear_fwd": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_i32, c_p, c_p]),
     "bgnn_small_linear_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p]),

@@ -124,10 +124,17 @@ class _LinearGatherReLU(torch.autograd.Function):
             else:
                 g = torch.ops.aten.threshold_backward(g.contiguous(), out, 0.0)
                 db = torch.sum(g, 0, dtype=torch.float32) if ctx.has_bias else None
-            de = (gemm_bf16(g, W.t().contiguous(), False, True, out_bf16=e.dtype == torch.bfloat16)
-                  if ctx.needs_input_grad[0] else None)
-            if de is not None and ctx.slot is not None:
-                de = ctx.slot.add_to(de)   # + the skip + dropout's share of e's gradient, one pass
+            de = None
+            if ctx.needs_input_grad[0]:
+                slot = ctx.slot
+                if (slot is not None and slot.armed and GEMM_DROPADD and e.dtype == torch.bfloat16
+                        and g.dtype == torch.bfloat16):
+                    # + the skip + dropout's share of e's gradient in the dgrad GEMM's epilogue
+                    de = slot.gemm_dropadd(g, W)
+                else:
+                    de = gemm_bf16(g, W.t().contiguous(), False, True, out_bf16=e.dtype == torch.bfloat16)
+                    if slot is not None:
+                        de = slot.add_to(de)   # + the skip + dropout's share of e's gradient, one pass
             dW = gemm_bf16(g, e, True, False)
             if ctx.dp is not None:
                 cg, i1, i2 = ctx.dp
@@ -191,12 +198,33 @@ class GradSlot:
     def __init__(self):
         self.armed, self.g, self.p, self.seed = False, None, 0.0, 0
 
-    def add_to(self, de: torch.Tensor) -> torch.Tensor:
-        if not self.armed:
-            return de
+    def _arrived(self):
         if self.g is None:
             raise RuntimeError("GradSlot: the skip + dropout gradient had not arrived when the edge Linear's "
                                "backward ran (autograd order)")
+        return self.g
+
+    def gemm_dropadd(self, g: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+        """The consumer Linear's input gradient g W plus drop(slot gradient), both bf16, in one
+        launch (bgnn_gemm_bf16_dropadd: the same bits as gemm_bf16 followed by add_to)."""
+        src = self._arrived()
+        g = g.contiguous()
+        M, K = g.shape
+        N = W.size(1)
+        if src.shape != (M, N) or src.dtype != torch.bfloat16 or not src.is_contiguous():
+            raise RuntimeError("GradSlot: gradient shape / dtype mismatch")
+        wt = b16_weight(g, W.t().contiguous())   # W^T rounded to bf16 once (the B operand, [N, K])
+        if wt.dtype != torch.bfloat16 or K % 64 or N % 8:   # not the LDS-DMA kernel's shapes: two steps
+            return self.add_to(gemm_bf16(g, W.t().contiguous(), False, True, out_bf16=True))
+        de = torch.empty(M, N, dtype=torch.bfloat16, device=g.device)
+        _lib.call("bgnn_gemm_bf16_dropadd", M, N, K, g.data_ptr(), g.stride(0), wt.data_ptr(), wt.stride(0),
+                  de.data_ptr(), N, src.data_ptr(), N, float(self.p), self.seed, _stream())
+        return de
+
+    def add_to(self, de: torch.Tensor) -> torch.Tensor:
+        if not self.armed:
+            return de
+        self._arrived()
         de = de.contiguous()
         g = self.g
         if g.shape != de.shape or g.dtype != torch.bfloat16 or de.dtype != torch.bfloat16:
@@ -280,6 +308,9 @@ BF16_STORAGE = True
 # bf16 storage: the two gradients of every edge activation (an edge Linear's input gradient and the
 # skip + dropout's) summed by the Linear's backward in one pass (GradSlot) instead of autograd's add
 FUSED_GRAD_ADD = True
+# ... and that sum in the dgrad GEMM's epilogue (bgnn_gemm_bf16_dropadd) instead of a pass over the
+# GEMM's stored output (A/B switch; the same bits)
+GEMM_DROPADD = True
 
 
 def _add_dropout(a: torch.Tensor, b, p: float, seed: int) -> torch.Tensor:

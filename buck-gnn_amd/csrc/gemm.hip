@@ -783,6 +783,54 @@ static int gather_add_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t
     return BGNN_OK;
 }
 
+// C = round(round(A B^T) + drop(src)) with A [M, K], B [N, K], C and src [M, N] all bf16 (ABI 11):
+// EA_GNN's edge Linear dgrad plus the skip + dropout's share of the same activation's gradient
+// (bgnn/ea.py GradSlot), in the LDS-DMA kernel's epilogue -- the bits of bgnn_gemm_bf16 (storage 7)
+// followed by bgnn_add_dropped_bf16(C, src), without C's write and read back. Mask: keep_bits4(seed,
+// (row * ld_src + col) / 4), kept values / (1 - p); ld_src == N == ldc (the flat index the two-step
+// form masks by). Forms other than the whole-line bf16 C kernel, and operands the LDS-DMA kernel does not
+// take, run those two steps.
+extern "C" int bgnn_add_dropped_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
+                                     void* stream);
+extern "C" int bgnn_gemm_bf16(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, float alpha, const void* A,
+                              int64_t lda, const void* B, int64_t ldb, float beta, void* C, int64_t ldc,
+                              const float* bias, int32_t relu, int32_t storage, void* ws, size_t ws_bytes,
+                              void* stream);
+extern "C" int bgnn_gemm_bf16_dropadd(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                                      int64_t ldb, void* C, int64_t ldc, const void* src, int64_t ld_src, float p,
+                                      uint64_t seed, void* stream) {
+    BGNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_bf16_dropadd: negative size");
+    BGNN_REQUIRE(p >= 0.f && p < 1.f, "gemm_bf16_dropadd: p must be in [0, 1)");
+    BGNN_REQUIRE(ldc == N && ld_src == N && lda >= K && ldb >= K, "gemm_bf16_dropadd: need ldc == ld_src == N");
+    if (M == 0 || N == 0) return BGNN_OK;
+    BGNN_REQUIRE(A && B && C && src && N % 8 == 0, "gemm_bf16_dropadd: null pointer or N % 8 != 0");
+    hipStream_t s = as_stream(stream);
+    GemmArgs g{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), nullptr,
+               M, N, K, lda, ldb, ldc, 1.f, 0.f, K, 1, nullptr, 0, 0, 0, 0, 0, nullptr, nullptr, nullptr};
+    g.st = 7;
+    if (!b16_ok(g, 0, 1)) {   // (K % 64, alignment, lda / ldb % 8, or b16 variant -1): the two steps
+        const int rc = bgnn_gemm_bf16(0, 1, M, N, K, 1.f, A, lda, B, ldb, 0.f, C, ldc, nullptr, 0, 7, nullptr, 0,
+                                      stream);
+        if (rc != BGNN_OK) return rc;
+        return bgnn_add_dropped_bf16(C, src, M * N, p, seed, C, stream);
+    }
+    GemmArgs gd = g;
+    gd.bsrc = static_cast<const float*>(src);
+    gd.ld_bsrc = ld_src;
+    gd.dseed = seed;
+    gd.dthr = dropout_threshold(p);
+    gd.dkeep = gd.dthr ? 1.f / (1.f - p) : 1.f;
+    gd.st = 7 | 8;
+    if (b16_dropadd_ok(gd)) {
+        launch_b16(s, gd);
+        BGNN_CHECK_LAUNCH();
+        return BGNN_OK;
+    }
+    launch_b16(s, g);
+    BGNN_CHECK_LAUNCH();
+    return bgnn_add_dropped_bf16(C, src, M * N, p, seed, C, stream);
+}
+
 extern "C" int bgnn_gemm_gather_add(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_t K, const float* A,
                                     int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                                     const float* bias, int32_t relu, const float* add0, const int64_t* idx0,

@@ -179,13 +179,11 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
     const int rq = lane / LPR, cq = (lane % LPR) * CPL;
     const bool gvec = (!g.ga0 || ((((uintptr_t)g.ga0 & 15) == 0) && g.ldg0 % 4 == 0)) &&
                       (!g.ga1 || ((((uintptr_t)g.ga1 & 15) == 0) && g.ldg1 % 4 == 0));
-    const bool fast = gvec && (((uintptr_t)g.C & 15) == 0) && g.ldc % 8 == 0 &&
-                      (!g.bias || (((uintptr_t)g.bias & 15) == 0)) && r0 + TM * 32 <= g.M && c0 + TN * 32 <= g.N;
-    if (!fast) {
-        x6_epilogue<TM, TN, 0, C16>(g, acc, r0, c0, c0, 0, lane, 1.f, 1.f, stage);
-        return;
-    }
+    const bool fast_cols = gvec && (((uintptr_t)g.C & 15) == 0) && g.ldc % 8 == 0 &&
+                           (!g.bias || (((uintptr_t)g.bias & 15) == 0)) && c0 + TN * 32 <= g.N;
+    const bool fast = fast_cols && r0 + TM * 32 <= g.M;
     if constexpr (C16 && TN % 2 == 0 && WIDE) {
+      if (fast_cols) {   // rows past M (the last row tile) are skipped row by row
         // bf16 C in whole 128-B lines: two adjacent 32-column blocks (64 bf16 columns) of 32 rows
         // staged together ([32][68] f32: the row pad keeps the two half-waves' ds_write_b32 rows
         // on different banks), then 8 lanes x 16 B per row -- a 32-column block alone is a 64-B
@@ -212,6 +210,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                 for (int q = 0; q < 4; ++q) {
                     const int rr = q * 8 + rq8;
                     const int64_t row = r0 + i * 32 + rr;
+                    if (row >= g.M) continue;
                     float e[8], x0[8], x1[8];
 #pragma unroll
                     for (int k = 0; k < 8; k += 4) {
@@ -244,6 +243,30 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                         if (g.relu) v = fmaxf(v, 0.f);
                         e[k] = v;
                     }
+                    if (g.st & 8) {
+                        // drop-add (bgnn_gemm_bf16_dropadd): the bf16 value this epilogue would store,
+                        // + drop(src) in f32, one more rounding -- bgnn_add_dropped_bf16 on the stored C,
+                        // bit for bit (mask group (row * ld + col) / 4, kept values * dkeep)
+                        const int64_t si = row * g.ld_bsrc + col;
+                        const uint4 sv = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(g.bsrc) + si);
+                        const uint32_t sw[4] = {sv.x, sv.y, sv.z, sv.w};
+                        float d[8];
+#pragma unroll
+                        for (int h = 0; h < 4; ++h) {
+                            d[2 * h] = __uint_as_float(sw[h] << 16);
+                            d[2 * h + 1] = __uint_as_float(sw[h] & 0xffff0000u);
+                        }
+                        if (g.dthr) {
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                const uint32_t keep = keep_bits4(g.dseed, (uint64_t)(si >> 2) + h, g.dthr);
+#pragma unroll
+                                for (int k = 0; k < 4; ++k) d[4 * h + k] = ((keep >> k) & 1u) ? d[4 * h + k] * g.dkeep : 0.f;
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) e[k] = __uint_as_float(pack_bf16(e[k], 0.f) << 16) + d[k];
+                    }
                     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
                     const u32x4_t w = {pack_bf16(e[0], e[1]), pack_bf16(e[2], e[3]), pack_bf16(e[4], e[5]),
                                        pack_bf16(e[6], e[7])};
@@ -253,6 +276,11 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         }
+        return;
+      }
+    }
+    if (!fast) {
+        x6_epilogue<TM, TN, 0, C16>(g, acc, r0, c0, c0, 0, lane, 1.f, 1.f, stage);
         return;
     }
 #pragma unroll
@@ -607,7 +635,7 @@ constexpr int64_t kPersistentWgs = 256;   // MI355X CUs   // -1: bf16-stored NT 
 bool b16_ok(const GemmArgs& g, int ta, int tb) {
     constexpr int64_t kMaxTileBytes = int64_t(1) << 31;
     return g_b16_variant >= 0 && ta == 0 && tb == 1 && (g.st & 3) == 3 && g.split <= 1 && g.K > 0 && g.K % 64 == 0 &&
-           g.a_blk == 0 && g.c_blk == 0 && g.bsrc == nullptr && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+           g.a_blk == 0 && g.c_blk == 0 && (g.bsrc == nullptr || (g.st & 8)) && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
            aligned16(g.A) && aligned16(g.B) && 256 * g.lda * 2 < kMaxTileBytes && 256 * g.ldb * 2 < kMaxTileBytes;
 }
 
@@ -661,6 +689,14 @@ static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
         default:  // 7: 256x256, k64 slices (whole 128-B row segments) x 2 slots
             hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
     }
+}
+
+// the variant launch_b16 runs implements the drop-add (st bit 8) epilogue: the whole-line bf16 C
+// forms (WIDE)
+bool b16_dropadd_ok(const GemmArgs& g) {
+    const int v = b16_pick(g);
+    return (v == 11 || v == 12 || v == 13) && (g.st & 7) == 7 && g.N % 256 == 0 && g.ldc % 8 == 0 &&
+           g.ld_bsrc % 8 == 0 && aligned16(g.C) && aligned16(g.bsrc);
 }
 
 void launch_b16(hipStream_t s, const GemmArgs& g0) {

@@ -34,7 +34,8 @@ struct GemmArgs {
     // values scaled by dkeep; dthr = 0: no mask), so bgnn_sage_bwd_rows need not write it
     const float* bsrc; int64_t ld_bsrc; uint64_t dseed; uint32_t dthr; float dkeep;
     // bf16-operand family (PREC 2) only: bf16 STORAGE of A (bit 0), B (bit 1), C (bit 2) -- the
-    // pointers then address bf16 elements and lda / ldb / ldc count bf16 elements
+    // pointers then address bf16 elements and lda / ldb / ldc count bf16 elements; bit 3 (LDS-DMA
+    // bf16 kernel, bf16 C): bsrc holds bf16 and is added through its mask to the ROUNDED product
     int st;
     // f16x3 C = A B^T only: B points to a pre-split image of B^T (bgnn_gemm_wsplit, column tile =
     // the launch tile's BN) instead of f32 rows; the kernel copies its LDS image
@@ -95,6 +96,9 @@ void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_
 // launch_b16 covers all M rows (no tail split; tile / persistent form picked per call)
 bool b16_ok(const GemmArgs& g, int ta, int tb);
 void launch_b16(hipStream_t s, const GemmArgs& g);
+// the launch would run the drop-add epilogue (st bit 8: bsrc = bf16 [M, ld_bsrc] through the dropout
+// mask, added to the stored bf16 C) -- a whole-line bf16 C variant, N % 256 == 0, aligned C / bsrc
+bool b16_dropadd_ok(const GemmArgs& g);
 // folds max |P| over the rows x cols matrix (ld; plane-split by blk / pstride when blk > 0)
 // into *out (f32 bits, unsigned atomic max; *out must hold a non-negative value)
 void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64_t blk, int64_t pstride,

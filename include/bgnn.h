@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 10
+#define BGNN_ABI_VERSION 11
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -355,6 +355,14 @@ int bgnn_add_dropout_bf16(const void* a, const void* b, int64_t n, float p, uint
  * an edge Linear's input gradient (a) and the skip + dropout's gradient (b) in one pass. */
 int bgnn_add_dropped_bf16(const void* a, const void* b, int64_t n, float p, uint64_t seed, void* out,
                           void* stream);
+/* ABI 11: C = round(round(A B^T) + drop(src)), A [M, K], B [N, K], C and src [M, N] all bf16,
+ * ldc == ld_src == N -- bgnn_gemm_bf16 (storage 7) followed by bgnn_add_dropped_bf16(C, src) bit for
+ * bit, the add done in the LDS-DMA kernel's epilogue (EA_GNN's edge Linear dgrad + the skip +
+ * dropout's gradient of the same activation). Needs K % 64 == 0, lda / ldb % 8 == 0, 16-B aligned
+ * operands; the forms without that epilogue run the two steps. */
+int bgnn_gemm_bf16_dropadd(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                           int64_t ldb, void* C, int64_t ldc, const void* src, int64_t ld_src, float p,
+                           uint64_t seed, void* stream);
 int bgnn_segment_sum_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const void* x,
                           int64_t ldx, int32_t H, int32_t mean, float* out, int64_t ldo, void* stream);
 /* Backward of bgnn_segment_sum_bf16 (ABI 10): every position p of segment r (the CSR's col lists

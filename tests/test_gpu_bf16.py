@@ -270,3 +270,32 @@ def test_rel_error_loss_kernel_nan_like_torch(dev):
     assert torch.isnan(got) and torch.isnan(ref)
     assert g[1].item() == gref[1].item() == 0.0
     torch.testing.assert_close(g[[0, 2, 3]], gref[[0, 2, 3]], rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("mnk", [(1000, 512, 512), (70001, 512, 512), (4099, 256, 128), (300, 256, 96)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_bf16_dropadd_bit_identical_to_two_steps(dev, b16_variant, mnk, p):
+    """bgnn_gemm_bf16_dropadd (EA_GNN's edge Linear dgrad + the skip + dropout's gradient of the same
+    activation, ea.GradSlot.gemm_dropadd): the drop-add in the LDS-DMA kernel's epilogue equals
+    bgnn_gemm_bf16 (bf16 C) followed by bgnn_add_dropped_bf16 on the stored C, bit for bit -- ragged
+    M (the last row tile), N = 256 / 512, K % 64 != 0 (the two-step fallback), every kernel form
+    (the whole-line bf16 C forms with the fused add, the others and the register-staged kernel by
+    the two steps)."""
+    M, N, K = mnk
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+    src = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def fused_():
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=dev)
+        _lib.call("bgnn_gemm_bf16_dropadd", M, N, K, a.data_ptr(), K, w.data_ptr(), K, out.data_ptr(), N,
+                  src.data_ptr(), N, float(p), 77, s)
+        return out
+
+    ref = fused.gemm_bf16(a, w, False, True, out_bf16=True)
+    _lib.call("bgnn_add_dropped_bf16", ref.data_ptr(), src.data_ptr(), M * N, float(p), 77, ref.data_ptr(), s)
+    for v in (0, 11, 12, 13, 6, 1, -1):
+        b16_variant(v)
+        assert torch.equal(fused_(), ref), v

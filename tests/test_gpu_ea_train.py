@@ -85,7 +85,8 @@ def test_ea_bf16_grad_handoff_matches_autograd_add(dev, monkeypatch):
     """EA_GNN bf16 with dropout 0.1 (the cfg5 training configuration): the edge-gradient hand-off
     (bgnn.ea.GradSlot: an edge Linear's input gradient + the skip/dropout gradient in one pass) is
     taken in every block but the last, and every parameter gradient matches the path where
-    autograd adds the two (same dropout masks) to bf16 rounding."""
+    autograd adds the two (same dropout masks) to bf16 rounding; the add in the dgrad GEMM's
+    epilogue gives the bits of the separate add pass."""
     from bgnn import ea
     b = S.make_batch(12, 4).to(dev)
     crit, norm = bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5)
@@ -94,15 +95,21 @@ def test_ea_bf16_grad_handoff_matches_autograd_add(dev, monkeypatch):
     model.train()
     model.ea_bf16 = True
     used = []
-    orig = ea.GradSlot.add_to
+    orig, orig_gemm = ea.GradSlot.add_to, ea.GradSlot.gemm_dropadd
 
     def counting(self, de):
         used.append(self.armed)
         return orig(self, de)
-    monkeypatch.setattr(ea.GradSlot, "add_to", counting)
 
-    def grads(handoff):
+    def counting_gemm(self, g, W):
+        used.append(self.armed)
+        return orig_gemm(self, g, W)
+    monkeypatch.setattr(ea.GradSlot, "add_to", counting)
+    monkeypatch.setattr(ea.GradSlot, "gemm_dropadd", counting_gemm)
+
+    def grads(handoff, in_gemm=True):
         monkeypatch.setattr(ea, "FUSED_GRAD_ADD", handoff)
+        monkeypatch.setattr(ea, "GEMM_DROPADD", in_gemm)
         model.zero_grad(set_to_none=True)
         torch.manual_seed(123)   # the same dropout seeds (bgnn.BuckGNN._seed) in both runs
         pred, _ = model(b.x, b.edge_index, b.edge_attr, b.batch)
@@ -117,3 +124,10 @@ def test_ea_bf16_grad_handoff_matches_autograd_add(dev, monkeypatch):
     assert got.keys() == ref.keys()
     for k in ref:
         torch.testing.assert_close(got[k], ref[k], rtol=3e-2, atol=3e-2 * (1e-6 + ref[k].abs().max().item()), msg=k)
+    # the hand-off's add in the dgrad GEMM's epilogue (bgnn_gemm_bf16_dropadd) or as its own pass
+    # over the stored GEMM output (bgnn_add_dropped_bf16): the same bits
+    used.clear()
+    two_step = grads(True, in_gemm=False)
+    assert sum(used) == 9
+    for k in got:
+        assert torch.equal(got[k], two_step[k]), k
