@@ -29,7 +29,7 @@ import torch
 
 from . import _lib
 from . import fused
-from .fused import b16_weight, gemm, gemm_bf16, linear, linear_bf16, mlp, relu_bias_grad
+from .fused import Pair, Planes, b16_weight, gemm, gemm_bf16, linear, linear_bf16, mlp, relu_bias_grad
 from .graph import SegmentIndex, _index_cache, _stream
 from .ops import segment_reduce
 
@@ -294,8 +294,55 @@ class _ColumnBlocks(torch.autograd.Function):
         return torch.cat(gs, 1), None, None
 
 
+class _PairLinear(torch.autograd.Function):
+    """act([x | agg] W^T + b) with bf16 operands for node_mlp_gamma's first Linear
+    (Models/BuckGNN.py:560, `node_mlp_gamma(torch.cat([x, agg], 1))`), [x | agg] read in place as
+    two planes of the GEMM's A operand (fused.Pair) instead of a [N, 2H] torch.cat; backward: the
+    ReLU mask and bias sum (relu_bias_grad), [dx | dagg] = g' W written as two planes (each a dense
+    [N, H] gradient, no slicing of a [N, 2H] one), dW = ([x | agg]^T g')^T. The forward and dx / dagg
+    are the bits of LinearFn on the concatenation (the bf16 tiles all sum in increasing k); dW is
+    the transposed product (its split-K grouping may differ: rounding-equal)."""
+
+    @staticmethod
+    def forward(ctx, x, agg, weight, bias, relu: bool):
+        y = gemm(Pair(x, agg), weight.contiguous(), trans_a=False, trans_b=True, bias=bias, relu=relu, bf16=True)
+        ctx.relu, ctx.has_bias = relu, bias is not None
+        ctx.save_for_backward(x, agg, weight, y if relu else torch.empty(0, device=x.device))
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, agg, weight, y = ctx.saved_tensors
+        g, db, _ = relu_bias_grad(g, y if ctx.relu else None, ctx.has_bias)
+        dx = dagg = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            N, H = x.shape
+            t = torch.empty(2, N, H, dtype=torch.float32, device=x.device)
+            gemm(g, weight.t().contiguous(), trans_a=False, trans_b=True, out=Planes(t), bf16=True)
+            dx, dagg = t[0], t[1]
+        dwt = gemm(Pair(x, agg), g, trans_a=True, trans_b=False, bf16=True)   # [2H, H_out]
+        return dx, dagg, dwt.t(), db, None
+
+
+def _gamma_mlp(seq: torch.nn.Sequential, x: torch.Tensor, agg: torch.Tensor) -> torch.Tensor:
+    """node_mlp_gamma([x | agg]) in bf16 operands: the first Linear on the two planes (_PairLinear)
+    when the halves qualify, the rest through fused.mlp; else mlp over torch.cat."""
+    mods = list(seq)
+    ok = (PAIR_GAMMA and fused.GEMM_BACKEND == "hip" and len(mods) >= 1 and isinstance(mods[0], torch.nn.Linear)
+          and x.shape == agg.shape and x.dtype == agg.dtype == torch.float32 and x.is_contiguous()
+          and agg.is_contiguous() and x.size(1) % 256 == 0 and (agg.data_ptr() - x.data_ptr()) % 16 == 0)
+    if not ok:
+        return mlp(seq, torch.cat([x, agg], 1), bf16=True)
+    relu = len(mods) > 1 and isinstance(mods[1], torch.nn.ReLU)
+    h = _PairLinear.apply(x, agg, mods[0].weight, mods[0].bias, relu)
+    rest = mods[2 if relu else 1:]
+    return mlp(torch.nn.Sequential(*rest), h, bf16=True) if rest else h
+
+
 # the two-step form (linear, then _GatherAdd) is kept for A/B measurement
 FUSED_GATHER = True
+# bf16 storage: node_mlp_gamma's first Linear reads [x | agg] as two GEMM planes (no torch.cat)
+PAIR_GAMMA = True
 # bf16 storage: the P column blocks' gradients written into one shared buffer (ColGrad, A/B switch)
 COLGRAD = True
 # EA_GNN's skip add + dropout over [E, H] / [N, H] as one pass (bgnn_add_dropout)
@@ -384,7 +431,7 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
         with fused._timed("ea_edge_fwd"):
             msg = linear_bf16(m1, Wp2, bp2, False, True)
         agg = segment_reduce(msg, seg_row, "mean")
-        out = mlp(blk.node_mlp_gamma, torch.cat([x, agg], 1), bf16=True)
+        out = _gamma_mlp(blk.node_mlp_gamma, x, agg)
         out = out + mlp(blk.node_mlp_beta, out, bf16=True)
         return out, e_out
     with fused._timed("ea_edge_fwd"):

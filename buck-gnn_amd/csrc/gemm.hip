@@ -402,19 +402,21 @@ struct Plan {
 static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a_blk, int64_t c_blk,
                       int precision = 0, bool wb = false) {
     Plan p{};
+    auto planes_ok = [&](int bm, int bn, int bk) {
+        return (a_blk == 0 || a_blk % (ta ? bm : bk) == 0) && (c_blk == 0 || c_blk % bn == 0);
+    };
     if (precision == 1) {   // bf16 operands, f32 accumulation (the split kernel with one piece)
         p.x6 = 1;
         p.prec = 2;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, 1);
         if (p.cfg == kX6CfgWB) p.cfg = 4;
-        if (a_blk != 0 || c_blk != 0) p.cfg = 0;
+        // plane blocks must be whole tiles (every bf16 tile gives the same bits: 16x16x32 MFMAs
+        // in increasing k), else the 128x128 tile
+        if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
         p.bm = kX6Cfgs[p.cfg].bm; p.bn = kX6Cfgs[p.cfg].bn; p.bk = 32;
         p.split = choose_split(M, N, K, GemmCfg{p.bm, p.bn, p.bk, kX6Cfgs[p.cfg].waves, kX6Cfgs[p.cfg].blocks_per_cu});
         return p;
     }
-    auto planes_ok = [&](int bm, int bn, int bk) {
-        return (a_blk == 0 || a_blk % (ta ? bm : bk) == 0) && (c_blk == 0 || c_blk % bn == 0);
-    };
     if (g_gemm_mode == 2) {
         p.x6 = 1;
         p.prec = 1;

@@ -131,3 +131,42 @@ def test_ea_bf16_grad_handoff_matches_autograd_add(dev, monkeypatch):
     assert sum(used) == 9
     for k in got:
         assert torch.equal(got[k], two_step[k]), k
+
+
+def test_ea_pair_gamma_matches_cat(dev, monkeypatch):
+    """EA_GNN bf16: node_mlp_gamma's first Linear on [x | agg] read as two GEMM planes
+    (bgnn.ea._PairLinear, no torch.cat; Models/BuckGNN.py:560) gives the forward of the
+    concatenation path bit for bit, and the same gradients to rounding (the gamma weight's gradient
+    is the transposed product, and autograd's sum order over a node tensor's consumers changes)."""
+    from bgnn import ea
+    b = S.make_batch(12, 4).to(dev)
+    crit, norm = bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5)
+    torch.manual_seed(0)
+    model = bgnn.BuckGNN(16, 5, hidden_channels=256, num_layers=3, dropout_rate=0.0, model_name="EA_GNN").to(dev)
+    model.train()
+    model.ea_bf16 = True
+    calls = []
+    real_apply = ea._PairLinear.apply
+
+    def spy(*a):
+        calls.append(1)
+        return real_apply(*a)
+    monkeypatch.setattr(ea._PairLinear, "apply", spy)
+
+    def run(pair):
+        monkeypatch.setattr(ea, "PAIR_GAMMA", pair)
+        model.zero_grad(set_to_none=True)
+        torch.manual_seed(7)
+        pred, _ = model(b.x, b.edge_index, b.edge_attr, b.batch)
+        crit(norm.denormalize_eigenvalue(pred), norm.denormalize_eigenvalue(b.y)).backward()
+        return pred.detach().clone(), {k: p.grad.detach().clone() for k, p in model.named_parameters()
+                                       if p.grad is not None}
+
+    p1, g1 = run(True)
+    assert len(calls) == 3
+    p0, g0 = run(False)
+    assert len(calls) == 3
+    assert torch.equal(p1, p0)
+    assert g1.keys() == g0.keys()
+    for k in g0:   # (autograd may sum a node tensor's gradient contributions in another order)
+        torch.testing.assert_close(g1[k], g0[k], rtol=1e-4, atol=1e-5 * (1e-6 + g0[k].abs().max().item()), msg=k)
