@@ -339,8 +339,70 @@ def _gamma_mlp(seq: torch.nn.Sequential, x: torch.Tensor, agg: torch.Tensor) -> 
     return mlp(torch.nn.Sequential(*rest), h, bf16=True) if rest else h
 
 
+_IDENTITY = {}
+
+
+def _identity_index(n: int, device) -> torch.Tensor:
+    key = (n, str(device))
+    t = _IDENTITY.get(key)
+    if t is None:
+        t = _IDENTITY[key] = torch.arange(n, dtype=torch.int64, device=device)
+    return t
+
+
+class _LinearResidual(torch.autograd.Function):
+    """r + (h W^T + b) with bf16 operands as ONE GEMM whose epilogue adds row r[i] to output row i
+    (bgnn_gemm_gather_add with the identity index): node_mlp_beta's last Linear and the residual
+    `out + node_mlp_beta(out)` (Models/BuckGNN.py:561), the bits of LinearFn followed by torch's add
+    (the epilogue adds bias, then the row) without the [N, H] add pass. Backward: LinearFn's
+    (relu_bias_grad for the bias sum, dgrad and wgrad GEMMs), and g itself for r."""
+
+    @staticmethod
+    def forward(ctx, h, weight, bias, r):
+        h = h.contiguous()
+        M, K = h.shape
+        N = weight.size(0)
+        W = weight.contiguous()
+        out = torch.empty(M, N, dtype=torch.float32, device=h.device)
+        idx = _identity_index(M, h.device)
+        ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, 0, 1, 1)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=h.device) if ws_bytes else None
+        _lib.call("bgnn_gemm_gather_add", 0, 1, M, N, K, h.data_ptr(), h.stride(0), W.data_ptr(), W.stride(0),
+                  out.data_ptr(), N, None if bias is None else bias.contiguous().data_ptr(), 0,
+                  r.data_ptr(), idx.data_ptr(), r.stride(0), None, None, 0, 1,
+                  None if ws is None else ws.data_ptr(), ws_bytes, _stream())
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(h, weight)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, weight = ctx.saved_tensors
+        gg, db, _ = relu_bias_grad(g, None, ctx.has_bias)
+        dh = gemm(gg, weight.t().contiguous(), trans_a=False, trans_b=True, bf16=True) if ctx.needs_input_grad[0] else None
+        dw = gemm(gg, h, trans_a=True, trans_b=False, bf16=True)
+        return dh, dw, db, g
+
+
+def _beta_residual(seq: torch.nn.Sequential, out: torch.Tensor) -> torch.Tensor:
+    """out + node_mlp_beta(out) in bf16 operands: the last Linear and the add as one GEMM
+    (_LinearResidual) when it qualifies, else fused.mlp and torch's add."""
+    mods = list(seq)
+    ok = (RESIDUAL_EPILOGUE and fused.GEMM_BACKEND == "hip" and _epilogue_gather_available() and len(mods) >= 1
+          and isinstance(mods[-1], torch.nn.Linear) and out.dtype == torch.float32 and out.is_contiguous()
+          and out.size(1) == mods[-1].weight.size(0) and out.size(1) % 4 == 0 and out.data_ptr() % 16 == 0)
+    if not ok:
+        return out + mlp(seq, out, bf16=True)
+    h = mlp(torch.nn.Sequential(*mods[:-1]), out, bf16=True) if len(mods) > 1 else out
+    return _LinearResidual.apply(h, mods[-1].weight, mods[-1].bias, out)
+
+
 # the two-step form (linear, then _GatherAdd) is kept for A/B measurement
 FUSED_GATHER = True
+# bf16 storage: node_mlp_beta's last Linear adds the residual in its epilogue (no [N, H] add pass).
+# Off: measured equal to the separate add (cfg5 204.0-204.7 either way, tools/ab_ea_residual.sh,
+# profiles/r05_ab_ea_residual.txt) -- the gathered-row epilogue costs what the add pass did
+RESIDUAL_EPILOGUE = False
 # bf16 storage: node_mlp_gamma's first Linear reads [x | agg] as two GEMM planes (no torch.cat)
 PAIR_GAMMA = True
 # bf16 storage: the P column blocks' gradients written into one shared buffer (ColGrad, A/B switch)
@@ -432,7 +494,7 @@ def graphnet_block(blk, x: torch.Tensor, e: torch.Tensor, edge_index: torch.Tens
             msg = linear_bf16(m1, Wp2, bp2, False, True)
         agg = segment_reduce(msg, seg_row, "mean")
         out = _gamma_mlp(blk.node_mlp_gamma, x, agg)
-        out = out + mlp(blk.node_mlp_beta, out, bf16=True)
+        out = _beta_residual(blk.node_mlp_beta, out)
         return out, e_out
     with fused._timed("ea_edge_fwd"):
         if FUSED_GATHER:

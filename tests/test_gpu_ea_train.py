@@ -133,11 +133,14 @@ def test_ea_bf16_grad_handoff_matches_autograd_add(dev, monkeypatch):
         assert torch.equal(got[k], two_step[k]), k
 
 
-def test_ea_pair_gamma_matches_cat(dev, monkeypatch):
-    """EA_GNN bf16: node_mlp_gamma's first Linear on [x | agg] read as two GEMM planes
-    (bgnn.ea._PairLinear, no torch.cat; Models/BuckGNN.py:560) gives the forward of the
-    concatenation path bit for bit, and the same gradients to rounding (the gamma weight's gradient
-    is the transposed product, and autograd's sum order over a node tensor's consumers changes)."""
+@pytest.mark.parametrize("switch,fn", [("PAIR_GAMMA", "_PairLinear"), ("RESIDUAL_EPILOGUE", "_LinearResidual")])
+def test_ea_node_mlp_fusions_match_torch_ops(dev, monkeypatch, switch, fn):
+    """EA_GNN bf16 node MLPs (Models/BuckGNN.py:560-561): node_mlp_gamma's first Linear on [x | agg]
+    read as two GEMM planes (bgnn.ea._PairLinear, no torch.cat), and node_mlp_beta's last Linear
+    with the residual `out + beta(out)` added in its epilogue (bgnn.ea._LinearResidual), each give
+    the forward of the torch-op path bit for bit and the same gradients to rounding (the gamma
+    weight's gradient is the transposed product, and autograd's sum order over a node tensor's
+    consumers changes)."""
     from bgnn import ea
     b = S.make_batch(12, 4).to(dev)
     crit, norm = bgnn.RelativeErrorLoss(), bgnn.EigenvalueScaler(1.0, 0.5)
@@ -146,15 +149,15 @@ def test_ea_pair_gamma_matches_cat(dev, monkeypatch):
     model.train()
     model.ea_bf16 = True
     calls = []
-    real_apply = ea._PairLinear.apply
+    real_apply = getattr(ea, fn).apply
 
     def spy(*a):
         calls.append(1)
         return real_apply(*a)
-    monkeypatch.setattr(ea._PairLinear, "apply", spy)
+    monkeypatch.setattr(getattr(ea, fn), "apply", spy)
 
     def run(pair):
-        monkeypatch.setattr(ea, "PAIR_GAMMA", pair)
+        monkeypatch.setattr(ea, switch, pair)
         model.zero_grad(set_to_none=True)
         torch.manual_seed(7)
         pred, _ = model(b.x, b.edge_index, b.edge_attr, b.batch)
