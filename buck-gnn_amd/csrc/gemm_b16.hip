@@ -203,6 +203,18 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
+                // drop-add source rows of this 32-row block issued before the staging, so their
+                // latency runs under the LDS writes and waits
+                uint4 spre[4];
+                if (g.st & 8) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int64_t row = r0 + i * 32 + q * 8 + rq8;
+                        spre[q] = row < g.M ? *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(g.bsrc) +
+                                                                             row * g.ld_bsrc + col)
+                                            : make_uint4(0u, 0u, 0u, 0u);
+                    }
+                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) b16_stage_block(stage, LDW, h * 32, 0, acc, i, j + h, lane);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -248,7 +260,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                         // + drop(src) in f32, one more rounding -- bgnn_add_dropped_bf16 on the stored C,
                         // bit for bit (mask group (row * ld + col) / 4, kept values * dkeep)
                         const int64_t si = row * g.ld_bsrc + col;
-                        const uint4 sv = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(g.bsrc) + si);
+                        const uint4 sv = spre[q];
                         const uint32_t sw[4] = {sv.x, sv.y, sv.z, sv.w};
                         float d[8];
 #pragma unroll

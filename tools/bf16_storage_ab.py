@@ -65,6 +65,18 @@ def gather7():
     return out
 
 
+def dropadd(fused_epi):
+    out = torch.empty(E, H, dtype=torch.bfloat16, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    if fused_epi:
+        _lib.call("bgnn_gemm_bf16_dropadd", E, H, H, g16.data_ptr(), H, W16.data_ptr(), H, out.data_ptr(), H,
+                  x16.data_ptr(), H, 0.1, 5, s)
+    else:
+        fused.gemm_bf16(g16, W16, False, True, out=out)
+        _lib.call("bgnn_add_dropped_bf16", out.data_ptr(), x16.data_ptr(), E * H, 0.1, 5, out.data_ptr(), s)
+    return out
+
+
 st7 = lambda: fused.gemm_bf16(x16, W16, False, True, out_bf16=True, bias=bias, relu=True)   # noqa: E731
 st3 = lambda: fused.gemm_bf16(x16, W16, False, True, bias=bias, relu=True)                  # noqa: E731
 cases = {
@@ -98,6 +110,8 @@ cases = {
     "gather st7 b16 v11": v(11, lambda: gather7()),
     "gather st7 b16 v12": v(12, lambda: gather7()),
     "gather st7 b16 v13 (v11, idx global)": v(13, lambda: gather7()),
+    "dropadd b16 (fused)": lambda: dropadd(True),
+    "dropadd two-step": lambda: dropadd(False),
     "TN st0 (f32 g, f32 e)": lambda: fused.gemm_bf16(g32, x32, True, False),
     "TN st3 (bf16 g, bf16 e)": lambda: fused.gemm_bf16(g16, x16, True, False),
 }
@@ -113,6 +127,8 @@ refg = cases["gather st7 x6"]()
 for k in ("gather st7 b16 v0", "gather st7 b16 v2", "gather st7 b16 v6", "gather st7 b16 v8", "gather st7 b16 v9",
           "gather st7 b16 v10", "gather st7 b16 v11", "gather st7 b16 v12", "gather st7 b16 v13 (v11, idx global)"):
     print(f"{k:28s} bit-identical to x6: {torch.equal(cases[k](), refg)}", flush=True)
+print(f"{'dropadd fused':28s} bit-identical to two-step: {torch.equal(cases['dropadd b16 (fused)'](), cases['dropadd two-step']())}",
+      flush=True)
 del ref7, ref3, refg
 POISON[0] = False
 ts = {k: [] for k in cases}
