@@ -167,7 +167,7 @@ __device__ __forceinline__ float b16_acc_probe(const floatx4 (&acc)[TM2][TN2], i
 // C: 8 columns per lane (4 lanes per 64-B row segment; x6_epilogue stores 8 B). Per element the
 // arithmetic and its order are x6_epilogue's: acc, + bias, + ga0[gi0[row]], + ga1[gi1[row]],
 // ReLU, one bf16 rounding (RNE). Edge blocks fall back to x6_epilogue's element-guarded path.
-template <int TM, int TN, bool C16, bool WIDE = false, typename Acc>
+template <int TM, int TN, bool C16, bool WIDE = false, bool GPRE = false, typename Acc>
 __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
                                              int64_t c0, int lane, float* __restrict__ stage,
                                              const int64_t* __restrict__ li0 = nullptr,
@@ -206,6 +206,19 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                 // drop-add source rows of this 32-row block issued before the staging, so their
                 // latency runs under the LDS writes and waits
                 uint4 spre[4];
+                float4 gpre[4][2];   // the block's ga0 rows: [q][k0..3, k4..7] (ga1 stays in the loop)
+                if (GPRE && g.ga0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rr = q * 8 + rq8;
+                        const int64_t row = r0 + i * 32 + rr;
+                        if (row < g.M) {
+                            const float* s0 = g.ga0 + (li0 ? li0[i * 32 + rr] : g.gi0[row]) * g.ldg0 + col;
+                            gpre[q][0] = *reinterpret_cast<const float4*>(s0);
+                            gpre[q][1] = *reinterpret_cast<const float4*>(s0 + 4);
+                        }
+                    }
+                }
                 if (g.st & 8) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -229,7 +242,20 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                         const float4 sv = *reinterpret_cast<const float4*>(stage + rr * LDW + cq8 + k);
                         e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
                     }
-                    if (g.ga0) {
+                    if (GPRE && g.ga0) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            x0[k] = gpre[q][0][k]; x0[k + 4] = gpre[q][1][k];
+                        }
+                        if (g.ga1) {
+                            const float* s1 = g.ga1 + (li1 ? li1[i * 32 + rr] : g.gi1[row]) * g.ldg1 + col;
+#pragma unroll
+                            for (int k = 0; k < 8; k += 4) {
+                                const float4 t = *reinterpret_cast<const float4*>(s1 + k);
+                                x1[k] = t.x; x1[k + 1] = t.y; x1[k + 2] = t.z; x1[k + 3] = t.w;
+                            }
+                        }
+                    } else if (g.ga0) {
                         // the gather rows' indices from the tile's LDS copy when the kernel made one
                         const float* s0 = g.ga0 + (li0 ? li0[i * 32 + rr] : g.gi0[row]) * g.ldg0 + col;
 #pragma unroll
@@ -357,7 +383,8 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
 }
 
 // ABL: 0 = the kernel; 1 = timing ablation without the epilogue (one value per wave stored)
-template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, int ABL = 0, bool WIDE = false>
+template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, int ABL = 0, bool WIDE = false,
+          bool GPRE = false>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     using L = B16Slice<BK>;
     constexpr int NW = WM * WN;
@@ -454,7 +481,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     __syncthreads();   // every wave's fragment reads done before the epilogue reuses the LDS
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
     const int64_t* li = reinterpret_cast<const int64_t*>(smem + SMEM_U4) + wm * (BM / WM);
-    b16_epilogue<TM, TN, C16, WIDE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage,
+    b16_epilogue<TM, TN, C16, WIDE, GPRE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage,
                                     lidx ? li : nullptr, lidx && g.ga1 ? li + BM : nullptr);
 }
 
@@ -696,6 +723,8 @@ static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
         case 11:  // variant 7 with whole-line bf16 C stores (b16_epilogue WIDE); gathered rows'
                   // indices staged in LDS
             hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
+        case 14:  // variant 11 with each 32-row block's ga0 rows loaded before its staging
+            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 0, true, true>), grid, dim3(512), 0, s, g); break;
         case 12:  // variant 1 with whole-line bf16 C stores
             hipLaunchKernelGGL((k_gemm_b16<256, 256, 32, 4, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
         default:  // 7: 256x256, k64 slices (whole 128-B row segments) x 2 slots
@@ -707,7 +736,7 @@ static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
 // forms (WIDE)
 bool b16_dropadd_ok(const GemmArgs& g) {
     const int v = b16_pick(g);
-    return (v == 11 || v == 12 || v == 13) && (g.st & 7) == 7 && g.N % 256 == 0 && g.ldc % 8 == 0 &&
+    return (v == 11 || v == 12 || v == 13 || v == 14) && (g.st & 7) == 7 && g.N % 256 == 0 && g.ldc % 8 == 0 &&
            g.ld_bsrc % 8 == 0 && aligned16(g.C) && aligned16(g.bsrc);
 }
 
@@ -723,7 +752,7 @@ void launch_b16(hipStream_t s, const GemmArgs& g0) {
 }  // namespace bgnn
 
 extern "C" int bgnn_gemm_b16_variant(int32_t variant) {
-    BGNN_REQUIRE(variant >= -1 && variant <= 13, "gemm_b16_variant: must be -1 (off) or 0..13");
+    BGNN_REQUIRE(variant >= -1 && variant <= 14, "gemm_b16_variant: must be -1 (off) or 0..14");
     bgnn::g_b16_variant = variant;
     return BGNN_OK;
 }

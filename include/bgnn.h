@@ -334,8 +334,9 @@ int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm, int64_t n_
  *   0/1/3/4/5/7 (B bf16 = the weight rounded once by the caller; ABI 6 takes B as const void*).
  * bgnn_gemm_b16_variant (ABI 6, measurement): -1 = the bf16-stored NT products on the
  *   register-staged kernel instead; 0 = default (variant 11: one 256x256 tile per workgroup,
- *   whole-line bf16 C stores, a gathered epilogue's row indices staged in LDS); 1-13 = fixed
- *   forms (A/B; 13 = variant 11 reading the gather indices from global memory per row).
+ *   whole-line bf16 C stores, a gathered epilogue's row indices staged in LDS); 1-14 = fixed
+ *   forms (A/B; 13 = variant 11 reading the gather indices from global memory per row, 14 =
+ *   variant 11 loading each 32-row block's first gathered rows before its staging).
  * bgnn_add_dropout_bf16: bgnn_add_dropout over bf16 (same mask; f32 sum, one rounding).
  * bgnn_segment_sum_bf16: out[r] = sum (mean: / max(deg, 1)) of the bf16 rows x[col[p]], p in
  *   [rowptr[r], rowptr[r+1]), in CSR order, f32 result (H % 8 == 0, H <= 512). */

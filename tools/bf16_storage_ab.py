@@ -110,6 +110,7 @@ cases = {
     "gather st7 b16 v11": v(11, lambda: gather7()),
     "gather st7 b16 v12": v(12, lambda: gather7()),
     "gather st7 b16 v13 (v11, idx global)": v(13, lambda: gather7()),
+    "gather st7 b16 v14 (v11, rows prefetched)": v(14, lambda: gather7()),
     "dropadd b16 (fused)": lambda: dropadd(True),
     "dropadd two-step": lambda: dropadd(False),
     "TN st0 (f32 g, f32 e)": lambda: fused.gemm_bf16(g32, x32, True, False),
@@ -125,7 +126,8 @@ print(f"{'NT st3 b16 v0':28s} bit-identical to x6: {torch.equal(cases['NT st3 b1
 print(f"{'NT st3 b16 v6':28s} bit-identical to x6: {torch.equal(cases['NT st3 b16 v6'](), ref3)}", flush=True)
 refg = cases["gather st7 x6"]()
 for k in ("gather st7 b16 v0", "gather st7 b16 v2", "gather st7 b16 v6", "gather st7 b16 v8", "gather st7 b16 v9",
-          "gather st7 b16 v10", "gather st7 b16 v11", "gather st7 b16 v12", "gather st7 b16 v13 (v11, idx global)"):
+          "gather st7 b16 v10", "gather st7 b16 v11", "gather st7 b16 v12", "gather st7 b16 v13 (v11, idx global)",
+          "gather st7 b16 v14 (v11, rows prefetched)"):
     print(f"{k:28s} bit-identical to x6: {torch.equal(cases[k](), refg)}", flush=True)
 print(f"{'dropadd fused':28s} bit-identical to two-step: {torch.equal(cases['dropadd b16 (fused)'](), cases['dropadd two-step']())}",
       flush=True)
