@@ -183,10 +183,21 @@ def load():
         return lib
 
 
+def _checked(lib, name: str, args):
+    """The entry point, after checking the argument count against its SIGNATURES entry (ctypes
+    passes surplus arguments on as C varargs, which shifts nothing it can see but everything the
+    callee reads: a stale caller would hand the kernels wrong pointers)."""
+    fn = getattr(lib, name)
+    sig = SIGNATURES.get(name)
+    if sig is not None and len(args) != len(sig[1]):
+        raise TypeError(f"bgnn: {name} takes {len(sig[1])} arguments, {len(args)} given")
+    return fn
+
+
 def call(name: str, *args):
     """Call a status-returning entry point and raise BgnnError on failure."""
     lib = load()
-    rc = getattr(lib, name)(*args)
+    rc = _checked(lib, name, args)(*args)
     if rc != 0:
         msg = lib.bgnn_last_error_string().decode(errors="replace")
         raise BgnnError(name, rc, msg)
@@ -195,4 +206,5 @@ def call(name: str, *args):
 
 def query(name: str, *args):
     """Call a value-returning entry point (sizes, slot counts)."""
-    return getattr(load(), name)(*args)
+    lib = load()
+    return _checked(lib, name, args)(*args)

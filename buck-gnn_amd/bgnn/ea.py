@@ -343,11 +343,13 @@ _IDENTITY = {}
 
 
 def _identity_index(n: int, device) -> torch.Tensor:
-    key = (n, str(device))
+    """arange(n) as a view of one per-device arange sized to the largest n seen (batches have varying
+    node counts: a cache keyed by n would grow without bound)."""
+    key = str(device)
     t = _IDENTITY.get(key)
-    if t is None:
-        t = _IDENTITY[key] = torch.arange(n, dtype=torch.int64, device=device)
-    return t
+    if t is None or t.numel() < n:
+        t = _IDENTITY[key] = torch.arange(max(n, 1), dtype=torch.int64, device=device)
+    return t[:n]
 
 
 class _LinearResidual(torch.autograd.Function):

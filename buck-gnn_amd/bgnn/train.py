@@ -115,12 +115,16 @@ class GradAllReduce:
     no gradient (the reference's unused modules) are never part of a bucket."""
 
     def __init__(self, model: nn.Module, group: Optional[dist.ProcessGroup] = None, bucket_mb: float = 4.0,
-                 overlap: bool = True):
+                 overlap: bool = True, _force_collectives: bool = False):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.bucket_bytes = int(bucket_mb * (1 << 20))
-        self.overlap = overlap and self.world > 1
+        # test-only: issue the collectives (hook-launched buckets included) even at world size 1,
+        # so a one-GPU box runs the RCCL path for real (tests/test_gpu_rccl.py); at world 1 the
+        # sum and the 1/world scale are exact, the gradients come back unchanged
+        self._force = bool(_force_collectives) and dist.is_initialized()
+        self.overlap = overlap and (self.world > 1 or self._force)
         self._flat = None
         self._seen = []            # gradient arrival order of the recording step
         self._buckets = None       # [(params, flat buffer, views)]
@@ -228,7 +232,7 @@ class GradAllReduce:
 
     # ---------------------------------------------------------------- per step
     def __call__(self) -> None:
-        if self.world <= 1:
+        if self.world <= 1 and not self._force:
             return
         if self.overlap and self._buckets is not None:
             self._launch_rest()

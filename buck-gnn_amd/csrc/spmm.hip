@@ -1255,6 +1255,13 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
     A.x = x; A.ldx = ldx;
     A.out = out; A.ldo = ldo;
     if (arg) {
+        // the compact state stores a light row's argmax as a byte offset into its edge list
+        // (deg <= chunk) and marks heavy rows with 255: a chunk of 255 or more would let a light
+        // row's offset wrap or collide with the marker (bgnn_spmm_bwd_max would then read a
+        // heavy-row slot that was never written)
+        BGNN_REQUIRE(csr->chunk > 0 && csr->chunk < 255,
+                     "spmm_fwd(max, arg): the CSR's chunk must be in [1, 254] for the compact argmax (got %d)",
+                     csr->chunk);
         const MaxArgLayout L = max_arg_layout(csr->n_rows, H);
         A.arg8 = static_cast<uint8_t*>(arg);
         A.heavy_of = reinterpret_cast<int32_t*>(static_cast<char*>(arg) + L.heavy_of);

@@ -189,8 +189,7 @@ int bgnn_group_plan(const int32_t* rowptr, const int32_t* col, int64_t n_rows, i
  *   out[r, :] = REDUCE_{e in row r} x[col[e], :]
  * H columns, row strides ldx / ldo in elements. For MEAN the sum is divided by
  * max(deg, 1); empty rows give 0 for every reduce (PyG semantics).
- * MAX writes the CSR position of the winning entry to arg[r, c] (first maximum
- * in CSR order; -1 for empty rows) when arg != NULL.
+ * MAX writes the argmax state (below) when arg != NULL.
  * `partial` is scratch of n_chunks * H floats (+ n_chunks * H int32 for MAX).
  * ---------------------------------------------------------------------- */
 int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H,
@@ -199,9 +198,11 @@ int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx, int32_t H,
 /* MAX: `arg` (optional; needed for the backward) receives the argmax state, a device buffer of
  * bgnn_spmm_max_arg_bytes(n_rows, H, n_heavy) bytes (round 5, ABI 10; was an int32 [rows, H]
  * array of CSR positions): per (row, column) the argmax edge's offset in the row's edge list as
- * one byte for light rows (deg <= chunk <= 64), and for heavy rows (super nodes) a marker byte
+ * one byte for light rows (deg <= chunk), and for heavy rows (super nodes) a marker byte (255)
  * plus the int32 offset in a per-heavy-row array -- 1 B instead of 4 B per element written by the
- * forward and gathered per edge by the backward. Ties: the first maximising edge in CSR order. */
+ * forward and gathered per edge by the backward. Ties: the first maximising edge in CSR order.
+ * Requires csr->chunk in [1, 254] when arg != NULL (BGNN_E_ARG otherwise: a larger chunk would
+ * let a light row's offset reach the marker); the library's plans use chunk 64. */
 size_t bgnn_spmm_max_arg_bytes(int64_t n_rows, int32_t H, int32_t n_heavy);
 
 /* Backward of bgnn_spmm_fwd through the transpose CSR (rows = sources):
@@ -597,8 +598,10 @@ int bgnn_add_dropout(const float* a, const float* b, int64_t n, float p, uint64_
  * modules the reference builds after each SAGEConv, Models/BuckGNN.py:133,148,163,179; used by
  * bgnn.nn.BatchNorm1d on the per-module path). C % 4 == 0 with C / 4 a power of two <= 256;
  * 16-byte aligned pointers.
- *   bgnn_bn_stats:     per-block partials [bgnn_bn_slots(n_rows, C), 2, C] of sum x, sum x^2
- *                      (finished by bgnn_bn_finalize)
+ *   bgnn_bn_stats:     per-block partials [bgnn_bn_slots(n_rows, C), 2, C] of the SHIFTED sums
+ *                      sum (x - k), sum (x - k)^2 with k = x's first row (round 5), finished by
+ *                      bgnn_bn_finalize_shifted with kshift = x (NOT bgnn_bn_finalize, which
+ *                      takes unshifted sums: it would return a mean off by the first row)
  *   bgnn_bn_apply:     y = x * scale + shift
  *   bgnn_bn_bwd_stats: partials of sum g, sum g * (x - mean) * invstd (finished by
  *                      bgnn_reduce_partials into sums[2, C] = dbeta, dgamma)

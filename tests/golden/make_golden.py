@@ -67,6 +67,11 @@ CASES = [
      False),
     ("mean_h512_n1k", "GraphSage_meanAggr", 512, "mean", [(23, False, 33), (23, True, 34)], False),
     ("sag_h512_n1k", "GraphSAGE_SAG", 512, "mean", [(23, False, 35), (23, False, 36)], False),
+    # round 6: BASELINE configs[0] itself -- one 45x45 mesh (2,025 nodes, virtual edges), batch=None
+    # (INFERENCE.py:261 at BATCH_SIZE = 1; global_mean_pool with batch=None, Models/BuckGNN.py:273-274),
+    # h = 512, the add loop and TRAIN_FINAL.py's default Shared loop
+    ("add_cfg1_h512", "GraphSage_addAggr", 512, "mean", [(45, False, 50)], False),
+    ("shared_cfg1_h512", "GraphSage_addAggr_Shared", 512, "mean", [(45, False, 51)], False),
 ]
 
 

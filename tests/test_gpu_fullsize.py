@@ -19,7 +19,14 @@ captures every layer's GPU argmax and its layer input, checks that each place wh
 choice differs from fp64's first argmax is a near tie -- fp64 margin max - x_choice at most twice
 the layer input's largest f32 error (measured, max |x_gpu - x_fp64|) -- and then evaluates the
 fp64 backward along the GPU's choices, so the whole-tensor gradient bounds are the same as for
-the linear aggregations. The flip counts are printed."""
+the linear aggregations. The flip counts are printed.
+
+Every layer's normalised SAGEConv output (the north star's "match the reference CPU SAGEConv outputs
+on identical edge_index/x within 1e-4 fp32", Models/BuckGNN.py:434) is checked twice at full size:
+(1) literally -- the fp64 oracle's SAGEConv (oracle/pyg_ref.py) evaluated on the GPU layer's own
+input x (for the folded first layer, x = h W_in^T + b_in from the GPU's encoder hidden h, in fp64)
+against the GPU's output, max |diff| <= 1e-4; (2) along the whole chain -- the fp64 oracle's
+layer-i output against the GPU's, max |diff| <= 1e-4 (every earlier layer's rounding included)."""
 import numpy as np
 import pytest
 import torch
@@ -88,6 +95,13 @@ def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg, model_n
     real_layer = buckgnn.sage_layer
     monkeypatch.setattr(buckgnn, "sage_layer", lambda *a, **k: folds.append(k.get("w_in") is not None)
                         or real_layer(*a, **k))
+    layer_io = []   # per layer: (SAGEConv input as the GPU layer received it, normalised output o)
+    real_glue = fused._glue_fwd
+
+    def glue_spy(o, bn_part, slots, x_prev, *a, **k):
+        layer_io.append((x_prev.detach().cpu(), o.detach().cpu()))
+        return real_glue(o, bn_part, slots, x_prev, *a, **k)
+    monkeypatch.setattr(fused, "_glue_fwd", glue_spy)
     captured = []   # max: per layer (input x [N, C] f32, argmax [N, C] as forward-CSR positions)
     if is_max:
         real_mt = fused._max_transform
@@ -116,6 +130,27 @@ def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg, model_n
 
     # fp64 oracle on the host (~25-60 s with 8-16 threads)
     torch.set_num_threads(min(16, torch.get_num_threads()))
+    assert len(layer_io) == 6
+    attr, aggr, _ = R.SAGE[model_name]
+    sd64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
+    gpu_o = [o for _, o in layer_io]
+    worst_in = []
+    for i, (x_in, o) in enumerate(layer_io):   # (1) identical input x, fp64 SAGEConv, literal 1e-4
+        pre = attr if model_name.endswith("_Shared") else f"{attr}.{i}"
+        x_in = x_in.double()
+        if i == 0 and folds and folds[0]:   # the folded layer received the encoder hidden h
+            last = max(int(k.split(".")[1]) for k in sd64 if k.startswith("node_encoder."))
+            x_in = torch.nn.functional.linear(x_in, sd64[f"node_encoder.{last}.weight"],
+                                              sd64[f"node_encoder.{last}.bias"])
+        ref_o = R.sage_conv(sd64, pre, x_in, b.edge_index, aggr)
+        d = float((o.double() - ref_o).abs().max())
+        worst_in.append(d)
+        assert d <= 1e-4, ("SAGEConv output vs fp64 on the identical input", i, d)
+    del layer_io
+    print("per-layer SAGEConv max |GPU - fp64| on the identical input:", [f"{d:.2e}" for d in worst_in])
+    chain_o = []
+    real_conv = R.sage_conv
+    monkeypatch.setattr(R, "sage_conv", lambda *a, **k: chain_o.append(real_conv(*a, **k)) or chain_o[-1])
     flips = []
     if is_max:
         # forward-CSR position -> edge id (the CSR is a stable sort of edge_index by target)
@@ -146,6 +181,11 @@ def test_full_size_train_step_matches_fp64_oracle(dev, monkeypatch, cfg, model_n
         assert len(flips) == 6
         print("argmax flips per layer (count, largest fp64 margin, allowance):", flips)
 
+    assert len(chain_o) == 6
+    worst_chain = [float((o.double() - c.detach()).abs().max()) for o, c in zip(gpu_o, chain_o)]
+    print("per-layer SAGEConv max |GPU - fp64| along the chain:", [f"{d:.2e}" for d in worst_chain])
+    assert max(worst_chain) <= 1e-4, worst_chain
+    del gpu_o, chain_o
     np.testing.assert_allclose(pred_g.numpy(), pred_o.detach().numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(loss_g, float(loss_o), rtol=1e-4, atol=1e-4)
     ref = {k: v.grad.numpy() for k, v in st.items() if v.grad is not None}

@@ -178,3 +178,24 @@ def test_max_group_kernel_matches_sweep(dev, case):
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][2], outs[1][2])
     assert torch.equal(outs[0][1][:N * H], outs[1][1][:N * H])   # the per-element bytes (padding aside)
+
+
+def test_compact_argmax_rejects_chunk_beyond_byte_range(dev):
+    """The compact argmax state keeps a light row's argmax as a byte offset (heavy rows: marker 255),
+    so a CSR whose chunk lets a light row have >= 255 edges is rejected loudly instead of wrapping
+    the offsets: a 300-chunk CSR with a row of degree 280 fails, the same graph with the
+    default chunk (the row is then heavy) runs, and its forward max equals the fp64 oracle."""
+    from bgnn import ops
+    n = 300
+    src = torch.arange(1, 281, dtype=torch.long)
+    ei = torch.stack([src, torch.zeros_like(src)])            # row 0: in-degree 280
+    ei = torch.cat([ei, torch.stack([torch.arange(n - 1), torch.arange(1, n)])], 1)
+    x = torch.randn(n, 64)
+    g_big = Graph.build(ei.to(dev), n, chunk=300)
+    from bgnn._lib import BgnnError
+    with pytest.raises(BgnnError, match="chunk"):
+        ops.spmm_fwd(g_big.fwd, x.to(dev), 2, n, want_arg=True)
+    g = Graph.build(ei.to(dev), n)
+    agg, arg = ops.spmm_fwd(g.fwd, x.to(dev), 2, n, want_arg=True)
+    ref = P.sage_aggregate(x.double(), ei, "max")
+    torch.testing.assert_close(agg.cpu().double(), ref, rtol=0, atol=0)

@@ -103,7 +103,7 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         _lib.call("bgnn_spmm_bwd", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), z[:, H:].data_ptr(),
-                  z.stride(0), H, 0, None, gx.data_ptr(), gx.stride(0), part.data_ptr(), None, s)
+                  z.stride(0), H, 0, gx.data_ptr(), gx.stride(0), part.data_ptr(), None, s)
         e1.record()
         return (e0, e1), (gx[:, :H],)
 
