@@ -11,8 +11,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 11
+# BGNN_LIBRARY: a measurement build of the same ABI (make -C buck-gnn_amd m16), for tools/ only
+LIB_PATH = os.environ.get("BGNN_LIBRARY") or os.path.join(_HERE, "_lib", "libbgnn.so")
+ABI_VERSION = 12
 
 _lock = threading.Lock()
 _lib = None

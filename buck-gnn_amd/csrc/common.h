@@ -87,8 +87,6 @@ void set_rows_nt(int on);
 int rows_nt();
 void set_rows_rev(int on);
 int rows_rev();
-void set_gemm_pp(int v);
-int gemm_pp();
 
 // 16-byte store, non-temporal (streamed once: no write-allocate in L2 / Infinity Cache)
 __device__ __forceinline__ void store4(float* p, float a, float b, float c, float d, bool nt) {

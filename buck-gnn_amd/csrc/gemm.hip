@@ -92,7 +92,7 @@ __device__ __forceinline__ void store_slice(float* __restrict__ S, const float (
 // = TM x TN MFMA tiles of 32x32.
 // TA: 0 -> A is [M,K] (K-contiguous), 1 -> A is [K,M].
 // TB: 0 -> B is [K,N] (N-contiguous), 1 -> B is [N,K] (K-contiguous).
-template <int TA, int TB, int BM, int BN, int BK, int WM, int WN, int ABL = 0>
+template <int TA, int TB, int BM, int BN, int BK, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -148,42 +148,35 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_f32(GemmArgs g) {
         load_ab(kb);
         store_slice<AK, BM, BK, LDA_S, NT>(As[0], ra);
         store_slice<BKc, BN, BK, LDB_S, NT>(Bs[0], rb);
-        if (nk > 1 && ABL == 0) load_ab(kb + BK);
+        if (nk > 1) load_ab(kb + BK);
     }
     __syncthreads();
 
     const int li = lane & 31, lk = lane >> 5;
     for (int64_t kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk && ABL <= 1) {
+        if (kt + 1 < nk) {
             store_slice<AK, BM, BK, LDA_S, NT>(As[cur ^ 1], ra);
             store_slice<BKc, BN, BK, LDB_S, NT>(Bs[cur ^ 1], rb);
         }
-        if (kt + 2 < nk && ABL == 0) load_ab(kb + (kt + 2) * BK);
+        if (kt + 2 < nk) load_ab(kb + (kt + 2) * BK);
         const float* as = As[cur] + wm * (BM / WM) + li;
         const float* bs = Bs[cur] + wn * (BN / WN) + li;
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
             const int kr = 2 * kk + lk;
             float a[TM], b[TN];
-            if constexpr (ABL >= 3) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) a[i] = ra[0][i & 3] + (float)kk;
+            for (int i = 0; i < TM; ++i) a[i] = as[kr * LDA_S + i * 32];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) b[j] = rb[0][j & 3];
-            } else {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) a[i] = as[kr * LDA_S + i * 32];
-#pragma unroll
-                for (int j = 0; j < TN; ++j) b[j] = bs[kr * LDB_S + j * 32];
-            }
+            for (int j = 0; j < TN; ++j) b[j] = bs[kr * LDB_S + j * 32];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
-        if constexpr (ABL <= 1) __syncthreads();
+        __syncthreads();
     }
 
     // epilogue: C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -310,7 +303,6 @@ constexpr GemmCfg kCfgs[] = {
 };
 constexpr int kNumCfgs = 9;
 static int g_gemm_cfg = -1;   // -1 = automatic
-static int g_gemm_abl = 0;    // ablation (measurement only)
 static int g_gemm_mode = 2;   // 0 = f32 MFMA kernel (gemm.hip), 2 = f16x3 (gemm_x6.hip, default: error
                               // below the f32 MFMA's at 3 f16 MFMAs per product; tools/tune_gemm.py)
 
@@ -365,12 +357,7 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
         case 2: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 256, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
         case 3: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 16, 4, 2>), grid, dim3(512), 0, s, g); break;
         case 4: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 16, 2, 2>), grid, dim3(256), 0, s, g); break;
-        case 5:
-            if (g_gemm_abl == 1) hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4, 1>), grid, dim3(512), 0, s, g);
-            else if (g_gemm_abl == 2) hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4, 2>), grid, dim3(512), 0, s, g);
-            else if (g_gemm_abl == 3) hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4, 3>), grid, dim3(512), 0, s, g);
-            else hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4>), grid, dim3(512), 0, s, g);
-            break;
+        case 5: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 16, 2, 4>), grid, dim3(512), 0, s, g); break;
         case 6: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 128, 256, 32, 2, 4>), grid, dim3(512), 0, s, g); break;
         case 7: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 256, 32, 2, 4>), grid, dim3(512), 0, s, g); break;
         case 8: hipLaunchKernelGGL((k_gemm_f32<TA, TB, 256, 128, 32, 4, 2>), grid, dim3(512), 0, s, g); break;
@@ -383,10 +370,10 @@ void launch_cfg(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
 using namespace bgnn;
 
 extern "C" int bgnn_gemm_set_cfg(int32_t cfg) {
-    BGNN_REQUIRE(cfg >= -1 && cfg % 100 < (kNumCfgs > kNumX6Cfgs ? kNumCfgs : kNumX6Cfgs) && cfg < 1200,
-                 "gemm: config %d out of range", cfg);
-    g_gemm_abl = cfg / 100;
-    g_gemm_cfg = cfg % 100;
+    // (-1 = automatic; the f16x3 / bf16 families have kNumX6Cfgs tiles, the f32 MFMA family kCfgs)
+    const int n = g_gemm_mode == 0 ? kNumCfgs : kNumX6Cfgs;
+    BGNN_REQUIRE(cfg >= -1 && cfg < n, "gemm: config %d out of range [-1, %d)", cfg, n);
+    g_gemm_cfg = cfg;
     return BGNN_OK;
 }
 
@@ -409,7 +396,6 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.x6 = 1;
         p.prec = 2;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, 1);
-        if (p.cfg == kX6CfgWB) p.cfg = 4;
         // plane blocks must be whole tiles (every bf16 tile gives the same bits: 16x16x32 MFMAs
         // in increasing k), else the 128x128 tile
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
@@ -421,7 +407,6 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.x6 = 1;
         p.prec = 1;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
-        if (p.cfg == kX6CfgWB && !wb) p.cfg = 4;   // (the 320-row tile exists for pre-split B only)
         // plane blocks must be whole tiles: fall back to an 8-wave tile that divides them (the
         // 16x16x32 MFMA family, the same rounding as the dense layout's), else the 128x128 tile
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) {
@@ -570,7 +555,7 @@ extern "C" int bgnn_gemm_f32_dropadd_cols(int64_t M, int64_t N, int64_t K, const
 extern "C" int32_t bgnn_gemm_w_tile(int64_t M, int64_t N, int64_t K) {
     if (gemm_mode() != 2 || M <= 0 || N <= 0 || K <= 0) return 0;
     const Plan pl = make_plan(M, N, K, 0, 1, 0, 0, 0, true);
-    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg < 1 || pl.cfg > kX6CfgWB) return 0;
+    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg < 1 || pl.cfg > 4) return 0;
     if (N % pl.bn != 0 || K % 32 != 0) return 0;
     return pl.bn;
 }
@@ -697,7 +682,7 @@ static int gemm_scaled_impl(int32_t ta, int32_t tb, int64_t M, int64_t N, int64_
     g.kchunk = kc > 0 ? kc : pl.bk;
     const int64_t tiles_a = ((Ma + pl.bm - 1) / pl.bm) * ((N + pl.bn - 1) / pl.bn);
     dim3 grid((unsigned)tiles_a, split);
-    if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, bs.src ? 8 : g_gemm_abl, grid, s, g);
+    if (pl.x6) launch_x6(pl.prec, ta, tb, pl.cfg, bs.src ? 8 : 0, grid, s, g);
     else if (ta == 0 && tb == 0) launch_cfg<0, 0>(pl.cfg, grid, s, g);
     else if (ta == 0 && tb == 1) launch_cfg<0, 1>(pl.cfg, grid, s, g);
     else if (ta == 1 && tb == 0) launch_cfg<1, 0>(pl.cfg, grid, s, g);

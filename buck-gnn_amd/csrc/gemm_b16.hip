@@ -152,14 +152,6 @@ __device__ __forceinline__ void b16_stage_block(float* __restrict__ stage, int l
             for (int r = 0; r < 4; ++r)
                 stage[(row0 + si * 16 + 4 * lq + r) * ld + coff + sj * 16 + l16] = acc[2 * i + si][2 * j + sj][r];
 }
-template <int TM, int TN>
-__device__ __forceinline__ float b16_acc_probe(const floatx16 (&acc)[TM][TN], int i, int j) {
-    return acc[i][j][0] + acc[i][j][15];
-}
-template <int TM2, int TN2>
-__device__ __forceinline__ float b16_acc_probe(const floatx4 (&acc)[TM2][TN2], int i, int j) {
-    return acc[2 * i][2 * j][0] + acc[2 * i + 1][2 * j + 1][3];
-}
 
 // Epilogue (alpha 1, beta 0, no split-K): per 32-column block, the wave's TM x 32 x 32
 // accumulators go through its LDS stage (x6_epilogue's C/D map and stage layout) and leave as
@@ -167,7 +159,7 @@ __device__ __forceinline__ float b16_acc_probe(const floatx4 (&acc)[TM2][TN2], i
 // C: 8 columns per lane (4 lanes per 64-B row segment; x6_epilogue stores 8 B). Per element the
 // arithmetic and its order are x6_epilogue's: acc, + bias, + ga0[gi0[row]], + ga1[gi1[row]],
 // ReLU, one bf16 rounding (RNE). Edge blocks fall back to x6_epilogue's element-guarded path.
-template <int TM, int TN, bool C16, bool WIDE = false, bool GPRE = false, typename Acc>
+template <int TM, int TN, bool C16, bool WIDE = false, typename Acc>
 __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
                                              int64_t c0, int lane, float* __restrict__ stage,
                                              const int64_t* __restrict__ li0 = nullptr,
@@ -205,20 +197,9 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
             for (int i = 0; i < TM; ++i) {
                 // drop-add source rows of this 32-row block issued before the staging, so their
                 // latency runs under the LDS writes and waits
+                // (the gathered ga0 rows loaded the same way ran slower: 2776 -> 3003 us at E = 2.86M,
+                // their 32 VGPRs beside the 128 accumulator registers; round 5, measured, removed)
                 uint4 spre[4];
-                float4 gpre[4][2];   // the block's ga0 rows: [q][k0..3, k4..7] (ga1 stays in the loop)
-                if (GPRE && g.ga0) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int rr = q * 8 + rq8;
-                        const int64_t row = r0 + i * 32 + rr;
-                        if (row < g.M) {
-                            const float* s0 = g.ga0 + (li0 ? li0[i * 32 + rr] : g.gi0[row]) * g.ldg0 + col;
-                            gpre[q][0] = *reinterpret_cast<const float4*>(s0);
-                            gpre[q][1] = *reinterpret_cast<const float4*>(s0 + 4);
-                        }
-                    }
-                }
                 if (g.st & 8) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -242,20 +223,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
                         const float4 sv = *reinterpret_cast<const float4*>(stage + rr * LDW + cq8 + k);
                         e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
                     }
-                    if (GPRE && g.ga0) {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            x0[k] = gpre[q][0][k]; x0[k + 4] = gpre[q][1][k];
-                        }
-                        if (g.ga1) {
-                            const float* s1 = g.ga1 + (li1 ? li1[i * 32 + rr] : g.gi1[row]) * g.ldg1 + col;
-#pragma unroll
-                            for (int k = 0; k < 8; k += 4) {
-                                const float4 t = *reinterpret_cast<const float4*>(s1 + k);
-                                x1[k] = t.x; x1[k + 1] = t.y; x1[k + 2] = t.z; x1[k + 3] = t.w;
-                            }
-                        }
-                    } else if (g.ga0) {
+                    if (g.ga0) {
                         // the gather rows' indices from the tile's LDS copy when the kernel made one
                         const float* s0 = g.ga0 + (li0 ? li0[i * 32 + rr] : g.gi0[row]) * g.ldg0 + col;
 #pragma unroll
@@ -382,9 +350,7 @@ __device__ __forceinline__ void b16_epilogue(const GemmArgs& g, const Acc& acc, 
     }
 }
 
-// ABL: 0 = the kernel; 1 = timing ablation without the epilogue (one value per wave stored)
-template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, int ABL = 0, bool WIDE = false,
-          bool GPRE = false>
+template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16, int MINB = 1, bool WIDE = false>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     using L = B16Slice<BK>;
     constexpr int NW = WM * WN;
@@ -433,7 +399,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
         dst[q] = ((isa ? 0 : BM) + r0) * L::CPR;
     }
     // the index copies go first: the slice waits' in-order vmcnt covers them
-    const bool lidx = kIdx && g.ga0 != nullptr && g.gidx_lds;
+    const bool lidx = kIdx && g.ga0 != nullptr;
     if (lidx) {
         int64_t row = m0 + wave * 32 + (lane >> 1);
         if (row > g.M - 1) row = g.M - 1;
@@ -469,205 +435,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
         issue(m + NS - 1);
         b16_mma<BM, BN, BK, WM, WN>(smem + (int)(m % NS) * SLICE_U4, acc, wm, wn, lane);
     }
-    if constexpr (ABL == 1) {
-        float t0 = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) t0 += b16_acc_probe(acc, i, j);
-        if (lane == 0) reinterpret_cast<float*>(g.C)[wave] = t0;
-        return;
-    }
     __syncthreads();   // every wave's fragment reads done before the epilogue reuses the LDS
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
     const int64_t* li = reinterpret_cast<const int64_t*>(smem + SMEM_U4) + wm * (BM / WM);
-    b16_epilogue<TM, TN, C16, WIDE, GPRE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage,
+    b16_epilogue<TM, TN, C16, WIDE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage,
                                     lidx ? li : nullptr, lidx && g.ga1 ? li + BM : nullptr);
 }
 
-// Epilogue of one wave's TM x TN blocks for the persistent kernel: each 32x32 block through a
-// wave-private 4 KiB LDS stage (separate from the operand slots, so the next tile's slices can be
-// in flight meanwhile), out as 16-B non-temporal row stores (f32: 4 columns per lane, bf16: 8);
-// x6_epilogue's per-element arithmetic and order; edge blocks store element-wise within bounds.
-template <int TM, int TN, bool C16, typename Acc>
-__device__ __forceinline__ void b16p_epilogue(const GemmArgs& g, const Acc& acc, int64_t r0,
-                                              int64_t c0, int lane, float* __restrict__ stage) {
-    constexpr int CPL = C16 ? 8 : 4;
-    constexpr int LPR = 32 / CPL;
-    constexpr int RPP = 64 / LPR;
-
-    const int rq = lane / LPR, cq = (lane % LPR) * CPL;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int64_t col = c0 + j * 32 + cq;
-        const bool cfull = c0 + j * 32 + 32 <= g.N;
-        float bv[CPL];
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) bv[k] = (g.bias && (cfull || col + k < g.N)) ? g.bias[col + k] : 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            b16_stage_block(stage, 32, 0, 0, acc, i, j, lane);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const bool full = cfull && r0 + i * 32 + 32 <= g.M;
-#pragma unroll
-            for (int q = 0; q < 32 / RPP; ++q) {
-                const int rr = q * RPP + rq;
-                const int64_t row = r0 + i * 32 + rr;
-                float e[CPL];
-#pragma unroll
-                for (int k = 0; k < CPL; k += 4) {
-                    const float4 sv = *reinterpret_cast<const float4*>(stage + rr * 32 + cq + k);
-                    e[k] = sv.x; e[k + 1] = sv.y; e[k + 2] = sv.z; e[k + 3] = sv.w;
-                }
-                if (!full && row >= g.M) continue;
-                float x0[CPL], x1[CPL];
-                if (g.ga0) {
-                    const float* s0 = g.ga0 + g.gi0[row] * g.ldg0 + col;
-                    const float* s1 = g.ga1 ? g.ga1 + g.gi1[row] * g.ldg1 + col : nullptr;
-                    if (full) {
-#pragma unroll
-                        for (int k = 0; k < CPL; k += 4) {
-                            const float4 t = *reinterpret_cast<const float4*>(s0 + k);
-                            x0[k] = t.x; x0[k + 1] = t.y; x0[k + 2] = t.z; x0[k + 3] = t.w;
-                            const float4 u = s1 ? *reinterpret_cast<const float4*>(s1 + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-                            x1[k] = u.x; x1[k + 1] = u.y; x1[k + 2] = u.z; x1[k + 3] = u.w;
-                        }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < CPL; ++k) {
-                            x0[k] = col + k < g.N ? s0[k] : 0.f;
-                            x1[k] = (s1 && col + k < g.N) ? s1[k] : 0.f;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < CPL; ++k) {
-                    float v = e[k];
-                    if (g.bias) v += bv[k];
-                    if (g.ga0) v += x0[k];
-                    if (g.ga1) v += x1[k];
-                    if (g.relu) v = fmaxf(v, 0.f);
-                    e[k] = v;
-                }
-                if constexpr (C16) {
-                    uint16_t* p = reinterpret_cast<uint16_t*>(g.C) + row * g.ldc + col;
-                    if (full) {
-                        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-                        const u32x4_t w = {pack_bf16(e[0], e[1]), pack_bf16(e[2], e[3]), pack_bf16(e[4], e[5]),
-                                           pack_bf16(e[6], e[7])};
-                        __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < CPL; ++k)
-                            if (col + k < g.N) p[k] = (uint16_t)(pack_bf16(e[k], 0.f) & 0xffffu);
-                    }
-                } else {
-                    float* p = g.C + row * g.ldc + col;
-                    if (full) {
-                        st_nt4(p, e);
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < CPL; ++k)
-                            if (col + k < g.N) p[k] = e[k];
-                    }
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-    }
-}
-
-// Persistent form (variant 6): one workgroup per CU walks tiles first, first + grid, ... (XCD-aware:
-// at each step one XCD's 32 workgroups hold consecutive tiles, i.e. whole row blocks, so A's rows
-// are shared in its L2). The slice pipeline runs across tile boundaries: at a tile's last slice
-// the next tile's first slices are issued before the MFMAs and the epilogue, so their HBM latency
-// hides under this tile's epilogue instead of being exposed at every workgroup start, and the
-// workgroup never ends between tiles. (The epilogue's own loads -- bias, gathered rows -- wait
-// behind those slices in the in-order vmcnt, but both latencies run concurrently.)
-template <int BM, int BN, int BK, int NS, int WM, int WN, bool C16>
-__global__ __launch_bounds__(64 * WM * WN) void k_gemm_b16p(GemmArgs g) {
-    using L = B16Slice<BK>;
-    constexpr int NW = WM * WN;
-    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-    constexpr int GA = BM / (L::RPI * NW), GB = BN / (L::RPI * NW);
-    constexpr int G = GA + GB;
-    constexpr int SLICE_U4 = (BM + BN) * L::CPR;
-    constexpr int STAGE_U4 = NW * 32 * 32 / 4;   // one 32x32 f32 block per wave
-    static_assert(GA * L::RPI * NW == BM && GB * L::RPI * NW == BN, "rows must split evenly over the waves");
-    static_assert((NS - 2) * G < 64, "vmcnt range");
-    static_assert((NS * SLICE_U4 + STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
-    __shared__ uint4 smem[NS * SLICE_U4 + STAGE_U4];
-
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wave = t >> 6;
-    const int wm = wave / WN, wn = wave % WN;
-    const int64_t ntn = (g.N + BN - 1) / BN;
-    const int64_t ntiles = ((g.M + BM - 1) / BM) * ntn;
-    const int64_t first = xcd_remap(blockIdx.x, gridDim.x);
-    const int64_t stride = gridDim.x;
-    if (first >= ntiles) return;   // (workgroup-uniform: the whole workgroup leaves together)
-    const int64_t my_tiles = (ntiles - first + stride - 1) / stride;
-    const int64_t nm = g.K / BK;
-    const int64_t total = my_tiles * nm;
-
-    uint32_t off[G];
-    int dst[G];
-    const char* abase = nullptr;
-    const char* bbase = nullptr;
-    int64_t off_tile = -1;
-    auto set_tile = [&](int64_t k) {
-        const int64_t lt = first + k * stride;
-        const int64_t m0 = (lt / ntn) * BM, n0 = (lt % ntn) * BN;
-        abase = reinterpret_cast<const char*>(g.A) + m0 * g.lda * 2;
-        bbase = reinterpret_cast<const char*>(g.B) + n0 * g.ldb * 2;
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-            const bool isa = q < GA;
-            const int r0 = (isa ? wave * GA + q : wave * GB + (q - GA)) * L::RPI;
-            int r = r0 + lane / L::CPR;
-            const int c = (lane % L::CPR) ^ L::swz((isa ? 0 : BM) + r);
-            const int64_t rmax = (isa ? g.M - m0 : g.N - n0) - 1;
-            if (r > rmax) r = (int)rmax;
-            off[q] = (uint32_t)((r * (isa ? g.lda : g.ldb) + 8 * c) * 2);
-            dst[q] = ((isa ? 0 : BM) + r0) * L::CPR;
-        }
-        off_tile = k;
-    };
-    auto issue = [&](int64_t S) {
-        if (S >= total) return;
-        const int64_t k = S / nm;
-        if (k != off_tile) set_tile(k);
-        const uint32_t kb = (uint32_t)((S % nm) * BK * 2);
-        uint4* slot = smem + (int)(S % NS) * SLICE_U4;
-#pragma unroll
-        for (int q = 0; q < G; ++q)
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)((q < GA ? abase : bbase) + (off[q] + kb)),
-                                             (lds_void_t*)(slot + dst[q]), 16, 0, 0);
-    };
-
-    floatx4 acc[2 * TM][2 * TN];   // 16x16x32 MFMA tiles (b16_mma)
-    b16_acc_zero(acc);
-    float* stage = reinterpret_cast<float*>(smem + NS * SLICE_U4) + wave * (32 * 32);
-
-    for (int S = 0; S < NS - 1; ++S) issue(S);
-    for (int64_t S = 0; S < total; ++S) {
-        if (S + NS - 2 < total) b16_wait_vmcnt<(NS - 2) * G>();
-        else b16_wait_vmcnt<0>();
-        b16_barrier();
-        issue(S + NS - 1);
-        b16_mma<BM, BN, BK, WM, WN>(smem + (int)(S % NS) * SLICE_U4, acc, wm, wn, lane);
-        if (S % nm == nm - 1) {   // the tile's last slice: its epilogue, the next tile's slices in flight
-            const int64_t lt = first + (S / nm) * stride;
-            const int64_t m0 = (lt / ntn) * BM, n0 = (lt % ntn) * BN;
-            b16p_epilogue<TM, TN, C16>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage);
-            b16_acc_zero(acc);
-        }
-    }
-}
-
-int g_b16_variant = 0;
-constexpr int64_t kPersistentWgs = 256;   // MI355X CUs   // -1: bf16-stored NT products on k_gemm_x6 instead (A/B)
+int g_b16_variant = 0;   // 0 = the LDS-DMA kernel (default), -1 = bf16-stored NT products on k_gemm_x6 (A/B)
 
 }  // namespace
 
@@ -678,81 +453,28 @@ bool b16_ok(const GemmArgs& g, int ta, int tb) {
            aligned16(g.A) && aligned16(g.B) && 256 * g.lda * 2 < kMaxTileBytes && 256 * g.ldb * 2 < kMaxTileBytes;
 }
 
-// variant 0 (default) picks variant 11 (one tile per workgroup, whole-line bf16 C stores): at
-// E = 2,863,488 x 512 x 512 (cfg5, tools/bf16_storage_ab.py, same box, medians) bf16 C 1985 us
-// against 2145 (variant 7's half-line stores) and 2200 (persistent, variant 6); gathered bf16 C
-// 3620 against 3700 (variant 6). Round 2's pick at E = 715,872 was variant 6 for bf16 C and
-// gathers (gathered 1141 -> 1012 us, bf16 C 601 -> 574 us); for f32 C variants 7 and 11 are the
-// same kernel.
-static int b16_pick(const GemmArgs& g) {
-    if (g_b16_variant != 0) return g_b16_variant;
-    return 11;
-}
-
-static int b16_bm(int v) { return (v == 2 || v == 3 || v == 5 || v == 10) ? 128 : 256; }
-
-static int64_t b16_grid(int v, int64_t M, int64_t N) {
-    const int bm = b16_bm(v);
-    const int64_t tiles = ((M + bm - 1) / bm) * ((N + 255) / 256);
-    if (v == 6 || v == 8 || v == 9 || v == 10) return tiles < kPersistentWgs ? tiles : kPersistentWgs;   // persistent: one per CU
-    return tiles;
-}
-
-template <bool C16>
-static void launch_b16_t(int v, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    switch (v) {
-        case 1:   // 256x256, k32 slices (64-B row segments) x 4 slots
-            hipLaunchKernelGGL((k_gemm_b16<256, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 2:   // 128x256, k32 x 3 slots (72 KiB of LDS, <= 128 VGPRs: two workgroups per CU)
-            hipLaunchKernelGGL((k_gemm_b16<128, 256, 32, 3, 2, 4, C16, 4>), grid, dim3(512), 0, s, g); break;
-        case 3:   // 128x256, k64 x 2 slots (96 KiB: one workgroup per CU)
-            hipLaunchKernelGGL((k_gemm_b16<128, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 4:   // ablation: variant 0 without the epilogue
-            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 1>), grid, dim3(512), 0, s, g); break;
-        case 5:   // ablation: variant 2 without the epilogue
-            hipLaunchKernelGGL((k_gemm_b16<128, 256, 32, 3, 2, 4, C16, 4, 1>), grid, dim3(512), 0, s, g); break;
-        case 6:   // persistent 256x256, k64 x 2 slots (+ 32 KiB epilogue stage)
-            hipLaunchKernelGGL((k_gemm_b16p<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 8:   // persistent 256x256, k32 x 4 slots (prefetch distance 3; 128 + 32 KiB of LDS)
-            hipLaunchKernelGGL((k_gemm_b16p<256, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 9:   // persistent 256x256, k32 x 3 slots
-            hipLaunchKernelGGL((k_gemm_b16p<256, 256, 32, 3, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 10:  // persistent 128x256, k32 x 4 slots (96 + 32 KiB)
-            hipLaunchKernelGGL((k_gemm_b16p<128, 256, 32, 4, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-        case 13:  // variant 11 with the gather indices read from global memory per row (A/B)
-        case 11:  // variant 7 with whole-line bf16 C stores (b16_epilogue WIDE); gathered rows'
-                  // indices staged in LDS
-            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
-        case 14:  // variant 11 with each 32-row block's ga0 rows loaded before its staging
-            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16, 1, 0, true, true>), grid, dim3(512), 0, s, g); break;
-        case 12:  // variant 1 with whole-line bf16 C stores
-            hipLaunchKernelGGL((k_gemm_b16<256, 256, 32, 4, 2, 4, C16, 1, 0, true>), grid, dim3(512), 0, s, g); break;
-        default:  // 7: 256x256, k64 slices (whole 128-B row segments) x 2 slots
-            hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, C16>), grid, dim3(512), 0, s, g); break;
-    }
-}
-
-// the variant launch_b16 runs implements the drop-add (st bit 8) epilogue: the whole-line bf16 C
-// forms (WIDE)
+// One form: 256x256 tiles, one per workgroup, k64 slices (whole 128-B row segments) x 2 slots,
+// whole-line bf16 C stores, the gathered rows' indices staged in LDS. At E = 2,863,488 x 512 x 512
+// (cfg5, tools/bf16_storage_ab.py, same box, medians) bf16 C 1985 us against 2145 with half-line
+// stores and 2200 in the persistent form; gathered bf16 C 3620 against 3700 persistent. (ABI 12
+// removed the measured-and-rejected forms: persistent tiles, k32 slices with 3-4 slots, 128-row
+// tiles, per-row global gather indices, prefetched gather rows, the epilogue-free ablations;
+// records in profiles/r0[2-5]_*.)
 bool b16_dropadd_ok(const GemmArgs& g) {
-    const int v = b16_pick(g);
-    return (v == 11 || v == 12 || v == 13 || v == 14) && (g.st & 7) == 7 && g.N % 256 == 0 && g.ldc % 8 == 0 &&
-           g.ld_bsrc % 8 == 0 && aligned16(g.C) && aligned16(g.bsrc);
+    return (g.st & 7) == 7 && g.N % 256 == 0 && g.ldc % 8 == 0 && g.ld_bsrc % 8 == 0 && aligned16(g.C) &&
+           aligned16(g.bsrc);
 }
 
-void launch_b16(hipStream_t s, const GemmArgs& g0) {
-    const int v = b16_pick(g0);
-    const dim3 grid((unsigned)b16_grid(v, g0.M, g0.N));
-    GemmArgs g = g0;
-    g.gidx_lds = v != 13;
-    if (g.st & 4) launch_b16_t<true>(v, grid, s, g);
-    else launch_b16_t<false>(v, grid, s, g);
+void launch_b16(hipStream_t s, const GemmArgs& g) {
+    const dim3 grid((unsigned)(((g.M + 255) / 256) * ((g.N + 255) / 256)));
+    if (g.st & 4) hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, true, 1, true>), grid, dim3(512), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_b16<256, 256, 64, 2, 2, 4, false, 1, true>), grid, dim3(512), 0, s, g);
 }
 
 }  // namespace bgnn
 
 extern "C" int bgnn_gemm_b16_variant(int32_t variant) {
-    BGNN_REQUIRE(variant >= -1 && variant <= 14, "gemm_b16_variant: must be -1 (off) or 0..14");
+    BGNN_REQUIRE(variant == -1 || variant == 0, "gemm_b16_variant: must be -1 (off) or 0 (the LDS-DMA kernel)");
     bgnn::g_b16_variant = variant;
     return BGNN_OK;
 }

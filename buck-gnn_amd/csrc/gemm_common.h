@@ -43,9 +43,6 @@ struct GemmArgs {
     // drop-add epilogue: only columns >= bsrc_c0 take the beta operand, column c reading bsrc column
     // c - bsrc_c0 (a multiple of the tile width; the max layer's merged dgrad [dh W_l | dh W_r])
     int64_t bsrc_c0;
-    // LDS-DMA bf16 kernel (gemm_b16.hip), whole-line bf16 C with gathered rows: the tile's gi0 / gi1
-    // staged in LDS before the epilogue (1) or read from global memory per row (0, A/B variant 13)
-    int gidx_lds;
 };
 
 // the beta operand of 4 consecutive columns (col % 4 == 0) of row `row`: masked bsrc
@@ -82,18 +79,17 @@ __device__ __forceinline__ const float* plane_base(const float* P, int64_t x0, i
 }
 
 // GEMMs on 16-bit MFMAs (gemm_x6.hip): prec 1 = f16x3 (f32-accurate), 2 = bf16 operands; launches the
-// main kernel of tile config `cfg` (index into kX6Cfgs) on grid (tiles, split); abl != 0
-// selects a timing ablation.
+// main kernel of tile config `cfg` (index into kX6Cfgs) on grid (tiles, split); abl = 8: the
+// drop-add epilogue (bgnn_gemm_f32_dropadd), else 0.
 struct X6Cfg {
     int bm, bn, waves, blocks_per_cu;
 };
 extern const X6Cfg kX6Cfgs[];
 extern const int kNumX6Cfgs;
-constexpr int kX6CfgWB = 5;   // the 320 x 256 tile, built for pre-split B (bgnn_gemm_f32_w) only
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
 // bf16-operand GEMM on bf16-STORED A and B (gemm_b16.hip): b16_ok = the call qualifies (ta 0,
 // tb 1, storage bits 0 and 1, K % 64 == 0, dense 16-B aligned rows, no split-K / drop-add);
-// launch_b16 covers all M rows (no tail split; tile / persistent form picked per call)
+// launch_b16 covers all M rows (one 256x256 tile per workgroup)
 bool b16_ok(const GemmArgs& g, int ta, int tb);
 void launch_b16(hipStream_t s, const GemmArgs& g);
 // the launch would run the drop-add epilogue (st bit 8: bsrc = bf16 [M, ld_bsrc] through the dropout

@@ -184,11 +184,8 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const Acc& acc, i
                     e[k] = v;
                     cmax = max(cmax, __float_as_uint(v) & 0x7fffffffu);
                 }
-                if (ABL == 5 && e[0] != 1234.5f) continue;   // ablation: no C stores
                 if constexpr (C16) {
                     st_bf16x4(c16_at(r0 + q * 8 + rq, col), e);
-                } else if constexpr (ABL == 6) {   // ablation: cached (write-allocate) C stores
-                    *reinterpret_cast<float4*>(p) = make_float4(e[0], e[1], e[2], e[3]);
                 } else {
                     st_nt4(p, e);
                 }
@@ -203,7 +200,6 @@ __device__ __forceinline__ void x6_epilogue(const GemmArgs& g, const Acc& acc, i
             const float4 sv = *reinterpret_cast<const float4*>(stage + rr * 32 + c4);
             const int64_t row = r0 + rr;
             float e[4] = {(sv.x * ia) * ib, (sv.y * ia) * ib, (sv.z * ia) * ib, (sv.w * ia) * ib};
-            if (ABL == 5 && e[0] != 1234.5f) continue;   // ablation: no C stores
             if (row >= g.M || col >= g.N) continue;
             float* p = dst + row * ldd + col;
             const bool full = vec && col + 3 < g.N;

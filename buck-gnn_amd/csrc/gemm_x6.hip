@@ -25,8 +25,8 @@
 //
 // This file: the tile table, the per-family dispatch and the operand-max kernels; the kernel
 // template lives in gemm_x6_kernel.h, instantiated by gemm_x6_nt.hip (forward / dgrad shapes),
-// gemm_x6_nt_abl.hip (their timing ablations), gemm_x6_other.hip (weight gradient and the other
-// transposes) and gemm_x6_b16s.hip (bf16 operands and storage).
+// gemm_x6_other.hip (weight gradient and the other transposes) and gemm_x6_b16s.hip (bf16
+// operands and storage).
 #include "gemm_x6_kernel.h"
 
 namespace bgnn {
@@ -38,21 +38,14 @@ const X6Cfg kX6Cfgs[] = {
     {128, 256, 8, 1},   // 2: 2x4 waves of 64x64
     {256, 256, 8, 1},   // 3: 2x4 waves of 128x64
     {256, 256, 8, 1},   // 4: 4x2 waves of 64x128
-    {320, 256, 8, 1},   // 5: 2x4 waves of 160x64, pre-split B only (bgnn_gemm_f32_w): 80,656 rows
-                        //    are 253 row tiles, i.e. 2 x 253 = 506 tiles = 1.98 rounds of 256 CUs
 };
-const int kNumX6Cfgs = 6;
-
-int g_gemm_pp = 0;   // ping-pong main loop for the f16x3 K-contiguous shapes (BGNN_TUNE_GEMM_PP)
-void set_gemm_pp(int v) { g_gemm_pp = v; }
-int gemm_pp() { return g_gemm_pp; }
+const int kNumX6Cfgs = 5;
 
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if (prec == 2 && g.st != 0) launch_x6_bf16_storage(ta, tb, cfg, g.st, grid, s, g);
     else if (prec == 2) launch_x6_prec2(ta, tb, cfg, grid, s, g);
-    else if (ta == 0 && tb == 1 && (abl == 0 || abl == 8)) launch_x6_nt_main(cfg, abl, grid, s, g);
-    else if (ta == 0 && tb == 1) launch_x6_nt_abl(cfg, abl, grid, s, g);
-    else launch_x6_h3_other(ta, tb, cfg, abl, grid, s, g);
+    else if (ta == 0 && tb == 1) launch_x6_nt_main(cfg, abl, grid, s, g);
+    else launch_x6_h3_other(ta, tb, cfg, grid, s, g);
 }
 
 // max |x| over a strided (optionally plane-split) matrix, folded into *out by an unsigned
@@ -143,7 +136,7 @@ void launch_absmax(const float* P, int64_t rows, int64_t cols, int64_t ld, int64
 // grid.y = matrix index of a batch of equal-shape matrices.
 __global__ __launch_bounds__(256) void k_wsplit(const float* __restrict__ W, int64_t item_stride, int64_t N, int64_t K,
                                                 int64_t ldw, const float* __restrict__ amax, int64_t amax_stride,
-                                                uint4* __restrict__ img, int64_t img_stride_u4, int bn, int frag) {
+                                                uint4* __restrict__ img, int64_t img_stride_u4, int bn) {
     const int64_t item = blockIdx.y;
     const int64_t ku = K / 8;
     const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -161,12 +154,6 @@ __global__ __launch_bounds__(256) void k_wsplit(const float* __restrict__ W, int
     split2h(b.x * sc, b.y * sc, q0.z, q1.z);
     split2h(b.z * sc, b.w * sc, q0.w, q1.w);
     uint4* dst = img + item * img_stride_u4 + (tn * (K / 32) + sl) * (int64_t)(bn * 8);
-    if (frag) {   // MFMA fragment order: [32-column block][kk][piece][lane = 32 (c & 1) + r % 32]
-        const int pos = (((r >> 5) * 2 + (c >> 1)) * 2) * 64 + (c & 1) * 32 + (r & 31);
-        dst[pos] = q0;
-        dst[pos + 64] = q1;
-        return;
-    }
     const int pos = x6_pos(r, c);
     dst[pos] = q0;
     dst[bn * 4 + pos] = q1;
@@ -184,9 +171,6 @@ extern "C" int bgnn_gemm_wsplit(const float* W, int32_t n_items, int64_t item_st
                                 int64_t ldw, const float* amax, int64_t amax_stride, void* img, int64_t img_stride,
                                 int32_t bn, void* stream) {
     BGNN_REQUIRE(W && amax && img && n_items >= 0 && n_items <= 65535, "wsplit: bad args");
-    // (bn | BGNN_WSPLIT_FRAG: the MFMA-fragment order the B-in-registers kernel loads, BGNN_TUNE_GEMM_PP 4)
-    const int frag = (bn & BGNN_WSPLIT_FRAG) ? 1 : 0;
-    bn &= ~BGNN_WSPLIT_FRAG;
     BGNN_REQUIRE(bn == 128 || bn == 256, "wsplit: column tile must be 128 or 256 (got %d)", bn);
     BGNN_REQUIRE(N > 0 && K > 0 && N % bn == 0 && K % 32 == 0, "wsplit: N %% bn == 0 and K %% 32 == 0 required");
     BGNN_REQUIRE(ldw >= K && ldw % 4 == 0 && item_stride % 4 == 0 && ((uintptr_t)W & 15) == 0,
@@ -197,7 +181,7 @@ extern "C" int bgnn_gemm_wsplit(const float* W, int32_t n_items, int64_t item_st
     const int64_t units = N * (K / 8);
     hipLaunchKernelGGL(k_wsplit, dim3((unsigned)((units + 255) / 256), (unsigned)n_items), dim3(256), 0,
                        as_stream(stream), W, item_stride, N, K, ldw, amax, amax_stride, static_cast<uint4*>(img),
-                       img_stride / 16, (int)bn, frag);
+                       img_stride / 16, (int)bn);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

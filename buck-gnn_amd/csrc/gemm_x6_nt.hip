@@ -1,6 +1,6 @@
 // f16x3 GEMM C = A B^T with K-contiguous operands (the SAGE forward z = x [W_l;W_r]^T and input
 // gradient dx = [dz_l | dh] [W_l;W_r], plus the drop-add epilogue of bgnn_gemm_f32_dropadd):
-// the production instantiations of gemm_x6_kernel.h (ablation 0 and the masked-beta epilogue 8).
+// the instantiations of gemm_x6_kernel.h with the plain (0) and the drop-add (8) epilogue.
 #include "gemm_x6_kernel.h"
 
 namespace bgnn {

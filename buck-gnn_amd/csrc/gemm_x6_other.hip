@@ -4,15 +4,10 @@
 
 namespace bgnn {
 
-void launch_x6_h3_other(int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
-    if (ta == 1 && tb == 0) {   // wgrad: ablation 7 (dword k-major staging) for measurement
-        if (abl == 7) launch_x6_a<1, 1, 0, 7>(cfg, grid, s, g);
-        else launch_x6_a<1, 1, 0, 0>(cfg, grid, s, g);
-    } else if (ta == 0 && tb == 0) {
-        launch_x6_a<1, 0, 0, 0>(cfg, grid, s, g);
-    } else {
-        launch_x6_a<1, 1, 1, 0>(cfg, grid, s, g);
-    }
+void launch_x6_h3_other(int ta, int tb, int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    if (ta == 1 && tb == 0) launch_x6_a<1, 1, 0, 0>(cfg, grid, s, g);
+    else if (ta == 0 && tb == 0) launch_x6_a<1, 0, 0, 0>(cfg, grid, s, g);
+    else launch_x6_a<1, 1, 1, 0>(cfg, grid, s, g);
 }
 
 }  // namespace bgnn

@@ -841,31 +841,12 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                 ml_n = lane < c ? (uint32_t)A.gmask[b + lane] : 0u;
             }
             float a[R][NV][4];
-            // MAX: each element's argmax as an offset in its row's edge list, resolved per (key, row)
-            // from the row's neighbour list (lane k = k-th edge): the first position of the key's
-            // source -- a duplicate edge has the same value, so its first occurrence is the CSR-first
-            // maximum either way; keys arrive in first-appearance order over the group, not in each
-            // row's edge order, so ties take the smaller offset explicitly
-            int32_t gi[(OP == OP_MAX) ? R : 1][(OP == OP_MAX) ? NV : 1][(OP == OP_MAX) ? 4 : 1];
-            int32_t rl[(OP == OP_MAX) ? R : 1];
 #pragma unroll
             for (int t = 0; t < R; ++t)
 #pragma unroll
                 for (int v = 0; v < NV; ++v)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) a[t][v][q] = (OP == OP_MAX) ? -INFINITY : 0.f;
-            if constexpr (OP == OP_MAX) {
-#pragma unroll
-                for (int t = 0; t < R; ++t) {
-                    const int32_t rb = __builtin_amdgcn_readlane(rp, t);
-                    const int32_t dg = t < rows ? __builtin_amdgcn_readlane(rp, t + 1) - rb : 0;
-                    rl[t] = lane < dg ? A.col[rb + lane] : -1;
-#pragma unroll
-                    for (int v = 0; v < NV; ++v)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) gi[t][v][q] = 0;
-                }
-            }
+                    for (int q = 0; q < 4; ++q) a[t][v][q] = 0.f;
             for (int32_t eb = 0; eb < cnt; eb += 64) {
                 const int n = min(64, cnt - eb);
                 int32_t sl = sl0;
@@ -904,26 +885,12 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
                             // where the key is used, by a scalar branch (measured: spmm_bwd 138.5 ->
                             // 135.9 us against a per-lane select, profiles/r04_ab_agg_knobs.txt)
                             if (__builtin_amdgcn_readfirstlane((int)((m[u] >> t) & 1u))) {
-                                if constexpr (OP == OP_MAX) {
-                                    const uint64_t hit = __ballot(rl[t] == j[u]);
-                                    const int32_t off = hit ? (int32_t)__builtin_ctzll(hit) : 0;
 #pragma unroll
-                                    for (int v = 0; v < NV; ++v)
+                                for (int v = 0; v < NV; ++v)
 #pragma unroll
-                                        for (int q = 0; q < 4; ++q) {
-                                            const float x = val[u][v].f[q];
-                                            const bool better = x > a[t][v][q] || (x == a[t][v][q] && off < gi[t][v][q]);
-                                            a[t][v][q] = better ? x : a[t][v][q];
-                                            gi[t][v][q] = better ? off : gi[t][v][q];
-                                        }
-                                } else {
-#pragma unroll
-                                    for (int v = 0; v < NV; ++v)
-#pragma unroll
-                                        for (int q = 0; q < 4; ++q)
-                                            a[t][v][q] += (OP == OP_MEANT) ? __fmul_rn(val[u][v].f[q], w[u])
-                                                                           : val[u][v].f[q];
-                                }
+                                    for (int q = 0; q < 4; ++q)
+                                        a[t][v][q] += (OP == OP_MEANT) ? __fmul_rn(val[u][v].f[q], w[u])
+                                                                       : val[u][v].f[q];
                             }
                         }
                 }
@@ -988,10 +955,7 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
 #pragma unroll
                     for (int v = 0; v < NV; ++v)
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            acc.a[v][q] = a[t][v][q];
-                            if constexpr (OP == OP_MAX) acc.g[v][q] = rb + gi[t][v][q];   // (store_plain: CSR position)
-                        }
+                        for (int q = 0; q < 4; ++q) acc.a[v][q] = a[t][v][q];
                     store_plain<4, NV, OP>(A, acc, r, deg, cpos, cok, tmax);
                 }
             }
@@ -1013,9 +977,9 @@ __global__ __launch_bounds__(256) void k_seg_group(SegArgs A) {
 constexpr int kMaxLightBlocks = 1024;
 
 // Tuning knobs (process-wide; defaults are the production choice; see bgnn_set_tuning).
-static int g_max_group = 0;      // BGNN_TUNE_MAX_GROUP: max aggregation on the row-group kernel
-                                 // (measured slower: cfg2 max forward 156 -> 168 us, the per-(key,
-                                 // row) argmax resolution and tie test outweigh the deduplicated loads)
+// (ABI 12 removed BGNN_TUNE_MAX_GROUP, the max forward on the row-group kernel: bit-identical, but
+// cfg2 156 -> 168 us, the per-(key, row) argmax resolution and tie test outweighing the
+// deduplicated loads; round 5, profiles/r05_bench_max_group_j.json)
 static int g_seg_kernel = 0;     // 0 = auto (row-group kernel where planned, else sweep), 1 = blocked,
                                  // 2 = sweep
 static int g_grp_blocks = 1024;  // row-group kernel grid (4 blocks of 4 waves per CU)
@@ -1101,8 +1065,7 @@ inline HeavyEv* heavy_ev_next(int fwd) {
 // Whether launch_all runs the row-group kernel for this CSR / reduce.
 inline bool use_group(const SegArgs& A, int op, int vec, int lpr) {
     return g_seg_kernel == 0 && A.gcnt != nullptr && vec == 4 && lpr == 64 && A.chunk <= 64 &&
-           (op == OP_SUM || op == OP_MEAN || op == OP_MEANT ||
-            (op == OP_MAX && g_max_group && A.group_rows == 4));
+           (op == OP_SUM || op == OP_MEAN || op == OP_MEANT);
 }
 
 inline int64_t light_blocks_sage(const SegArgs& A) {
@@ -1133,12 +1096,6 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     if (blocks_out) *blocks_out = blocks;
     A.light_slots = (int32_t)blocks;
     if (A.n_rows > 0) {
-        if constexpr (VEC == 4 && LPR == 64 && OP == OP_MAX && EPI == EPI_PLAIN) {
-            if (group) {   // (4-row groups, 4 keys per batch: the argmax offsets take the registers)
-                hipLaunchKernelGGL((k_seg_group<NV, OP, EPI, 4, 4>), dim3((unsigned)blocks), dim3(256), 0, s, A);
-                BGNN_CHECK_LAUNCH();
-            }
-        }
         if constexpr (VEC == 4 && LPR == 64 && (OP == OP_SUM || OP == OP_MEAN || OP == OP_MEANT)) {
             if (group) {
                 const dim3 gr((unsigned)blocks);
@@ -1367,8 +1324,6 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
         case BGNN_TUNE_ROWS_REV: return rows_rev();
-        case BGNN_TUNE_GEMM_PP: return gemm_pp();
-        case BGNN_TUNE_MAX_GROUP: return g_max_group;
         default: return -1;
     }
 }
@@ -1395,11 +1350,6 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
-        case BGNN_TUNE_MAX_GROUP: g_max_group = value ? 1 : 0; return BGNN_OK;
-        case BGNN_TUNE_GEMM_PP:
-            BGNN_REQUIRE(value >= 0 && value <= 6, "set_tuning: gemm staging variant must be 0..6");
-            set_gemm_pp(value);
-            return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value == 0 || value == 2, "set_tuning: gemm mode must be 0 (f32 MFMA) or 2 (f16x3)");
             set_gemm_mode(value);

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 11
+#define BGNN_ABI_VERSION 12
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -82,22 +82,10 @@ const char* bgnn_last_error_string(void);
                                     rounding (the order of the dh bias partials / of the
                                     BatchNorm statistics sums; deterministic either way).
                                     Default 1 (measured: bits 1-3 gain nothing)              */
-#define BGNN_TUNE_GEMM_PP 14  /* f16x3 GEMMs with K-contiguous f32 operands (measurement): bit 0
-                                    = ping-pong main loop (the two waves of a SIMD alternate MFMA
-                                    and staging half steps), bit 1 = line-major staging loads
-                                    (whole 128-B lines per wave load); 0 = neither (default:
-                                    both measured slower, profiles/r05_ab_gemm_*); 4 = the
-                                    pre-split weight path (bgnn_gemm_f32_w) on 128x256 / 256x128
-                                    tiles loads B's MFMA fragments straight from the image into
-                                    registers instead of through LDS, 5 = an interleaved
-                                    steady-state schedule (staging spread between the MFMAs),
-                                    6 = 32x32x16 MFMAs instead of the 16x16x32 default. 0..5 are
-                                    bit-identical to each other; 6 differs within the f16x3 error
-                                    class (another summation order inside the matrix core). */
-#define BGNN_TUNE_MAX_GROUP 15  /* max aggregation (forward) on the row-group kernel where the CSR
-                                    has a 4-row plan (1) or on the sweep kernel (0, default: the
-                                    group form measured 168 against 156 us on cfg2); the same
-                                    values and argmax state */
+/* (ABI 12 retired knobs 14 and 15: the round-5 GEMM main-loop variants (ping-pong, line-major
+ * staging, B fragments in registers, interleaved schedule, 32x32x16 MFMAs), the round-6 wave-order
+ * swap and static priority, and the row-group max aggregation -- all measured slower or equal;
+ * profiles/r05_*, profiles/r06_gemm_ab_b.txt) */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose
@@ -389,8 +377,11 @@ int bgnn_segment_bcast_bf16(const int32_t* rowptr, const int32_t* col, int64_t n
  * bgnn_gemm_ws_bytes() returns 0 for the shape).
  * ---------------------------------------------------------------------- */
 size_t bgnn_gemm_ws_bytes(int64_t M, int64_t N, int64_t K, int32_t trans_a, int32_t trans_b);
-/* Force a tile configuration (tuning/tests; -1 = automatic, the default). Results are
- * identical up to the split-K partition; only speed changes. */
+/* Force a tile configuration (tuning/tests; -1 = automatic, the default; 0..4 = the f16x3 /
+ * bf16 tiles 128x128, 256x128, 128x256, 256x256 (2x4 waves), 256x256 (4x2 waves); values the
+ * GEMM mode has no tile for are rejected). Results are identical up to the split-K partition;
+ * only speed changes. (ABI 12: the timing ablations of 100 * k + cfg, which computed wrong
+ * results, are gone from the library.) */
 int bgnn_gemm_set_cfg(int32_t cfg);
 int bgnn_gemm_f32(int32_t trans_a, int32_t trans_b, int64_t M, int64_t N, int64_t K,
                   float alpha, const float* A, int64_t lda, const float* B, int64_t ldb,
@@ -441,7 +432,6 @@ int bgnn_gemm_f32_dropadd_cols(int64_t M, int64_t N, int64_t K, const float* A, 
                                int64_t ldb, float* C, int64_t ldc, const float* a_amax, const float* b_amax,
                                const float* src, int64_t ld_src, int64_t src_col0, float p, uint64_t seed, void* ws,
                                size_t ws_bytes, void* stream);
-#define BGNN_WSPLIT_FRAG 0x10000
 /* Pre-split weights (round 5). The f16x3 GEMM C = A W^T of the SAGE layers (forward z = x
  * [W_l;W_r]^T, input gradient dx = dz [W_l;W_r]) takes its weight operand W [N, K] as a
  * pre-split image: W scaled by the power of two of max|W| (amax) and split into two f16 pieces
@@ -449,9 +439,7 @@ int bgnn_gemm_f32_dropadd_cols(int64_t M, int64_t N, int64_t K, const float* A, 
  * item_stride, max|W_i| at amax[i * amax_stride], image i at img + i * img_stride bytes), stored
  * per (column tile of bn rows, 32-deep K slice) as the GEMM's own LDS image, so the GEMM copies
  * it into LDS (16-B register copies) instead of loading, splitting and storing it in every row
- * tile. bn | BGNN_WSPLIT_FRAG stores each slice in MFMA-fragment order instead ([32-column
- * block][k16 step][piece][64 lanes x 16 B]), the layout the B-in-registers variant
- * (BGNN_TUNE_GEMM_PP = 4, measurement) loads with one 1-KiB load per wave and fragment. The
+ * tile. The
  * product is bit-identical to bgnn_gemm_f32_scaled / bgnn_gemm_f32_dropadd on the same operands.
  *   bgnn_gemm_w_tile(M, N, K): the column tile bn the image must use for that GEMM shape, or 0
  *     when the shape has no pre-split path (then use bgnn_gemm_f32_scaled);

@@ -114,11 +114,11 @@ def b16_variant():
 @pytest.mark.parametrize("c16", [False, True], ids=["f32C", "bf16C"])
 @pytest.mark.parametrize("gather", [False, True], ids=["plain", "gather"])
 def test_b16_kernel_bit_identical_to_register_staged(dev, b16_variant, mnk, c16, gather):
-    """bf16-stored A and B (storage 3 / 7, the EA_GNN edge products): every form of the LDS-DMA
-    kernel (gemm_b16.hip: per-call default, persistent, one tile per workgroup, k32 slices,
-    128-row tiles, whole-line bf16 C stores) equals the register-staged k_gemm_x6 bit for bit -- bias, gathered node rows,
-    ReLU, f32 or bf16 C, ragged M and N -- and the register-staged result is the bf16-operand
-    product (fp64 reference on the same bf16 operands)."""
+    """bf16-stored A and B (storage 3 / 7, the EA_GNN edge products): the LDS-DMA kernel
+    (gemm_b16.hip: 256 x 256 tiles, whole-line bf16 C stores, gather indices in LDS) equals the
+    register-staged k_gemm_x6 bit for bit -- bias, gathered node rows, ReLU, f32 or bf16 C, ragged
+    M and N -- and the register-staged result is the bf16-operand product (fp64 reference on the
+    same bf16 operands)."""
     M, N, K = mnk
     torch.manual_seed(M + N)
     a = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -143,9 +143,8 @@ def test_b16_kernel_bit_identical_to_register_staged(dev, b16_variant, mnk, c16,
 
     b16_variant(-1)
     ref = run()
-    for v in (0, 6, 7, 1, 2, 3, 8, 9, 10, 11, 12):
-        b16_variant(v)
-        assert torch.equal(run(), ref), v
+    b16_variant(0)
+    assert torch.equal(run(), ref)
     exact = a.double() @ w.double().t() + bias.double()
     if gather:
         exact = exact + p1.double()[i1] + p2.double()[i2]
@@ -278,9 +277,8 @@ def test_gemm_bf16_dropadd_bit_identical_to_two_steps(dev, b16_variant, mnk, p):
     """bgnn_gemm_bf16_dropadd (EA_GNN's edge Linear dgrad + the skip + dropout's gradient of the same
     activation, ea.GradSlot.gemm_dropadd): the drop-add in the LDS-DMA kernel's epilogue equals
     bgnn_gemm_bf16 (bf16 C) followed by bgnn_add_dropped_bf16 on the stored C, bit for bit -- ragged
-    M (the last row tile), N = 256 / 512, K % 64 != 0 (the two-step fallback), every kernel form
-    (the whole-line bf16 C forms with the fused add, the others and the register-staged kernel by
-    the two steps)."""
+    M (the last row tile), N = 256 / 512, K % 64 != 0 (the two-step fallback), with the LDS-DMA
+    kernel (the fused add) and with the register-staged kernel (the two steps)."""
     M, N, K = mnk
     torch.manual_seed(M + K)
     a = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -296,6 +294,6 @@ def test_gemm_bf16_dropadd_bit_identical_to_two_steps(dev, b16_variant, mnk, p):
 
     ref = fused.gemm_bf16(a, w, False, True, out_bf16=True)
     _lib.call("bgnn_add_dropped_bf16", ref.data_ptr(), src.data_ptr(), M * N, float(p), 77, ref.data_ptr(), s)
-    for v in (0, 11, 12, 13, 6, 1, -1):
+    for v in (0, -1):
         b16_variant(v)
         assert torch.equal(fused_(), ref), v

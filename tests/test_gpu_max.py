@@ -144,42 +144,6 @@ def test_maxaggr_model_runs_fused_layers(dev, monkeypatch):
         torch.testing.assert_close(a, c, rtol=1e-3, atol=1e-4)
 
 
-@pytest.mark.parametrize("case", ["mesh", "ties", "super", "dups"])
-def test_max_group_kernel_matches_sweep(dev, case):
-    """Max aggregation on the row-group kernel (BGNN_TUNE_MAX_GROUP = 1) against the per-row sweep
-    kernel (0, the default): the same maxima bit for bit and the same argmax state byte for byte
-    (ties: the first maximum in CSR order, resolved per (key, row) from the row's neighbour list),
-    on meshes with virtual edges, integer features full of ties, super nodes (chunked heavy rows)
-    and duplicate edges."""
-    from bgnn import ops
-    torch.manual_seed(11)
-    b = S.make_batch(4, 12, super_node=(case == "super"))
-    ei = b.edge_index
-    if case == "dups":   # every 7th edge twice
-        ei = torch.cat([ei, ei[:, ::7]], 1)
-        ei = ei[:, torch.argsort(ei[1], stable=True)]
-    N = b.num_nodes
-    H = 512
-    x = torch.randn(N, H)
-    if case == "ties":
-        x = torch.randint(-2, 3, (N, H)).float().clamp_min(0)
-    g = Graph.build(ei.to(dev), N)
-    assert g.fwd.groups is not None
-    xd = x.to(dev)
-    outs = {}
-    try:
-        for knob in (0, 1):
-            bgnn._lib.call("bgnn_set_tuning", 15, knob)
-            out, arg = ops.spmm_fwd(g.fwd, xd, 2, N, want_arg=True)
-            torch.cuda.synchronize()
-            outs[knob] = (out, arg, ops.max_arg_positions(g.fwd, arg, N, H))
-    finally:
-        bgnn._lib.call("bgnn_set_tuning", 15, 0)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][2], outs[1][2])
-    assert torch.equal(outs[0][1][:N * H], outs[1][1][:N * H])   # the per-element bytes (padding aside)
-
-
 def test_compact_argmax_rejects_chunk_beyond_byte_range(dev):
     """The compact argmax state keeps a light row's argmax as a byte offset (heavy rows: marker 255),
     so a CSR whose chunk lets a light row have >= 255 edges is rejected loudly instead of wrapping

@@ -106,13 +106,16 @@ def inmodel(name="GraphSage_addAggr_Shared"):
         c = orig(a, b, trans_a, trans_b, **kw)
         M = a.size(1) if trans_a else a.size(0)
         N = b.size(0) if trans_b else b.size(1)
-        if M <= 1024 and N <= 1024 and not kw:
+        if M <= 1024 and N <= 1024:
             A = a.double().t() if trans_a else a.double()
             B = b.double().t() if trans_b else b.double()
             torch.cuda.synchronize()
-            e = ((c.double() - A @ B).abs() / (A.abs() @ B.abs()).clamp_min(1e-300)).max().item()
-            print(f"  gemm {tuple(a.shape)} x {tuple(b.shape)} ta={trans_a} tb={trans_b}: {e:.2e}"
-                  f" a contiguous {a.is_contiguous()} b contiguous {b.is_contiguous()} strides {a.stride()} {b.stride()}")
+            r = A @ B
+            e = ((c.double() - r).abs() / (A.abs() @ B.abs()).clamp_min(1e-300)).max().item()
+            l2 = ((c.double() - r).norm() / r.norm().clamp_min(1e-300)).item()
+            print(f"  gemm {tuple(a.shape)} x {tuple(b.shape)} ta={trans_a} tb={trans_b}: max/(|A||B|) {e:.2e}"
+                  f" rel L2 {l2:.2e}  ||C|| / || |A||B| || {(r.norm() / (A.abs() @ B.abs()).norm()).item():.2e}",
+                  flush=True)
         return c
     fused.gemm = g
     T.run(dev, name, 512, True)

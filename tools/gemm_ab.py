@@ -1,17 +1,16 @@
 #!/usr/bin/env python
-"""A/B of f16x3 GEMM variants on the SAGE layer shapes, in one process, each timed over REPS
-launches with HIP events with operand maxima supplied (as inside the layer: no absmax passes),
-with a 1 GiB cache flush between launches (cold L2 / Infinity Cache, as inside a training step).
+"""Interleaved A/B of f16x3 GEMM variants on the SAGE layer shapes, in one process: every round
+times each variant once (HIP events, operand maxima supplied as inside the layer, a 1 GiB cache
+flush before each launch: cold L2 / Infinity Cache, as inside a training step); medians over the
+rounds. Results are checked bit-identical to the first variant.
 
-    python tools/gemm_ab.py [--reps 20] [--variants=x-1,x2,x102] [--shapes fwd,dgrad]
+    python tools/gemm_ab.py [--reps 20] [--variants=w,d,w.2] [--shapes fwd,dgrad]
 
-A variant "xC" runs tile config C % 100 with timing ablation C // 100 (bgnn_gemm_set_cfg; x-1 =
-the automatic plan); "pC" the same with the ping-pong main loop (BGNN_TUNE_GEMM_PP = 1), "lC" with
-line-major staging loads (2), "qC" with both (3); "w" the pre-split weight path (bgnn_gemm_wsplit +
-bgnn_gemm_f32_w, the weight image copied into LDS), "d" the same with the drop-add epilogue (src = a
-[M, N] gradient, p = 0.1: the skip layers' dgrad); "r" / "s" as "w" / "d" with B's MFMA fragments
-loaded from the image into registers (BGNN_TUNE_GEMM_PP = 4); "i" / "j" as "w" / "d" with the interleaved
-steady-state schedule (BGNN_TUNE_GEMM_PP = 5); "m" / "n" with 16x16x32 MFMAs (BGNN_TUNE_GEMM_PP = 6).
+Variants: "xC" the register-staged kernel (bgnn_gemm_f32_scaled) on tile config C (-1 = the
+automatic plan); "w" the pre-split weight path (bgnn_gemm_wsplit + bgnn_gemm_f32_w); "d" the same
+with the drop-add epilogue (src = an [M, N] gradient, p = 0.1: the skip layers' dgrad); "w.C" /
+"d.C" on tile config C. (Round 6 measured the main-loop variants "wP" of the then knob 14 here,
+profiles/r06_gemm_ab_b.txt.)
 """
 import argparse
 import os
@@ -27,61 +26,75 @@ SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872,
           "fwd_small": (10082, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
 
 
+def parse(vs):
+    kind = vs[0]
+    if kind == "x":
+        return kind, 0, int(vs[1:])
+    _, _, cfg = vs[1:].partition(".")
+    return kind, 0, int(cfg) if cfg else -1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--variants", default="x-1")
+    ap.add_argument("--variants", default="w,d")
     ap.add_argument("--shapes", default="fwd,dgrad")
     ap.add_argument("--no-flush", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     flush = None if args.no_flush else torch.empty(1 << 28, device=dev)
+    variants = args.variants.split(",")
     for name in args.shapes.split(","):
         M, N, K = SHAPES[name]
         torch.manual_seed(0)
         a = torch.randn(M, K, device=dev)
         b = torch.randn(N, K, device=dev) * 0.05
         am = torch.stack([a.abs().max(), b.abs().max()]).contiguous()
-        out = torch.empty(M, N, device=dev)
         src = torch.randn(M, N, device=dev)
-        ref = None
-        for vs in args.variants.split(","):
-            wimg = None
-            if vs[0] in "wdrsijmn":   # pre-split weight image + bgnn_gemm_f32_w ("wC": tile config C)
-                _lib.call("bgnn_gemm_set_cfg", int(vs[1:]) if len(vs) > 1 else -1)
-                _lib.call("bgnn_set_tuning", 14, {"r": 4, "s": 4, "i": 5, "j": 5, "m": 6, "n": 6}.get(vs[0], 0))
+        outs = {v: torch.empty(M, N, device=dev) for v in variants}
+        imgs = {}
+        for vs in variants:
+            kind, pp, cfg = parse(vs)
+            if kind in "wd":
+                _lib.call("bgnn_gemm_set_cfg", cfg)
                 bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
-                wimg = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
-                _lib.call("bgnn_gemm_wsplit", b.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, wimg.data_ptr(),
-                          wimg.numel(), bn | (0x10000 if vs[0] in "rs" else 0), fused._stream())
-            else:
-                _lib.call("bgnn_gemm_set_cfg", int(vs[1:]))
-                _lib.call("bgnn_set_tuning", 14, {"x": 0, "p": 1, "l": 2, "q": 3}[vs[0]])   # BGNN_TUNE_GEMM_PP
-            ts = []
-            for i in range(args.reps + 3):
+                img = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
+                _lib.call("bgnn_gemm_wsplit", b.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, img.data_ptr(),
+                          img.numel(), bn, fused._stream())
+                imgs[vs] = (img, bn)
+        _lib.call("bgnn_gemm_set_cfg", -1)
+        times = {v: [] for v in variants}
+        for i in range(args.reps + 2):
+            for vs in variants:
+                kind, pp, cfg = parse(vs)
+                _lib.call("bgnn_gemm_set_cfg", cfg)
                 if flush is not None:
                     flush.fill_(float(i))
+                out = outs[vs]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                if wimg is not None:
-                    _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, wimg.data_ptr(), bn, out.data_ptr(), N,
+                if kind in "wd":
+                    img, bn = imgs[vs]
+                    _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N,
                               None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None,
-                              src.data_ptr() if vs[0] in "dsjn" else None, N, 0.1, 1234, fused._stream())
+                              src.data_ptr() if kind == "d" else None, N, 0.1, 1234, fused._stream())
                 else:
                     fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 e1.record()
-                ts.append((e0, e1))
-            torch.cuda.synchronize()
-            us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in ts[3:])
-            med = us[len(us) // 2]
-            same = "" if ref is None else ("bit-identical" if torch.equal(out, ref) else
-                                           f"DIFFERS max {(out - ref).abs().max().item():.3g}")
-            if ref is None:
-                ref = out.clone()
-            print(f"{name:9s} {M}x{N}x{K} staging {vs:>3s}: median {med:7.1f} us  min {us[0]:7.1f}  "
-                  f"{2 * M * N * K / med / 1e6:6.1f} TF  {same}", flush=True)
+                if i >= 2:
+                    times[vs].append((e0, e1))
         _lib.call("bgnn_gemm_set_cfg", -1)
-        _lib.call("bgnn_set_tuning", 14, 0)
+        torch.cuda.synchronize()
+        ref = {}
+        for vs in variants:
+            us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in times[vs])
+            med = us[len(us) // 2]
+            kind = vs[0]
+            r = ref.setdefault(kind == "d", outs[vs])
+            same = "ref" if r is outs[vs] else ("bit-identical" if torch.equal(outs[vs], r) else
+                                                f"DIFFERS max {(outs[vs] - r).abs().max().item():.3g}")
+            print(f"{name:9s} {M}x{N}x{K} {vs:>6s}: median {med:7.1f} us  min {us[0]:7.1f}  "
+                  f"{2 * M * N * K / med / 1e6:6.1f} TF  {same}", flush=True)
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@
 training step runs them: fwd z = x [W_l;W_r]^T, dgrad dx = dz Wcat (B = Wcat^T, K-contiguous), the
 drop-add dgrad of skip layers (bgnn_gemm_f32_dropadd), wgrad dW = dz^T x. Operand maxima supplied
 (as in the layer), 1 GiB cache flush between launches, median of R rounds; bit-identity against
-the default plan.   python tools/gemm_cfg_ab.py [--cfgs -1,5,6,7] [--rounds 15] [--shapes ...]"""
+the default plan.   python tools/gemm_cfg_ab.py [--cfgs -1,1,2,3,4] [--rounds 15] [--shapes ...]"""
 import argparse
 import os
 import sys
@@ -19,7 +19,7 @@ H = 512
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cfgs", default="-1,5,6,7")
+    ap.add_argument("--cfgs", default="-1,1,2,3,4")
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--shapes", default="fwd,dgrad,dropadd,wgrad")
     ap.add_argument("--rows", type=int, default=80656, help="M (node rows; cfg2 = 80656)")

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Run one GEMM (SAGE layer shape) repeatedly with a fixed kernel family / tile config, for
 rocprofv3 counter passes. Usage: tools/gemm_one.py MODE CFG SHAPE [REPS]
-MODE 0 = f32 MFMA, 2 = f16x3 (the bf16x6 mode 1 was removed in ABI 9); CFG as bgnn_gemm_set_cfg (100*k = ablation k);
+MODE 0 = f32 MFMA, 2 = f16x3 (the bf16x6 mode 1 was removed in ABI 9); CFG as bgnn_gemm_set_cfg (-1 = the plan, 0..4 the tiles);
 SHAPE in fwd, dgrad, wgrad. Env GEMM_FLUSH=1 overwrites a 1 GiB buffer between launches
 (cold L2 / Infinity Cache, as inside a training step); GEMM_RELU=1 makes A non-negative with
 ~half zeros (post-ReLU activations)."""

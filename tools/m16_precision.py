@@ -1,8 +1,11 @@
 #!/usr/bin/env python
-"""f16x3 error class of the 16x16x32 MFMA main loop (the default since round 5) against the
-32x32x16 form (BGNN_TUNE_GEMM_PP = 6, pre-split path): max |c - c64| / (|A||B|) and the mean
-signed error relative to |c64| (a truncating accumulator shows as a bias growing with K), on
-positive and on signed operands.
+"""f16x3 error class by MFMA shape: the 4-wave 128x128 tile (bgnn_gemm_set_cfg 0) runs
+v_mfma_f32_32x32x16_f16, the 8-wave tiles (cfg 1-4) v_mfma_f32_16x16x32_f16, on the same operands
+(register-staged path, fused.gemm): max |c - c64| / (|A||B|), the mean signed error relative to
+sum |a b| (the bias a truncating accumulator leaves, growing with K), and the RMS of that relative
+error -- on positive and on signed operands, over K, and on the folded encoder's weight products
+(fused.sage_layer: Wf = Wcat W_in, bf = Wcat b_in, dW = dWf W_in^T, dW_in = Wcat^T dWf,
+db_in = Wcat^T sum(dz)), both shapes.
 
     python tools/m16_precision.py
 """
@@ -16,66 +19,42 @@ import torch  # noqa: E402
 from bgnn import _lib, fused  # noqa: E402
 
 
-def run_w(a, w, pp):
-    M, K = a.shape
-    N = w.size(0)
-    am = torch.stack([a.abs().max(), w.abs().max()]).contiguous()
-    _lib.call("bgnn_set_tuning", 14, pp)
+def gemm_cfg(a, b, ta, tb, cfg):
+    _lib.call("bgnn_gemm_set_cfg", cfg)
     try:
-        bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
-        if bn == 0:
-            return None
-        img = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=a.device)
-        _lib.call("bgnn_gemm_wsplit", w.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, img.data_ptr(), img.numel(),
-                  bn, fused._stream())
-        out = torch.empty(M, N, device=a.device)
-        _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N, None, 0,
-                  am[0:1].data_ptr(), am[1:2].data_ptr(), None, None, 0, 0.0, 0, fused._stream())
-        return out
+        return fused.gemm(a, b, ta, tb)
     finally:
-        _lib.call("bgnn_set_tuning", 14, 0)
+        _lib.call("bgnn_gemm_set_cfg", -1)
 
 
-def stats(c, a, w):
-    r = a.double() @ w.double().t()
-    mag = a.abs().double() @ w.abs().double().t()
-    e = (c.double() - r)
-    return (e.abs() / mag).max().item(), (e / r.abs().clamp_min(1e-300)).mean().item()
+def stats(c, a, b, ta, tb):
+    A = (a.t() if ta else a).double()
+    B = (b.t() if tb else b).double()
+    r, mag = A @ B, A.abs() @ B.abs()
+    e = c.double() - r
+    rel = e / mag.clamp_min(1e-300)
+    return rel.abs().max().item(), rel.mean().item(), rel.pow(2).mean().sqrt().item()
 
 
 def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    # the folded encoder's weight products (fused.sage_layer): Wf = Wcat W_in, bf = Wcat b_in, and
-    # the backward's dW_in = Wcat^T dWf, db_in = Wcat^T sum(dz), dW = dWf W_in^T
-    for (M, N, K, ta, tb) in [(1024, 128, 512, False, False), (1024, 1, 512, False, False),
-                              (512, 128, 1024, True, False), (512, 1, 1024, True, False),
-                              (1024, 512, 128, False, True)]:
-        a = torch.randn((K, M) if ta else (M, K), device=dev) * 0.05
-        b = torch.randn((N, K) if tb else (K, N), device=dev) * 0.05
-        c = fused.gemm(a, b, ta, tb)
-        A = (a.t() if ta else a).double()
-        B = (b.t() if tb else b).double()
-        r, mag = A @ B, A.abs() @ B.abs()
-        e = c.double() - r
-        print(f"fold {M}x{N}x{K} ta={int(ta)} tb={int(tb)}: max {(e.abs() / mag).max().item():.2e} "
-              f"mean|rel| {(e.abs() / r.abs().clamp_min(1e-30)).median().item():.2e}", flush=True)
-    for M, N, K in [(80656, 1024, 512), (4096, 512, 1024)]:
-        for kind in ("signed", "positive"):
-            a = torch.randn(M, K, device=dev)
-            w = torch.randn(N, K, device=dev) * 0.03
+    print("shape                      operands  | 32x32x16 (cfg 0): max      bias       rms  | "
+          "16x16x32 (cfg 1): max      bias       rms")
+    cases = [(1024, 128, 512, False, False), (1024, 1, 512, False, False), (512, 128, 1024, True, False),
+             (512, 1, 1024, True, False), (1024, 512, 128, False, True)]
+    for M, N, K in [(4096, 512, 512), (4096, 512, 1024), (4096, 512, 4096), (4096, 512, 16384)]:
+        cases.append((M, N, K, False, True))
+    for (M, N, K, ta, tb) in cases:
+        for kind in ("positive", "signed"):
+            a = torch.randn((K, M) if ta else (M, K), device=dev) * 0.05
+            b = torch.randn((N, K) if tb else (K, N), device=dev) * 0.05
             if kind == "positive":
-                a, w = a.abs(), w.abs()
-            a = a[: min(M, 8192)].contiguous()
-            Mr = a.size(0)
-            c16 = run_w(a, w, 0)
-            c32 = run_w(a, w, 6)
-            if c16 is None or c32 is None:
-                continue
-            tm = fused.gemm(a, w, False, True)
-            s16, s32, sg = stats(c16, a, w), stats(c32, a, w), stats(tm, a, w)
-            print(f"{Mr}x{N}x{K} {kind:8s}: 16x16x32 max {s16[0]:.2e} bias {s16[1]:+.2e} | 32x32x16 max {s32[0]:.2e} "
-                  f"bias {s32[1]:+.2e} | fused.gemm max {sg[0]:.2e} bias {sg[1]:+.2e}", flush=True)
+                a, b = a.abs(), b.abs()
+            s0 = stats(gemm_cfg(a, b, ta, tb, 0), a, b, ta, tb)
+            s1 = stats(gemm_cfg(a, b, ta, tb, 1), a, b, ta, tb)
+            print(f"{M}x{N}x{K} ta={int(ta)} tb={int(tb)}  {kind:8s} | {s0[0]:.2e} {s0[1]:+.2e} {s0[2]:.2e} | "
+                  f"{s1[0]:.2e} {s1[1]:+.2e} {s1[2]:.2e}", flush=True)
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@
 interleaved in one process; median per-launch HIP-event time, TFLOP/s, and the error
 against an fp64 product as max_ij |c - c64|_ij / (|A| |B|)_ij.
 Variants: "3" = f32 MFMA config 3, "h1" = f16x3 config 1 (bf16x6 "x" variants removed in ABI 9),
-"torch" = torch.mm; add 100*k to a config for timing ablation k (wrong results)."""
+"torch" = torch.mm."""
 import argparse
 import os
 import statistics
