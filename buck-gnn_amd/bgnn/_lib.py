@@ -40,7 +40,7 @@ class CsrStruct(ctypes.Structure):
         ("n_heavy", c_i32),
         ("n_chunks", c_i32),
         ("chunk", c_i32),
-        ("_pad", c_i32),
+        ("ranges_all", c_i32),
         ("gsrc", c_p),
         ("gmask", c_p),
         ("gcnt", c_p),
@@ -48,6 +48,7 @@ class CsrStruct(ctypes.Structure):
         ("n_groups", c_i64),
         ("group_rows", c_i32),
         ("_pad2", c_i32),
+        ("ranges", c_p),
     ]
 
 
@@ -74,7 +75,12 @@ SIGNATURES = {
     "bgnn_heavy_plan": (c_i32, [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "bgnn_spmm_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_spmm_bwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p,
-                              c_p]),
+                              c_i32, c_p]),
+    "bgnn_heavy_ranges_bytes": (c_sz, [c_i32]),
+    "bgnn_heavy_ranges": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_p]),
+    "bgnn_range_partial_bytes": (c_sz, [c_i64, c_i32]),
+    "bgnn_range_sums_finish": (c_i32, [c_p, c_i64, c_i32, ctypes.POINTER(CsrStruct), c_i32, c_p, c_i64, c_p, c_p,
+                                       c_p]),
     "bgnn_bn_slots": (c_i32, [c_i64, c_i32]),
     "bgnn_bn_stats": (c_i32, [c_p, c_i64, c_i32, c_p, c_p]),
     "bgnn_bn_apply": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
@@ -89,13 +95,13 @@ SIGNATURES = {
     "bgnn_group_plan": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "bgnn_store_gather_groups": (c_i32, [c_p, c_i32, c_i32, c_i64, c_i64, c_i64, c_i64] + [c_p] * 14),
     "bgnn_sage_fwd": (c_i32, [ctypes.POINTER(CsrStruct), c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p,
-                              c_p, c_p]),
+                              c_p, c_p, c_i64, c_p]),
     "bgnn_bn_finalize": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
                                  c_p]),
     "bgnn_bn_finalize_shifted": (c_i32, [c_p, c_i32, c_i32, c_i64, c_p, c_p, c_p, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p, c_p,
                                  c_p]),
     "bgnn_bn_eval_coeffs": (c_i32, [c_i32, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p]),
-    "bgnn_sage_apply": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_f32, c_u64, c_i64, c_i32, c_p, c_p, c_p]),
+    "bgnn_sage_apply": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_f32, c_u64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "bgnn_rows_slots": (c_i32, [c_i64]),
     "bgnn_sage_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i64, c_i32, c_p, c_p]),
     "bgnn_reduce_partials": (c_i32, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p]),
@@ -110,7 +116,7 @@ SIGNATURES = {
     "bgnn_small_linear_fwd": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_i32, c_p, c_p]),
     "bgnn_small_linear_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p]),
     "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
-                                   c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p]),
+                                   c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),
     "bgnn_l2norm_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_gemm_bf16": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,
                                c_p, c_i32, c_i32, c_p, c_sz, c_p]),

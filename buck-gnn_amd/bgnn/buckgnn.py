@@ -25,7 +25,9 @@ from torch import Tensor, nn
 
 from . import ea as ea_mod
 from .ea import GradSlot as EAGradSlot, graphnet_block, skip_dropout
-from .fused import mlp, mlp_bf16, prepare_weights, sage_layer, small_mlp
+from . import _lib
+from . import fused as _fused
+from .fused import RangeRows, mlp, mlp_bf16, prepare_weights, sage_layer, small_mlp
 from .graph import SegmentIndex, graph_for, _index_cache
 from .nn import SAGEConv, SAGPooling, global_mean_pool, scatter_mean
 from .ops import segment_reduce
@@ -116,6 +118,21 @@ def super_node_index(batch: Optional[Tensor], n_nodes: int, device) -> Tensor:
         return torch.zeros(0, dtype=torch.long, device=device)
     change = torch.nonzero(batch[1:] != batch[:-1]).flatten()
     return torch.cat([change, torch.tensor([batch.numel() - 1], device=batch.device)])
+
+
+def _range_rows_on(graph, red: int, n_rows: int, H: int) -> bool:
+    """Whether the fused sum / mean layer loop takes the range-row path (fused.RangeRows) on this
+    graph: it has heavy rows, the row passes' blocks are short enough for the 3 range slots
+    (bgnn_range_sums_finish: rows per block <= 2 (chunk + 1)), and the transposed and forward ranges
+    are computed (Csr.ensure_ranges)."""
+    if not _fused.RANGE_ROWS or red == 2 or H > 512 or graph.fwd.plan.n_heavy <= 0:
+        return False
+    slots = _lib.query("bgnn_rows_slots", n_rows)
+    if (n_rows + slots - 1) // slots > 2 * (graph.fwd.plan.chunk + 1):
+        return False
+    graph.fwd.ensure_ranges()
+    graph.bwd.ensure_ranges()
+    return True
 
 
 class BuckGNN(nn.Module):
@@ -249,24 +266,31 @@ class BuckGNN(nn.Module):
             graph = graph_for(edge_index, x.size(0))
             red = {"mean": 1, "max": 2}.get(aggr, 0)
             amax = x_amax   # max|x| of the running features: each layer's apply kernel folds it in
-            # per-layer operand maxima and the folded layer's weight-product maxima, one fill
-            scratch = torch.zeros(3 * L + 5, dtype=torch.float32, device=x.device)
-            bufs, fold_amax = scratch[:3 * L].view(L, 3), scratch[3 * L:]
+            # per-layer operand maxima (slot 3: max|.| of the layer output's [N + R, H] range-row
+            # buffer, fused.RangeRows) and the folded layer's weight-product maxima, one fill
+            scratch = torch.zeros(4 * L + 5, dtype=torch.float32, device=x.device)
+            bufs, fold_amax = scratch[:4 * L].view(L, 4), scratch[4 * L:]
             layers = [convs[i] if convs is not None else self.shared_graphsage_block for i in range(L)]
+            rng_on = _range_rows_on(graph, red, x.size(0), layers[0].lin_l.weight.size(0))
+            R = graph.fwd.plan.n_heavy if rng_on else 0
             wprep = prepare_weights([(c.lin_l.weight, c.lin_r.weight) for c in layers], bufs,
                                     [not (i == 0 and x_in is not None) for i in range(L)],
-                                    n_rows=x.size(0) if red != 2 else 0)
+                                    n_rows=x.size(0) + R if red != 2 else 0)
             self._count_bn_batches(bns)
+            x_full = None
             for i in range(L):
                 conv = layers[i]
                 bn = bns[i] if bns is not None else None
                 skip = 0 < i < L - 1
                 fold = x_in if i == 0 else None
+                rng = (RangeRows(x_full=x_full, x_amax=bufs[i - 1, 3:4] if x_full is not None else None,
+                                 out=i < L - 1, out_amax=bufs[i, 3:4]) if rng_on else None)
                 x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
                                      skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
                                      amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
                                      b_in=None if fold is None else fold.bias, wprep=wprep[i], count_batch=False,
-                                     fold_amax=fold_amax)
+                                     fold_amax=fold_amax, rng=rng)
+                x_full = rng.holder[0] if (rng is not None and rng.holder) else None
             return x
         if x_in is not None:   # (only reached when the caller folded the encoder's last Linear)
             x = x_in(x)

@@ -577,8 +577,32 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+class RangeRows:
+    """Range-row plumbing of one fused sum / mean layer (csrc/ranges.hip; Csr.ensure_ranges): the
+    super nodes of a stiffened batch (VirtualEdgeCreate.py:81-113) aggregate their graph's whole
+    contiguous real-node range, so
+      forward   the previous layer's bgnn_sage_apply also writes the range sums S of x_next as R
+                extra rows after it ([N + R, H], x_full); this layer's GEMM runs on all N + R rows,
+                and z_l's extra rows (S W_l^T = the summed z_l rows) are the range rows' aggregates
+                (bgnn_sage_fwd heavy_agg) -- no chunk pass over the real rows;
+      backward  bgnn_sage_bwd_rows also sums dh over each transposed range row's targets, and
+                bgnn_range_sums_finish writes those dz_l rows (bgnn_spmm_bwd heavy_done).
+    x_full / x_amax: the input's [N + R, H] buffer and a device scalar >= its max |.| (the GEMM's A
+    scale), or None; out: write the range sums of x_next into `out_amax`'s layer buffer, appended
+    to `holder`; bwd: the backward takes the range path."""
+    __slots__ = ("x_full", "x_amax", "out", "out_amax", "bwd", "holder")
+
+    def __init__(self, x_full=None, x_amax=None, out=False, out_amax=None, bwd=True):
+        self.x_full, self.x_amax, self.out, self.out_amax, self.bwd = x_full, x_amax, out, out_amax, bwd
+        self.holder = []
+
+
+# range rows (RangeRows) for stiffened batches; False: the chunk + combine path for every heavy row
+RANGE_ROWS = True
+
+
 class LayerConfig:
-    __slots__ = ("reduce", "bn", "training", "momentum", "eps", "skip", "p", "seed", "famax")
+    __slots__ = ("reduce", "bn", "training", "momentum", "eps", "skip", "p", "seed", "famax", "rng")
 
     def __init__(self, reduce: int, bn: bool, training: bool, momentum: float, eps: float, skip: bool,
                  p: float, seed: int):
@@ -594,9 +618,11 @@ class LayerConfig:
         # (max|Wcat|, max|W_in|, max|b_in|, max|dWf|, max|dbf|), so those small f16x3 GEMMs need no
         # max pass (and no zero fill) of their own
         self.famax = None
+        self.rng = None     # RangeRows (range rows of a stiffened batch) or None
 
 
-def _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean, running_var, cfg: LayerConfig, next_amax):
+def _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean, running_var, cfg: LayerConfig, next_amax,
+              graph: Graph = None):
     """The layer glue after the normalised SAGE output o (Models/BuckGNN.py:436-444): BatchNorm
     finalize (train: batch statistics from the aggregation's partial sums, running stats updated;
     eval: running stats), then x_next = drop(relu(o * scale + shift) + skip * x_prev) with
@@ -629,9 +655,23 @@ def _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean, running_var,
                       running_var.data_ptr(), scale.data_ptr(), shift.data_ptr(), s)
             mean.copy_(running_mean)
             invstd.copy_(torch.rsqrt(running_var + cfg.eps))
+    rng = cfg.rng
+    if rng is not None and rng.out:
+        # x_next and the next layer's range sums S in one [N + R, H] buffer (RangeRows)
+        R = graph.fwd.plan.n_heavy
+        full = torch.empty(N + R, H, dtype=torch.float32, device=dev)
+        x_next = full[:N]
+        rp = torch.empty(_lib.query("bgnn_range_partial_bytes", N, H) // 4, dtype=torch.float32, device=dev)
+        _lib.call("bgnn_sage_apply", o.data_ptr(), _ptr(scale), _ptr(shift), x_prev.data_ptr(), int(cfg.skip),
+                  float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), graph.fwd.ranges.data_ptr(),
+                  rp.data_ptr(), s)
+        _lib.call("bgnn_range_sums_finish", rp.data_ptr(), N, H, graph.fwd.ref(), 0, full[N:].data_ptr(), H,
+                  next_amax.data_ptr(), rng.out_amax.data_ptr(), s)
+        rng.holder.append(full)
+        return x_next, (scale, shift, mean, invstd)
     x_next = torch.empty(N, H, dtype=torch.float32, device=dev)
     _lib.call("bgnn_sage_apply", o.data_ptr(), _ptr(scale), _ptr(shift), x_prev.data_ptr(), int(cfg.skip),
-              float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), s)
+              float(cfg.p), cfg.seed, N, H, x_next.data_ptr(), next_amax.data_ptr(), None, None, s)
     return x_next, (scale, shift, mean, invstd)
 
 
@@ -713,6 +753,15 @@ class SageLayerFn(torch.autograd.Function):
         if x_amax is None:
             x_amax = absmax(x_prev)
         planes = Z_PLANES and H % PLANE_TILE == 0 and not folded
+        # range rows (RangeRows): x_prev is the head of an [N + R, H] buffer whose last R rows are the
+        # range sums of x_prev; the GEMM runs on all N + R rows and z_l's extra rows are the range
+        # rows' aggregates
+        rng = cfg.rng
+        x_full = rng.x_full if (rng is not None and rng.x_full is not None and not folded and not planes) else None
+        if x_full is not None and x_full.data_ptr() != x_prev.data_ptr():
+            raise RuntimeError("sage_layer: RangeRows.x_full must start at x_prev")
+        xa, a_amax_g = (x_full, rng.x_amax) if x_full is not None else (x_prev, x_amax)
+        M = xa.size(0)
         # (the folded layer's transform has K = K_in, not H: timed under its own name so the
         # bench's flops per launch are right for every launch it averages)
         with _timed("gemm_fwd_fold" if folded else "gemm_fwd"):
@@ -720,15 +769,17 @@ class SageLayerFn(torch.autograd.Function):
                 z = torch.empty(2, N, H, dtype=torch.float32, device=dev)
                 gemm(x_prev, wmat, trans_a=False, trans_b=True, out=Planes(z), a_amax=x_amax, b_amax=w_amax)
                 zl, zr, ldz = z[0], z[1], H
-            elif img_f is not None and not folded:   # pre-split [W_l;W_r] staged by LDS-DMA
-                z = torch.empty(N, 2 * H, dtype=torch.float32, device=dev)
-                _lib.call("bgnn_gemm_f32_w", N, 2 * H, H, x_prev.data_ptr(), x_prev.stride(0), img_f.img_f.data_ptr(),
-                          img_f.bn_f, z.data_ptr(), 2 * H, None, 0, x_amax.data_ptr(), w_amax.data_ptr(), None, None, 0,
-                          0.0, 0, _stream())
+            elif (img_f is not None and not folded
+                  and _lib.query("bgnn_gemm_w_tile", M, 2 * H, H) == img_f.bn_f):   # pre-split [W_l;W_r]
+                z = torch.empty(M, 2 * H, dtype=torch.float32, device=dev)
+                _lib.call("bgnn_gemm_f32_w", M, 2 * H, H, xa.data_ptr(), xa.stride(0), img_f.img_f.data_ptr(),
+                          img_f.bn_f, z.data_ptr(), 2 * H, None, 0, a_amax_g.data_ptr(), w_amax.data_ptr(), None, None,
+                          0, 0.0, 0, _stream())
                 zl, zr, ldz = z, z[:, H:], 2 * H
-            else:        # interleaved [N, 2H]
-                z = gemm(x_prev, wmat, trans_a=False, trans_b=True, bias=bf, a_amax=x_amax, b_amax=w_amax)
+            else:        # interleaved [M, 2H]
+                z = gemm(xa, wmat, trans_a=False, trans_b=True, bias=bf, a_amax=a_amax_g, b_amax=w_amax)
                 zl, zr, ldz = z, z[:, H:], 2 * H
+        hagg = z[N:] if x_full is not None else None
         o = torch.empty(N, H, dtype=torch.float32, device=dev)
         nrm = torch.empty(N, dtype=torch.float32, device=dev)
         slots = _lib.query("bgnn_sage_fwd_slots", graph.fwd.ref())
@@ -738,10 +789,11 @@ class SageLayerFn(torch.autograd.Function):
         s = _stream()
         with _timed("sage_fwd"):
             _lib.call("bgnn_sage_fwd", graph.fwd.ref(), zl.data_ptr(), ldz, zr.data_ptr(), ldz, b_l.data_ptr(), H,
-                      cfg.reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part), s)
-        del z, zl, zr
+                      cfg.reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part), _ptr(hagg),
+                      2 * H if hagg is not None else 0, s)
+        del z, zl, zr, hagg
         x_next, (scale, shift, mean, invstd) = _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean,
-                                                         running_var, cfg, next_amax)
+                                                         running_var, cfg, next_amax, graph)
         ctx.graph = graph
         ctx.cfg = cfg
         ctx.folded = folded
@@ -785,13 +837,22 @@ class SageLayerFn(torch.autograd.Function):
         gskip = torch.empty(N, H, dtype=torch.float32, device=dev) if (cfg.skip and not dropadd) else None
         rs = _lib.query("bgnn_rows_slots", N)
         part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
+        # range rows (RangeRows): the transposed range rows' dz_l rows summed by this pass
+        bw = graph.bwd
+        rb = (cfg.rng is not None and cfg.rng.bwd and not planes and bw.ranges is not None)
+        rp = (torch.empty(_lib.query("bgnn_range_partial_bytes", N, H) // 4, dtype=torch.float32, device=dev)
+              if rb else None)
         _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), o.data_ptr(), nrm.data_ptr(),
                   _ptr(scale) if bn else None, _ptr(shift) if bn else None,
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
                   float(cfg.p), cfg.seed, int(cfg.skip and not dropadd), N, H, dh.data_ptr(), lddz, _ptr(gskip),
                   part_db.data_ptr(), dz_amax.data_ptr(), graph.fwd.rowptr.data_ptr() if ctx.folded else None,
-                  (2 if cfg.reduce == 1 else 1) if ctx.folded else 0, s)
+                  (2 if cfg.reduce == 1 else 1) if ctx.folded else 0, _ptr(bw.ranges) if rb else None,
+                  graph.fwd.rowptr.data_ptr() if (rb and cfg.reduce == 1) else None, _ptr(rp), s)
+        if rb:   # the super nodes' dz_l rows (and their max |.| into dz_amax)
+            _lib.call("bgnn_range_sums_finish", rp.data_ptr(), N, H, bw.ref(), 1, dzl.data_ptr(), lddz, None,
+                      dz_amax.data_ptr(), s)
         db2 = torch.empty(2 if ctx.folded else 1, H, dtype=torch.float32, device=dev)
         # sum of dh (db_l) into the last row; folded input transform: the column sums of dz_l = A^T dh
         # into row 0, so that db2 viewed flat is [sum dz_l ; sum dh], the folded layer's dbf
@@ -799,12 +860,11 @@ class SageLayerFn(torch.autograd.Function):
                   db2[0].data_ptr() if ctx.folded else None, 0, s)
         db, db_zl = db2[-1], (db2[0] if ctx.folded else None)
         # dz_l = A^T dh (transpose CSR; MEAN scales by the target's in-degree)
-        bw = graph.bwd
         part = torch.empty(bw.plan.n_chunks * H, dtype=torch.float32, device=dev) if bw.plan.n_chunks else None
         with _timed("spmm_bwd"):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
                       dh.data_ptr(), lddz, H, cfg.reduce, dzl.data_ptr(), lddz, _ptr(part),
-                      dz_amax.data_ptr(), s)
+                      dz_amax.data_ptr(), int(rb), s)
         has_affine = bn and gamma.numel() > 0
         if ctx.folded:
             # x = h W_in^T + b_in folded in: dh = dz Wf; dWf = dz^T h; dbf = column sums of dz;
@@ -838,7 +898,8 @@ class SageLayerFn(torch.autograd.Function):
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
         wcat_t = (ctx.wcat_t if ctx.wcat_t is not None else wcat.t().contiguous()) if DGRAD_WT else wcat
         img_d = ctx.img_d if (not planes and DGRAD_WT) else None
-        if img_d is not None and (dropadd or gskip is None):   # pre-split [W_l;W_r]^T by LDS-DMA
+        if (img_d is not None and (dropadd or gskip is None)
+                and _lib.query("bgnn_gemm_w_tile", N, H, 2 * H) == img_d.bn_d):   # pre-split [W_l;W_r]^T
             dx = torch.empty(N, H, dtype=torch.float32, device=dev)
             with _timed("gemm_dgrad"):
                 _lib.call("bgnn_gemm_f32_w", N, H, 2 * H, dz.data_ptr(), lddz, img_d.img_d.data_ptr(), img_d.bn_d,
@@ -901,7 +962,7 @@ def _max_rows_fwd(y, b_l, H: int):
     slots = _lib.query("bgnn_sage_fwd_slots", csr.ref())
     bn_part = torch.empty(slots, 2, H, dtype=torch.float32, device=dev)
     _lib.call("bgnn_sage_fwd", csr.ref(), y.data_ptr(), y.stride(0), y.data_ptr(), y.stride(0), bias.data_ptr(), H,
-              0, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), None, _stream())
+              0, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), None, None, 0, _stream())
     return o, nrm, bn_part, slots
 
 
@@ -1046,7 +1107,7 @@ class SageMaxLayerFn(torch.autograd.Function):
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
                   float(cfg.p), cfg.seed, 0, N, H, dh.data_ptr(), H, None, part_db.data_ptr(), dz_amax.data_ptr(),
-                  None, 0, s)
+                  None, 0, None, None, None, s)
         db = torch.empty(H, dtype=torch.float32, device=dev)
         _lib.call("bgnn_reduce_partials", part_db.data_ptr(), rs, H, db.data_ptr(), None, 0, s)
         dx, dw_l, dw_r = _max_backward(dh, dz_amax, wcat_t, x_prev, agg, arg, ctx.graph, x_amax, w_amax,
@@ -1164,13 +1225,14 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
                seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None,
                w_in: torch.Tensor = None, b_in: torch.Tensor = None, wprep=None, count_batch: bool = True,
-               fold_amax: torch.Tensor = None):
+               fold_amax: torch.Tensor = None, rng: RangeRows = None):
     """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
     x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
     spares the GEMM a pass over x_prev; return_amax: also return max|x_next|.
     w_in / b_in: fold a preceding Linear into this layer (x_prev is then that Linear's INPUT h,
     and the layer computes on x = h W_in^T + b_in without materialising x); only for a layer
-    without skip connection (the reference's first SAGE layer after the node encoder)."""
+    without skip connection (the reference's first SAGE layer after the node encoder).
+    rng: the range-row plumbing of a stiffened batch (RangeRows; sum / mean only)."""
     require_cuda(x_prev, w_l, b_l, w_r, what="sage_layer")
     H = w_l.size(0)
     if w_in is None and x_prev.size(1) != H:
@@ -1194,6 +1256,7 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                           else 0.0, float(bn_module.eps), skip, p, seed)
         cfg.p = p if training else 0.0
         cfg.famax = fold_amax if w_in is not None else None
+        cfg.rng = rng if reduce != 2 else None
         if reduce == 2:
             out = SageMaxLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
                                        bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, wprep)
@@ -1204,6 +1267,7 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
         cfg.famax = fold_amax if w_in is not None else None
+        cfg.rng = rng if reduce != 2 else None
         if reduce == 2:
             out = SageMaxLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
                                        wprep)
@@ -1258,7 +1322,7 @@ class SageConvFn(torch.autograd.Function):
         with _timed("conv_sage_fwd"):
             _lib.call("bgnn_sage_fwd", graph.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H,
                       bias.data_ptr(), H, reduce, o.data_ptr(), nrm.data_ptr(), bn_part.data_ptr(), _ptr(part),
-                      _stream())
+                      None, 0, _stream())
         ctx.save_for_backward(x, o, nrm, wcat, x_amax, w_amax)
         return o
 
@@ -1293,7 +1357,7 @@ class SageConvFn(torch.autograd.Function):
         with _timed("conv_spmm_bwd"):
             _lib.call("bgnn_spmm_bwd", bw.ref(), graph.perm_t.data_ptr(), graph.fwd.rowptr.data_ptr(),
                       dh.data_ptr(), 2 * H, H, ctx.reduce, dz.data_ptr(), 2 * H, _ptr(part),
-                      dz_amax.data_ptr(), s)
+                      dz_amax.data_ptr(), 0, s)
         dx = None
         if ctx.needs_input_grad[0]:
             with _timed("conv_gemm_dgrad"):

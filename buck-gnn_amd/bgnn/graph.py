@@ -117,6 +117,10 @@ class Csr:
     plan: Plan
     groups: Optional[Groups] = None
     _struct: Optional[_lib.CsrStruct] = field(default=None, repr=False)
+    # heavy-row ranges (bgnn_heavy_ranges, ensure_ranges): None until requested; ranges_all = 1 when
+    # every heavy row is a range row, 0 when not, -1 unknown (ensure_ranges reads it back once)
+    ranges: Optional[torch.Tensor] = field(default=None, repr=False)
+    ranges_all: int = -1
 
     def struct(self) -> _lib.CsrStruct:
         if self._struct is None:
@@ -126,11 +130,30 @@ class Csr:
             self._struct = _lib.CsrStruct(
                 self.rowptr.data_ptr(), self.col.data_ptr(), p.heavy_row.data_ptr(),
                 p.heavy_chunk0.data_ptr(), p.chunk_heavy.data_ptr(), self.n_rows, self.nnz,
-                p.n_heavy, p.n_chunks, p.chunk, 0,
+                p.n_heavy, p.n_chunks, p.chunk, max(self.ranges_all, 0) if self.ranges is not None else 0,
                 gr.gsrc.data_ptr() if gr else None, gr.gmask.data_ptr() if gr else None,
                 gr.gcnt.data_ptr() if gr else None, _ptr(gr.grow) if gr else None,
-                gr.n_groups if gr else 0, gr.rows if gr else 0, 0)
+                gr.n_groups if gr else 0, gr.rows if gr else 0, 0, _ptr(self.ranges))
         return self._struct
+
+    def ensure_ranges(self) -> Optional[torch.Tensor]:
+        """The heavy rows' source ranges (bgnn_heavy_ranges; include/bgnn.h): a super node wired to
+        its graph's contiguous real-node range is a "range row", whose aggregation the row passes
+        sum as a by-product (ranges.hip). Computed once per CSR; when ranges_all is not known (no
+        GraphStore hint) it is read back with one host sync."""
+        p = self.plan
+        if p.n_heavy <= 0:
+            return None
+        if self.ranges is None:
+            buf = torch.empty(_lib.query("bgnn_heavy_ranges_bytes", p.n_heavy) // 4, dtype=torch.int32,
+                              device=self.rowptr.device)
+            self._struct = None
+            _lib.call("bgnn_heavy_ranges", self.ref(), buf.data_ptr(), _stream())
+            self.ranges = buf
+            if self.ranges_all < 0:
+                self.ranges_all = int(int(buf[0].item()) == p.n_heavy)
+            self._struct = None
+        return self.ranges
 
     def ref(self):
         return ctypes.byref(self.struct())

@@ -67,7 +67,7 @@ def spmm_bwd(csr_t, perm_t, fwd_rowptr, g: torch.Tensor, reduce: int, arg, out_r
             _lib.call("bgnn_spmm_bwd", csr_t.ref(), None if perm_t is None else perm_t.data_ptr(),
                       None if fwd_rowptr is None else fwd_rowptr.data_ptr(), g.data_ptr(), g.stride(0), H, reduce,
                       gx.data_ptr(), gx.stride(0), None if part is None else part.data_ptr(),
-                      None if amax is None else amax.data_ptr(), _stream())
+                      None if amax is None else amax.data_ptr(), 0, _stream())
     return gx
 
 

@@ -125,6 +125,7 @@ class GraphStore:
             self.gmask_t = torch.empty(max(sumE, 1), dtype=torch.uint8, device=dev)
             self.gcnt = torch.zeros(max(sumG, 1), dtype=torch.int32, device=dev)
             self.gcnt_t = torch.zeros(max(sumG, 1), dtype=torch.int32, device=dev)
+        self.ranges_all = [True, True]   # (fwd, bwd): every heavy row a range row (_build_group)
         g0 = 0
         while g0 < G:
             g1 = g0 + 1
@@ -177,6 +178,13 @@ class GraphStore:
         hf, cf = _heavy_counts(gr.fwd.rowptr, gid_n, Gg, self.chunk)
         hb, cb = _heavy_counts(gr.bwd.rowptr, gid_n, Gg, self.chunk)
         heavy[g0:g1] = torch.stack([hf, cf, hb, cb], 1)
+        # range rows (graph.Csr.ensure_ranges): whether every heavy row of these graphs is one; a
+        # graph's ranges are graph-local and stay increasing and disjoint in any batch of graphs, so
+        # the store-wide answer holds for every batch (its CSRs then skip the read-back)
+        for i, csr in enumerate((gr.fwd, gr.bwd)):
+            if csr.plan.n_heavy > 0:
+                csr.ensure_ranges()
+                self.ranges_all[i] = self.ranges_all[i] and csr.ranges_all == 1
 
     # ------------------------------------------------------------------------------------
     def batch(self, graph_ids: Sequence[int]) -> Batch:
@@ -245,8 +253,10 @@ class GraphStore:
         # graph structure of the batch, registered for prepare()/SAGEConv/BuckGNN
         hv = self.heavy[ids].sum(0)
         gf, gb = self._groups(ids, gt_d, dn, de, ne, Nb, Eb)
-        fwd = Csr(rowptr, col, Nb, Eb, self._plan(rowptr, Nb, Eb, int(hv[0]), int(hv[1])), gf)
-        bwd = Csr(rowptr_t, col_t, Nb, Eb, self._plan(rowptr_t, Nb, Eb, int(hv[2]), int(hv[3])), gb)
+        fwd = Csr(rowptr, col, Nb, Eb, self._plan(rowptr, Nb, Eb, int(hv[0]), int(hv[1])), gf,
+                  ranges_all=int(self.ranges_all[0]))
+        bwd = Csr(rowptr_t, col_t, Nb, Eb, self._plan(rowptr_t, Nb, Eb, int(hv[2]), int(hv[3])), gb,
+                  ranges_all=int(self.ranges_all[1]))
         graph = Graph(Nb, Eb, fwd, bwd, perm_t, ei_b, None)
         _graph_cache.put(ei_b, (Nb, self.chunk), graph)
         # pooling segments: graph b owns positions [ptr[b], ptr[b+1])

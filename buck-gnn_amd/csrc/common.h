@@ -48,6 +48,14 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// xcd_remap with each XCD's share walked from its last block down
+__device__ __forceinline__ int xcd_remap_rev(int b, int nblk) {
+    const int q = nblk / kNumXcd, r = nblk % kNumXcd;
+    const int x = b % kNumXcd, i = b / kNumXcd;
+    const int len = x < r ? q + 1 : q;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + len - 1 - i;
+}
+
 // Wave-wide sum over groups of `width` lanes (width a power of two ≤ 64).
 __device__ __forceinline__ float group_sum(float v, int width) {
     for (int m = width >> 1; m > 0; m >>= 1) v += __shfl_xor(v, m, kWave);

@@ -7,18 +7,9 @@
 // contiguous row ranges, reduced afterwards in fp64 in a fixed order, so results
 // do not depend on scheduling.
 #include "common.h"
+#include "ranges.h"
 
 namespace bgnn {
-
-constexpr int kRowsBlocks = 1024;   // max partial slots for row-blocked reductions (2048: rows 112 -> 121 us, stats 58 -> 61 us)
-
-inline int64_t rows_grid(int64_t n_rows, int rows_per_block_min, int64_t* rpb) {
-    int64_t blocks = (n_rows + rows_per_block_min - 1) / rows_per_block_min;
-    if (blocks > kRowsBlocks) blocks = kRowsBlocks;
-    if (blocks < 1) blocks = 1;
-    *rpb = (n_rows + blocks - 1) / blocks;
-    return blocks;
-}
 
 // ---------------------------------------------------------------------------
 // Stage 1 of every partial-slot reduction: [n_slots, 2H] -> kGroups group sums,
@@ -275,6 +266,98 @@ __global__ __launch_bounds__(256) void k_sage_apply(const float4* __restrict__ o
     if (amax) block_amax(amax, m);
 }
 
+// Row-blocked form of k_sage_apply with the range partials of x_next (bgnn_sage_apply given a
+// `ranges` buffer; ranges.hip): block lb owns rows [lb rpb, (lb+1) rpb) of the bgnn_rows_slots
+// partition, one wave per row (two rows in flight). The element-wise arithmetic, the dropout mask
+// index and the store are k_sage_apply's, so x_next has the same bits. Like k_sage_apply's `rev`
+// sweep, each XCD takes its share of the row blocks from the last one down and each block its rows
+// from the last one down, so the first rows read are the ones the aggregation on that XCD wrote last
+// (still in the Infinity Cache). Each wave adds its rows' x_next into its own LDS sum per range
+// slot (BlockRanges; the slot is wave-uniform, so no register array is indexed); the 4 waves' sums
+// are added in wave order into rpart[lb][slot][H] (every slot written, 0 when unused).
+template <int NV>
+__global__ __launch_bounds__(256) void k_sage_apply_rows(const float* __restrict__ o, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift,
+                                                         const float* __restrict__ xprev, int skip, uint32_t thr,
+                                                         float inv_keep, uint64_t seed, int64_t n_rows, int H,
+                                                         int64_t rpb, float* __restrict__ xn,
+                                                         uint32_t* __restrict__ amax, int nt,
+                                                         const int32_t* __restrict__ ranges,
+                                                         float* __restrict__ rpart) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lb = xcd_remap_rev(blockIdx.x, gridDim.x);
+    const int64_t r0 = (int64_t)lb * rpb;
+    const int64_t r1 = min(n_rows, r0 + rpb);
+    const int H4 = H / 4;
+    BlockRanges br;
+    br.load(ranges, r0, r1);
+    __shared__ float4 racc[4][kRangeSlots][128];
+    int c4[NV];
+    bool cok[NV];
+    float4 sc[NV], sh[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        c4[v] = lane + 64 * v;
+        cok[v] = c4[v] < H4;
+        const int c = cok[v] ? 4 * c4[v] : 0;
+        sc[v] = scale ? *reinterpret_cast<const float4*>(scale + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+        sh[v] = shift ? *reinterpret_cast<const float4*>(shift + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < kRangeSlots; ++q)
+            if (cok[v]) racc[wave][q][c4[v]] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    uint32_t m = 0;
+    auto row = [&](int64_t r) {
+        const int sl = br.slot(r);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (!cok[v]) continue;
+            const int64_t i = r * H4 + c4[v];
+            const float4 ov = reinterpret_cast<const float4*>(o)[i];
+            float y[4] = {ov.x, ov.y, ov.z, ov.w};
+            if (scale) {
+                y[0] = y[0] * sc[v].x + sh[v].x; y[1] = y[1] * sc[v].y + sh[v].y;
+                y[2] = y[2] * sc[v].z + sh[v].z; y[3] = y[3] * sc[v].w + sh[v].w;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[k] = fmaxf(y[k], 0.f);
+            if (skip) {
+                const float4 p = reinterpret_cast<const float4*>(xprev)[i];
+                y[0] += p.x; y[1] += p.y; y[2] += p.z; y[3] += p.w;
+            }
+            if (thr) {
+                const uint32_t keep = keep_bits4(seed, (uint64_t)i, thr);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) y[k] = ((keep >> k) & 1u) ? y[k] * inv_keep : 0.f;
+            }
+            store4(xn + 4 * i, y[0], y[1], y[2], y[3], nt);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m = max(m, __float_as_uint(y[k]) & 0x7fffffffu);
+            if (sl >= 0) {
+                float4 t = racc[wave][sl][c4[v]];
+                t.x += y[0]; t.y += y[1]; t.z += y[2]; t.w += y[3];
+                racc[wave][sl][c4[v]] = t;
+            }
+        }
+    };
+    int64_t r = r1 - 1 - wave;
+    for (; r - 4 >= r0; r -= 8) {
+        row(r);
+        row(r - 4);
+    }
+    if (r >= r0) row(r);
+    if (amax) block_amax(amax, m);
+    __syncthreads();
+    float4* dst = reinterpret_cast<float4*>(rpart + (int64_t)lb * kRangeSlots * H);
+    for (int c = threadIdx.x; c < kRangeSlots * H4; c += 256) {
+        const int q = c / H4, cc = c % H4;
+        const float4 a0 = racc[0][q][cc], a1 = racc[1][q][cc], a2 = racc[2][q][cc], a3 = racc[3][q][cc];
+        dst[c] = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                             (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+    }
+}
+
 // Backward pass 1: partial sums over rows of g2 and g2*xhat per channel.
 // Thread layout: H4 = H/4 threads per row, 256/H4 rows per step.
 __global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict__ g, const float* __restrict__ o,
@@ -342,15 +425,16 @@ __global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict_
 // Backward pass 2: one wave per row (H <= 512, NV float4 per lane). RELU = false: the layer
 // is the bare SAGEConv(normalize=True) of the per-op path (g is dL/do; no ReLU mask, no BN,
 // no dropout), i.e. only the L2-normalize backward.
-template <int NV, bool RELU = true>
-__global__ __launch_bounds__(256) void k_sage_bwd_rows(
+template <int NV, bool RELU = true, bool RANGES = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sage_bwd_rows(
     const float* __restrict__ g, const float* __restrict__ o, const float* __restrict__ nrm,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sum_g2,
     const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
     int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
     float* __restrict__ gskip, float* __restrict__ part, uint32_t* __restrict__ amax, int nt,
-    const int32_t* __restrict__ w_rowptr, int w_mode, int rev) {
+    const int32_t* __restrict__ w_rowptr, int w_mode, int rev, const int32_t* __restrict__ ranges,
+    const int32_t* __restrict__ rw_rowptr, float* __restrict__ rpart) {
     const int lane = threadIdx.x & 63;
     uint32_t tmax = 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -392,6 +476,20 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
     for (int v = 0; v < NV; ++v)
 #pragma unroll
         for (int k = 0; k < 4; ++k) db[v][k] = dw[v][k] = 0.f;
+    // end-of-block reductions; RANGES: first each wave's own sums of rw * dh per range slot
+    // (ranges.h; the transposed aggregation of range rows: a super node's dz_l row; rw = 1 or
+    // 1 / max(deg_fwd, 1)), kept in LDS rather than registers (the slot is wave-uniform; a register
+    // array per slot would cost this kernel a wave per SIMD)
+    __shared__ __attribute__((aligned(16))) float red[4][RANGES ? kRangeSlots : 2][512];
+    BlockRanges br;
+    if constexpr (RANGES) {
+        br.load(ranges, r0, r1);
+#pragma unroll
+        for (int q = 0; q < kRangeSlots; ++q)
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (cok[v]) *reinterpret_cast<float4*>(&red[wave][q][cpos[v]]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 
     // the next row's g and o rows are loaded one row ahead (two rows in flight per wave: the
     // kernel is latency-bound on these loads, not bandwidth-bound); same rows, same order
@@ -466,6 +564,15 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
             const int32_t d = w_rowptr[r + 1] - w_rowptr[r];
             wr = (w_mode == 1) ? (float)d : (d > 0 ? 1.f : 0.f);
         }
+        int sl = -1;
+        float rw = 1.f;
+        if constexpr (RANGES) {
+            sl = br.slot(r);
+            if (rw_rowptr) {   // (spmm.hip inv_deg: the MEAN transposed weight)
+                const int32_t d = rw_rowptr[r + 1] - rw_rowptr[r];
+                rw = __frcp_rn((float)(d > 0 ? d : 1));
+            }
+        }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if (!cok[v]) continue;
@@ -477,13 +584,32 @@ __global__ __launch_bounds__(256) void k_sage_bwd_rows(
                 dw[v][k] = fmaf(wr, out[k], dw[v][k]);
                 tmax = max(tmax, __float_as_uint(out[k]) & 0x7fffffffu);
             }
+            if constexpr (RANGES) {
+                if (sl >= 0) {
+                    float4* a = reinterpret_cast<float4*>(&red[wave][sl][cpos[v]]);
+                    float4 t = *a;
+                    t.x += rw_rowptr ? __fmul_rn(out[0], rw) : out[0];
+                    t.y += rw_rowptr ? __fmul_rn(out[1], rw) : out[1];
+                    t.z += rw_rowptr ? __fmul_rn(out[2], rw) : out[2];
+                    t.w += rw_rowptr ? __fmul_rn(out[3], rw) : out[3];
+                    *a = t;
+                }
+            }
             store4(dh + r * lddh + cpos[v], out[0], out[1], out[2], out[3], nt);
             if (skip)
                 store4(gskip + r * H + cpos[v], g1v[v][0], g1v[v][1], g1v[v][2], g1v[v][3], nt);
         }
     }
     if (amax) block_amax(amax, tmax);
-    __shared__ __attribute__((aligned(16))) float red[4][2][512];
+    if constexpr (RANGES) {   // the range slots first; then the same LDS for db / dw
+        __syncthreads();
+        float* rd = rpart + (int64_t)lb * kRangeSlots * H;
+        for (int c = threadIdx.x; c < kRangeSlots * H; c += 256) {
+            const int q = c / H, cc = c % H;
+            rd[c] = (red[0][q][cc] + red[1][q][cc]) + (red[2][q][cc] + red[3][q][cc]);
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v)
         if (cok[v])
@@ -749,15 +875,33 @@ extern "C" int bgnn_bn_eval_coeffs(int32_t H, const float* gamma, const float* b
 
 extern "C" int bgnn_sage_apply(const float* o, const float* scale, const float* shift, const float* x_prev,
                                int32_t skip, float p, uint64_t seed, int64_t n_rows, int32_t H, float* x_next,
-                               float* amax, void* stream) {
+                               float* amax, const int32_t* ranges, float* range_partial, void* stream) {
     BGNN_REQUIRE(H > 0 && H % 4 == 0, "sage_apply: H must be a multiple of 4");
     BGNN_REQUIRE(p >= 0.f && p < 1.f, "sage_apply: dropout p must be in [0, 1)");
     BGNN_REQUIRE((scale == nullptr) == (shift == nullptr), "sage_apply: scale/shift must both be set or NULL");
     BGNN_REQUIRE(!skip || x_prev, "sage_apply: skip requires x_prev");
     BGNN_REQUIRE(al16(o) && al16(x_next) && (!x_prev || al16(x_prev)) && (!scale || (al16(scale) && al16(shift))),
                  "sage_apply: pointers must be 16-byte aligned");
+    BGNN_REQUIRE(!ranges || (range_partial && ((uintptr_t)range_partial & 15) == 0 && H <= 512),
+                 "sage_apply: ranges need a 16-B aligned range_partial and H <= 512");
     if (n_rows == 0) return BGNN_OK;
     hipStream_t s = as_stream(stream);
+    if (ranges) {   // row-blocked form with the range partials (the same x_next)
+        const uint32_t thr = dropout_threshold(p);
+        const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
+        int64_t rpb = 0;
+        const int64_t blocks = rows_slots_of(n_rows, &rpb);
+        if (H > 256)
+            hipLaunchKernelGGL(k_sage_apply_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, o, scale, shift, x_prev,
+                               skip, thr, inv_keep, seed, n_rows, H, rpb, x_next, reinterpret_cast<uint32_t*>(amax),
+                               rows_nt(), ranges, range_partial);
+        else
+            hipLaunchKernelGGL(k_sage_apply_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, o, scale, shift, x_prev,
+                               skip, thr, inv_keep, seed, n_rows, H, rpb, x_next, reinterpret_cast<uint32_t*>(amax),
+                               rows_nt(), ranges, range_partial);
+        BGNN_CHECK_LAUNCH();
+        return BGNN_OK;
+    }
     const int64_t n4 = n_rows * (H / 4);
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -800,6 +944,7 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
                                   const float* sum_g2, const float* sum_g2xhat, float p, uint64_t seed,
                                   int32_t skip, int64_t n_rows, int32_t H, float* dh, int64_t lddh, float* gskip,
                                   float* partial_db, float* amax, const int32_t* w_rowptr, int32_t w_mode,
+                                  const int32_t* ranges, const int32_t* range_w_rowptr, float* range_partial,
                                   void* stream) {
     BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 512, "sage_bwd_rows: H=%d unsupported", H);
     BGNN_REQUIRE(w_mode >= 0 && w_mode <= 2 && (w_mode == 0 || w_rowptr), "sage_bwd_rows: bad row weights");
@@ -808,19 +953,25 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
     BGNN_REQUIRE(!mean || (invstd && sum_g2 && sum_g2xhat), "sage_bwd_rows: BN stats incomplete");
     BGNN_REQUIRE(al16(g) && al16(o) && al16(dh) && (!gskip || al16(gskip)) && al16(partial_db),
                  "sage_bwd_rows: pointers must be 16-byte aligned");
+    BGNN_REQUIRE(!ranges || (range_partial && al16(range_partial)), "sage_bwd_rows: ranges need range_partial");
     hipStream_t s = as_stream(stream);
     int64_t rpb = 0;
     const int64_t blocks = rows_grid(n_rows, 4, &rpb);
     const uint32_t thr = dropout_threshold(p);
     const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
-    if (H > 256)
-        hipLaunchKernelGGL(k_sage_bwd_rows<2>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
-                           gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode, rows_rev() & 1);
-    else
-        hipLaunchKernelGGL(k_sage_bwd_rows<1>, dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale, shift,
-                           gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb, dh,
-                           lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode, rows_rev() & 1);
+#define BGNN_ROWS(NV, R)                                                                                              \
+    hipLaunchKernelGGL((k_sage_bwd_rows<NV, true, R>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale,    \
+                       shift, gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb,    \
+                       dh, lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode,  \
+                       rows_rev() & 1, ranges, range_w_rowptr, range_partial)
+    if (ranges) {
+        if (H > 256) BGNN_ROWS(2, true);
+        else BGNN_ROWS(1, true);
+    } else {
+        if (H > 256) BGNN_ROWS(2, false);
+        else BGNN_ROWS(1, false);
+    }
+#undef BGNN_ROWS
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
@@ -842,12 +993,12 @@ extern "C" int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm,
         hipLaunchKernelGGL((k_sage_bwd_rows<2, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
                            rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
-                           0, rows_rev() & 1);
+                           0, rows_rev() & 1, nullptr, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_sage_bwd_rows<1, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
                            rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
-                           0, rows_rev() & 1);
+                           0, rows_rev() & 1, nullptr, nullptr, nullptr);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }

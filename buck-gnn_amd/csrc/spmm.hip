@@ -73,7 +73,20 @@ struct SegArgs {
     int64_t n_groups;
     int32_t group_rows;
     int32_t rev;            // row-group kernel: each eighth's groups swept from its last one down
+    // range rows (ranges.hip): hfirst[h] >= 0 marks heavy row h as a range row; with hagg its
+    // aggregate is row h of hagg (the forward), with hdone its output row is already written (the
+    // transpose); ranges_all: every heavy row is one (host-known)
+    const int32_t* hfirst;
+    const float* hagg;
+    int64_t ld_hagg;
+    int32_t hdone;
+    int32_t ranges_all;
 };
+
+// heavy row h takes the range path in this launch
+__device__ __forceinline__ bool range_row(const SegArgs& A, int32_t h) {
+    return A.hfirst != nullptr && (A.hagg != nullptr || A.hdone) && A.hfirst[h] >= 0;
+}
 
 // fold a lane's running max |out| into *amax: wave max, then one atomic per wave
 __device__ __forceinline__ void amax_flush_wave(uint32_t* amax, uint32_t m) {
@@ -447,6 +460,7 @@ __global__ __launch_bounds__(256) void k_seg_chunk(SegArgs A) {
     bool cok[NV];
     lane_cols<VEC, NV, LPR>(cb, lir, A.H, cpos, cok);
     const int32_t h = A.chunk_heavy[c];
+    if (range_row(A, h)) return;   // (wave-uniform) summed by the row passes instead
     const int32_t r = A.heavy_row[h];
     const int32_t k = (int32_t)(c - A.heavy_chunk0[h]);
     const int32_t beg = A.rowptr[r] + k * A.chunk;
@@ -481,6 +495,8 @@ __global__ __launch_bounds__(1024) void k_seg_combine(SegArgs A) {
     const int wave = threadIdx.x >> 6;
     const int h = blockIdx.x;
     if (h >= A.n_heavy) return;   // uniform over the block
+    const bool rng = range_row(A, h);
+    if (rng && !A.hagg) return;   // the transpose's range row: written by bgnn_range_sums_finish
     const bool act = (lane / LPR == 0) && wave < W;
     const int cb = blockIdx.y * TW;
     const int lir = lane % LPR;
@@ -494,7 +510,16 @@ __global__ __launch_bounds__(1024) void k_seg_combine(SegArgs A) {
     const int32_t qa = min(c1, c0 + wave * per), qb = min(c1, qa + per);
     Acc<VEC, NV, OP> acc;
     acc.init();
-    if (act) {
+    if (rng) {   // the forward's range row: its aggregate is given (row h of hagg)
+        if (wave != 0 || !act) return;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            if (!cok[v]) continue;
+            const Vec<VEC> p = ld<VEC>(A.hagg + (int64_t)h * A.ld_hagg + cpos[v]);
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) acc.a[v][q] = p.f[q];
+        }
+    } else if (act) {
 #pragma unroll 8
         for (int32_t c = qa; c < qb; ++c) {
 #pragma unroll
@@ -517,7 +542,7 @@ __global__ __launch_bounds__(1024) void k_seg_combine(SegArgs A) {
             }
         }
     }
-    if constexpr (W > 1) {
+    if (W > 1 && !rng) {
         if (act) {
 #pragma unroll
             for (int v = 0; v < NV; ++v)
@@ -1132,14 +1157,21 @@ int launch_all(SegArgs A, int ctiles, int max_blocks, hipStream_t s, int64_t* bl
     if (A.n_chunks > 0) {
         HeavyEv* ev = heavy_ev_next(g_heavy_dir == 0);
         if (ev) (void)hipEventRecord(ev->a, s);
+        // every heavy row a range row (host-known): no chunks to reduce; the transpose's range
+        // rows are written already (no combine either), the forward's combine applies the epilogue
+        const bool all_range = A.ranges_all && A.hfirst && (A.hagg || A.hdone);
         constexpr int COP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MAXT ? OP_MAXT : (OP == OP_MEANT ? OP_MEANT : OP_SUM));
-        hipLaunchKernelGGL((k_seg_chunk<VEC, NV, LPR, COP>), dim3((A.n_chunks + 3) / 4, ctiles), dim3(256), 0, s,
-                           A);
-        BGNN_CHECK_LAUNCH();
+        if (!all_range) {
+            hipLaunchKernelGGL((k_seg_chunk<VEC, NV, LPR, COP>), dim3((A.n_chunks + 3) / 4, ctiles), dim3(256), 0, s,
+                               A);
+            BGNN_CHECK_LAUNCH();
+        }
         constexpr int MOP = (OP == OP_MAX) ? OP_MAX : (OP == OP_MEAN ? OP_MEAN : OP_SUM);
-        hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles),
-                           dim3(MOP == OP_MAX ? 256 : 64 * kCombineWaves), 0, s, A);
-        BGNN_CHECK_LAUNCH();
+        if (!(all_range && A.hdone)) {
+            hipLaunchKernelGGL((k_seg_combine<VEC, NV, LPR, MOP, EPI>), dim3(A.n_heavy, ctiles),
+                               dim3(MOP == OP_MAX ? 256 : 64 * kCombineWaves), 0, s, A);
+            BGNN_CHECK_LAUNCH();
+        }
         if (ev) (void)hipEventRecord(ev->b, s);
     }
     return BGNN_OK;
@@ -1192,6 +1224,10 @@ inline SegArgs args_from_csr(const bgnn_csr_t* c) {
         A.grow = c->grow;
         A.n_groups = c->grow ? c->n_groups : (c->n_rows + c->group_rows - 1) / c->group_rows;
     }
+    if (c->ranges && c->n_heavy > 0) {
+        A.hfirst = c->ranges + 2 + 3 * c->n_heavy;
+        A.ranges_all = c->ranges_all;
+    }
     return A;
 }
 
@@ -1240,14 +1276,15 @@ extern "C" int bgnn_spmm_fwd(const bgnn_csr_t* csr, const float* x, int64_t ldx,
 static int spmm_bwd_impl(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                          int64_t fwd_rows, const float* g, int64_t ldg, int32_t H, int32_t reduce, const void* arg,
                          const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial, float* amax,
-                         void* stream);
+                         int heavy_done, void* stream);
 
 extern "C" int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                              const float* g, int64_t ldg, int32_t H, int32_t reduce, float* gx, int64_t ldgx,
-                             float* partial, float* amax, void* stream) {
+                             float* partial, float* amax, int32_t heavy_done, void* stream) {
     BGNN_REQUIRE(reduce != BGNN_REDUCE_MAX, "spmm_bwd: max aggregation takes bgnn_spmm_bwd_max");
-    return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, 0, g, ldg, H, reduce, nullptr, nullptr, 0, gx, ldgx, partial, amax,
-                         stream);
+    BGNN_REQUIRE(!heavy_done || (csr_t && csr_t->ranges), "spmm_bwd: heavy_done needs the CSR's ranges");
+    return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, 0, g, ldg, H, reduce, nullptr, nullptr, 0, gx, ldgx, partial,
+                         amax, heavy_done ? 1 : 0, stream);
 }
 
 extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
@@ -1255,7 +1292,7 @@ extern "C" int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t,
                                  int64_t ld_add, float* gx, int64_t ldgx, float* partial, float* amax, void* stream) {
     BGNN_REQUIRE(reduce != BGNN_REDUCE_MAX, "spmm_bwd_add: max aggregation takes bgnn_spmm_bwd_max");
     return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, 0, g, ldg, H, reduce, nullptr, addend, ld_add, gx, ldgx, partial,
-                         amax, stream);
+                         amax, 0, stream);
 }
 
 extern "C" int bgnn_spmm_bwd_max(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
@@ -1264,13 +1301,13 @@ extern "C" int bgnn_spmm_bwd_max(const bgnn_csr_t* csr_t, const int32_t* perm_t,
                                  float* amax, void* stream) {
     BGNN_REQUIRE(perm_t && fwd_rowptr && arg && fwd_rows >= 0, "spmm_bwd_max: perm_t, fwd_rowptr and arg required");
     return spmm_bwd_impl(csr_t, perm_t, fwd_rowptr, fwd_rows, g, ldg, H, BGNN_REDUCE_MAX, arg, addend, ld_add, gx, ldgx,
-                         partial, amax, stream);
+                         partial, amax, 0, stream);
 }
 
 static int spmm_bwd_impl(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                          int64_t fwd_rows, const float* g, int64_t ldg, int32_t H, int32_t reduce, const void* arg,
                          const float* addend, int64_t ld_add, float* gx, int64_t ldgx, float* partial, float* amax,
-                         void* stream) {
+                         int heavy_done, void* stream) {
     BGNN_REQUIRE(csr_t && csr_t->rowptr, "spmm_bwd: null csr");
     BGNN_REQUIRE(!addend || ld_add >= H, "spmm_bwd: bad ld_add");
     BGNN_REQUIRE(H > 0 && ldg >= H && ldgx >= H, "spmm_bwd: bad H/ld");
@@ -1292,6 +1329,7 @@ static int spmm_bwd_impl(const bgnn_csr_t* csr_t, const int32_t* perm_t, const i
     A.amax = reinterpret_cast<uint32_t*>(amax);
     A.add = addend;
     A.ld_add = ld_add;
+    A.hdone = heavy_done;
     const bool al = aligned16(g) && aligned16(gx) && ldg % 4 == 0 && ldgx % 4 == 0 &&
                     (!partial || aligned16(partial)) && (!arg || aligned16(arg)) &&
                     (!addend || (aligned16(addend) && ld_add % 4 == 0));
@@ -1360,7 +1398,7 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
 
 extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldzl, const float* zr, int64_t ldzr,
                              const float* bias, int32_t H, int32_t reduce, float* o, float* nrm, float* bn_partial,
-                             float* partial, void* stream) {
+                             float* partial, const float* heavy_agg, int64_t ld_heavy_agg, void* stream) {
     BGNN_REQUIRE(csr && csr->rowptr, "sage_fwd: null csr");
     BGNN_REQUIRE(H > 0 && H <= 512 && H % 4 == 0, "sage_fwd: H=%d unsupported (need H%%4==0, H<=512)", H);
     BGNN_REQUIRE(ldzl >= H && ldzl % 4 == 0 && ldzr >= H && ldzr % 4 == 0,
@@ -1380,6 +1418,12 @@ extern "C" int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldz
     A.nrm = nrm;
     A.bn_partial = bn_partial;
     A.partial = partial;
+    if (heavy_agg) {
+        BGNN_REQUIRE(csr->ranges && aligned16(heavy_agg) && ld_heavy_agg >= H && ld_heavy_agg % 4 == 0,
+                     "sage_fwd: heavy_agg needs the CSR's ranges, 16-B alignment and ld >= H");
+        A.hagg = heavy_agg;
+        A.ld_hagg = ld_heavy_agg;
+    }
     hipStream_t s = as_stream(stream);
     int64_t blocks = 0;
     if (H > 256) {

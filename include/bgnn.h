@@ -114,7 +114,8 @@ typedef struct bgnn_csr {
     int32_t n_heavy;
     int32_t n_chunks;
     int32_t chunk;               /* edges per chunk; rows with deg > chunk are heavy */
-    int32_t _pad;
+    int32_t ranges_all;          /* 1: every heavy row is a range row (host-known; chunk launches
+                                    skipped when the range path covers them), else 0 */
     /* Optional row-group plan (bgnn_group_plan; all NULL / 0 = none). Used by the sum/mean
      * aggregation kernels: a wave reduces up to `group_rows` consecutive rows and fetches each
      * distinct source row of the group once. */
@@ -125,6 +126,14 @@ typedef struct bgnn_csr {
     int64_t n_groups;            /* with grow; else ceil(n_rows / group_rows)  */
     int32_t group_rows;
     int32_t _pad2;
+    /* Optional (round 6, ABI 12): the heavy rows' source ranges, bgnn_heavy_ranges' output for
+     * this CSR, or NULL. A "range row" is a heavy row whose entries are exactly the contiguous
+     * increasing run [a, a + deg) -- the super node of VirtualEdgeCreate.py:106-111 over its
+     * graph's real nodes (GraphCreate.py:417-422 emits both directions, so its transposed row is
+     * one too). Its aggregation is a column sum over that row range, which bgnn_sage_apply /
+     * bgnn_sage_bwd_rows accumulate as a by-product (range partials) and
+     * bgnn_range_sums_finish completes; bgnn_sage_fwd / bgnn_spmm_bwd then skip its chunks. */
+    const int32_t* ranges;
 } bgnn_csr_t;
 
 /* Workspace for bgnn_graph_build (bytes). */
@@ -158,6 +167,35 @@ size_t bgnn_heavy_plan_ws_bytes(int64_t n_rows);
 int bgnn_heavy_plan(const int32_t* rowptr, int64_t n_rows, int64_t nnz, int32_t chunk,
                     int32_t* heavy_row, int32_t* heavy_chunk0, int32_t* chunk_heavy,
                     int32_t* dev_counts, void* ws, size_t ws_bytes, void* stream);
+
+/* Heavy-row ranges (round 6). ranges = int32 [bgnn_heavy_ranges_bytes(n_heavy) / 4]:
+ *   [0] = n_valid, [1] = n_heavy,
+ *   [2 + 3k .. 2 + 3k + 2] = (first, end, heavy index) of the k-th range row, k < n_valid, in
+ *                            increasing row order: a heavy row whose columns are one increasing
+ *                            run is kept when its run starts at or after the end of every earlier
+ *                            such row's run (so the kept ranges are sorted and disjoint); the
+ *                            others are left to the chunk path,
+ *   [2 + 3 n_heavy + h]    = first source row of heavy row h's range, or -1 (chunk path).
+ * Asynchronous (two launches); n_heavy is csr->n_heavy. */
+size_t bgnn_heavy_ranges_bytes(int32_t n_heavy);
+int bgnn_heavy_ranges(const bgnn_csr_t* csr, int32_t* ranges, void* stream);
+
+/* Range partials -> range row sums. bgnn_sage_apply / bgnn_sage_bwd_rows (given a `ranges` buffer)
+ * write, per block b of bgnn_rows_slots(n_rows) row blocks (rows [b rpb, (b+1) rpb), rpb =
+ * ceil(n_rows / slots)) and for the up to 3 range rows whose ranges meet the block, the column sums
+ * of their rows' outputs: range_partial [slots][3][H] (bgnn_range_partial_bytes). The block's
+ * ranges are those with end > b rpb, taken in order; the finish sums each range's block partials
+ * in block order (deterministic):
+ *   mode 0: out[h, :]               = sum (the forward: the range sums of x_next, which the next
+ *                                     layer's GEMM turns into the heavy rows' aggregates)
+ *   mode 1: out[heavy_row[h], :]    = sum (the backward: a super node's dz_l row)
+ * for each range row h of `csr`; mode 0 also zeroes row h of every heavy row left to the chunk path
+ * (its GEMM row is computed but unused); amax (optional): *amax = max(*amax, *amax_floor, max |sum|).
+ * Requires rpb <= 2 (chunk + 1) (every range spans more than chunk rows). */
+size_t bgnn_range_partial_bytes(int64_t n_rows, int32_t H);
+int bgnn_range_sums_finish(const float* range_partial, int64_t n_rows, int32_t H, const bgnn_csr_t* csr,
+                           int32_t mode, float* out, int64_t ldo, const float* amax_floor, float* amax,
+                           void* stream);
 
 /* Row-group plan of a CSR (R = group_rows <= 8, chunk <= 64). Group g = rows
  * [grow[g], grow[g+1]) (at most R rows; grow = NULL: rows [g*R, g*R+R), n_groups =
@@ -201,7 +239,10 @@ size_t bgnn_spmm_max_arg_bytes(int64_t n_rows, int32_t H, int32_t n_heavy);
  * GEMMs that consume gx (bgnn_gemm_f32_scaled). MAX takes bgnn_spmm_bwd_max. */
 int bgnn_spmm_bwd(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
                   const float* g, int64_t ldg, int32_t H, int32_t reduce,
-                  float* gx, int64_t ldgx, float* partial, float* amax, void* stream);
+                  float* gx, int64_t ldgx, float* partial, float* amax, int32_t heavy_done, void* stream);
+/* heavy_done = 1 (with csr_t->ranges): the range rows' gx rows were already written (and folded
+ * into amax) by bgnn_range_sums_finish (mode 1, from bgnn_sage_bwd_rows' range partials), so
+ * their chunks and combine are skipped. */
 /* bgnn_spmm_bwd with an addend: gx[j] = (A^T g)[j] + addend[j] (addend [rows, H], ld ld_add),
  * added after the reduction, in the same pass. */
 int bgnn_spmm_bwd_add(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int32_t* fwd_rowptr,
@@ -231,7 +272,11 @@ int bgnn_spmm_bwd_max(const bgnn_csr_t* csr_t, const int32_t* perm_t, const int3
 int32_t bgnn_sage_fwd_slots(const bgnn_csr_t* csr);
 int bgnn_sage_fwd(const bgnn_csr_t* csr, const float* zl, int64_t ldzl, const float* zr, int64_t ldzr,
                   const float* bias, int32_t H, int32_t reduce, float* o, float* nrm,
-                  float* bn_partial, float* partial, void* stream);
+                  float* bn_partial, float* partial, const float* heavy_agg, int64_t ld_heavy_agg,
+                  void* stream);
+/* heavy_agg (optional, with csr->ranges): row h = the summed z_l rows of range row h (the GEMM of
+ * the layer's input range sums: (sum_j x_j) W_l^T = sum_j z_l[j]); the range rows' epilogue takes
+ * it in place of their chunk sums (MEAN divides by the degree as for every row). */
 
 /* BatchNorm1d finalize (train): sums the partials in fp64, writes
  *   mean[H], invstd[H], scale = gamma*invstd, shift = beta - mean*scale,
@@ -253,7 +298,11 @@ int bgnn_bn_eval_coeffs(int32_t H, const float* gamma, const float* beta, float 
  * amax (optional): *amax = max(*amax, max |x_next|) (next layer's GEMM operand scale). */
 int bgnn_sage_apply(const float* o, const float* scale, const float* shift,
                     const float* x_prev, int32_t skip, float p, uint64_t seed,
-                    int64_t n_rows, int32_t H, float* x_next, float* amax, void* stream);
+                    int64_t n_rows, int32_t H, float* x_next, float* amax,
+                    const int32_t* ranges, float* range_partial, void* stream);
+/* ranges (optional, the next layer's forward-CSR bgnn_heavy_ranges buffer): also the range
+ * partials of x_next (bgnn_range_partial_bytes; finish with bgnn_range_sums_finish mode 0), by a
+ * row-blocked form of the same element-wise pass (the same x_next bits). */
 
 /* Backward pass 1: BatchNorm statistics of the incoming gradient g (= dL/dx_next):
  *   g2 = relu'(o*scale+shift) * dropout'(g);  partial sums of g2 and g2*xhat. */
@@ -300,7 +349,11 @@ int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
                        float p, uint64_t seed, int32_t skip,
                        int64_t n_rows, int32_t H, float* dh, int64_t lddh,
                        float* gskip, float* partial_db, float* amax,
-                       const int32_t* w_rowptr, int32_t w_mode, void* stream);
+                       const int32_t* w_rowptr, int32_t w_mode, const int32_t* ranges,
+                       const int32_t* range_w_rowptr, float* range_partial, void* stream);
+/* ranges (optional, the transpose CSR's bgnn_heavy_ranges buffer): also the range partials of
+ * w_r dh_r (w_r = 1, or 1 / max(deg, 1) with deg from range_w_rowptr -- the forward rowptr, MEAN's
+ * transposed weights), finished with bgnn_range_sums_finish mode 1 into the super nodes' dz_l rows. */
 
 /* The L2-normalize backward of SAGEConv(normalize=True) alone (ABI 5): the per-module
  * SAGEConv of the PyG surface (bgnn.nn.SAGEConv, called by the reference's unchanged

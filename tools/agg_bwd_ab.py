@@ -50,7 +50,7 @@ def main():
 
     def sage_fwd():
         _lib.call("bgnn_sage_fwd", g.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H, bias.data_ptr(), H,
-                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
+                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), None, 0, s)
 
     def plain_fwd():
         _lib.call("bgnn_spmm_fwd", g.fwd.ref(), z.data_ptr(), 2 * H, H, 0, out_dense.data_ptr(), H, None,
@@ -59,7 +59,7 @@ def main():
     def bwd(csr, src, ld_src, dst, ld_dst):
         def f():
             _lib.call("bgnn_spmm_bwd", csr.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), src.data_ptr(),
-                      ld_src, H, 0, dst.data_ptr(), ld_dst, part.data_ptr(), None, s)
+                      ld_src, H, 0, dst.data_ptr(), ld_dst, part.data_ptr(), None, 0, s)
         return f
 
     def nt0(f):

@@ -109,12 +109,12 @@ def main():
 
     def sage_fwd():
         _lib.call("bgnn_sage_fwd", g.fwd.ref(), z.data_ptr(), 2 * H, z[:, H:].data_ptr(), 2 * H, bias.data_ptr(), H,
-                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
+                  0, o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), None, 0, s)
         return o
 
     def bwd_t():
         _lib.call("bgnn_spmm_bwd", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), dz[:, H:].data_ptr(),
-                  2 * H, H, 0, dz.data_ptr(), 2 * H, part.data_ptr(), None, s)
+                  2 * H, H, 0, dz.data_ptr(), 2 * H, part.data_ptr(), None, 0, s)
         return dz[:, :H]
 
     def apply(setting, undo=None):

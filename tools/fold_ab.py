@@ -160,3 +160,106 @@ def relu_flips(name="GraphSage_addAggr_Shared"):
 
 if __name__ == "__main__" and os.environ.get("FOLD_FLIPS"):
     relu_flips()
+
+
+def m16_bisect(name="GraphSage_addAggr_Shared"):
+    """Which GEMM call of the folded path moves its gradients when it runs on 16x16x32 MFMAs: with
+    the product library (4-wave 128x128 tile = 32x32x16, 8-wave tiles = 16x16x32), force the 8-wave
+    256x128 tile (bgnn_gemm_set_cfg 1) for one group of fused.gemm calls at a time, identified by
+    (M, N, K, trans_a, trans_b), and report the gradients' mean / max relative error against fp64.
+    The folded layer's calls at the test batch (4 x 24x24 meshes, N = 2304 rows, H = 512,
+    K_in = 128): fwd_fold z = h Wf^T + bf; dgrad_fold dh = dz Wf; wgrad_fold dWf = dz^T h; and the
+    weight products wf, bf, dw, dw_in, db_in."""
+    from bgnn import _lib
+    dev = torch.device("cuda", 0)
+    orig = fused.gemm
+    N, H, K = 2304, 512, 128
+    groups = {"none": set(),
+              "fwd_fold": {(N, 2 * H, K, False, True)}, "dgrad_fold": {(N, K, 2 * H, False, True)},
+              "wgrad_fold": {(2 * H, K, N, True, False)},
+              "wf": {(2 * H, K, H, False, False)}, "bf": {(2 * H, 1, H, False, False)},
+              "dw": {(2 * H, H, K, False, True)}, "dw_in": {(H, K, 2 * H, True, False)},
+              "db_in": {(H, 1, 2 * H, True, False)}}
+    groups["all"] = set().union(*groups.values())
+    seen = set()
+
+    def make(route):
+        def g(a, b, trans_a, trans_b, **kw):
+            M = a.size(1) if trans_a else a.size(0)
+            Kd = a.size(0) if trans_a else a.size(1)
+            Nn = b.size(0) if trans_b else b.size(1)
+            key = (M, Nn, Kd, bool(trans_a), bool(trans_b))
+            seen.add(key)
+            if key in route:
+                _lib.call("bgnn_gemm_set_cfg", 1)
+                try:
+                    return orig(a, b, trans_a, trans_b, **kw)
+                finally:
+                    _lib.call("bgnn_gemm_set_cfg", -1)
+            return orig(a, b, trans_a, trans_b, **kw)
+        return g
+    fused.FOLD_WEIGHTS_TORCH = False
+    out = {}
+    for gname, route in groups.items():
+        fused.gemm = make(route)
+        b, sd, _, g = T.run(dev, name, 512, True)
+        out[gname] = g
+    fused.gemm = orig
+    exact = T.oracle_grads(b, sd, name)
+    print("fused.gemm calls seen (M, N, K, ta, tb):", sorted(seen))
+    for gname, g in out.items():
+        errs = [T.rel_err(g[k], exact[k]) for k in exact]
+        print(f"16x16x32 for {gname:10s}: mean rel err {sum(errs) / len(errs):.2e} max {max(errs):.2e}", flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("FOLD_M16_BISECT"):
+    m16_bisect()
+
+
+def global_cfg(name="GraphSage_addAggr_Shared"):
+    """Folded and unfolded gradients against fp64 (mean / max relative error over parameters) with
+    every bgnn GEMM of the step on its planned tile (-1: the 4-wave 128x128 tile of these N = 2304
+    shapes runs 32x32x16 MFMAs) or forced onto the 8-wave 256x128 tile (1: 16x16x32 MFMAs), for
+    three weight seeds: whether a change of MFMA shape moves the folded path's error systematically
+    or only reshuffles which rounding-sensitive elements the comparison meets."""
+    import bgnn
+    from bgnn import _lib, buckgnn
+    from bgnn import synthetic as S
+    dev = torch.device("cuda", 0)
+    b = S.make_batch(24, 4)
+
+    def run(seed, fold):
+        torch.manual_seed(seed)
+        m = bgnn.BuckGNN(16, 5, hidden_channels=512, num_layers=6, dropout_rate=0.0, model_name=name)
+        sd = {k: v.clone() for k, v in m.state_dict().items()}
+        m = m.to(dev).train()
+        old = buckgnn.FOLD_ENCODER
+        buckgnn.FOLD_ENCODER = fold
+        try:
+            bd = b.to(dev)
+            pred, _ = m(bd.x, bd.edge_index, bd.edge_attr, bd.batch)
+            bgnn.RelativeErrorLoss()(pred, bd.y).backward()
+        finally:
+            buckgnn.FOLD_ENCODER = old
+        return sd, {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    for seed in (0, 1, 2):
+        exact = None
+        for cfg in (-1, 1):
+            _lib.call("bgnn_gemm_set_cfg", cfg)
+            try:
+                res = {f: run(seed, f) for f in (False, True)}
+            finally:
+                _lib.call("bgnn_gemm_set_cfg", -1)
+            if exact is None:
+                exact = T.oracle_grads(b, res[False][0], name)
+            line = []
+            for f in (False, True):
+                errs = [T.rel_err(res[f][1][k], exact[k]) for k in exact]
+                line.append(f"{'folded' if f else 'unfolded'} mean {sum(errs) / len(errs):.2e} max {max(errs):.2e}")
+            print(f"seed {seed} gemm cfg {cfg:2d} ({'32x32x16' if cfg < 0 else '16x16x32'} at N = 2304): "
+                  + " | ".join(line), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("FOLD_GLOBAL_CFG"):
+    global_cfg()

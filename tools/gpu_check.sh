@@ -44,7 +44,7 @@ bench() {   # bench NAME SECONDS ARGS...
 prof() {   # prof NAME SECONDS ARGS...
   local name=$1 secs=$2; shift 2
   (cd /tmp && timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats --output-format csv \
-     -d "$ROOT/gpurun_out/prof_${name}_$TAG" -o run -- python "$ROOT/bench.py" "$@" \
+     -d "$ROOT/gpurun_out/prof_${name}_$TAG" -o run -- python "$ROOT/bench.py" "$@" ${BENCH_ARGS:-} \
      > "$ROOT/gpurun_out/prof_bench_${name}_$TAG.json" 2>&1) || die "prof_$name" $?
 }
 

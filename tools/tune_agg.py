@@ -92,7 +92,7 @@ def main():
         else:
             zl, zr, ld = zp[0], zp[1], H
         _lib.call("bgnn_sage_fwd", g.fwd.ref(), zl.data_ptr(), ld, zr.data_ptr(), ld, bias.data_ptr(), H, 0,
-                  o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), s)
+                  o.data_ptr(), nrm.data_ptr(), bnp.data_ptr(), part.data_ptr(), None, 0, s)
         e1.record()
         return (e0, e1), (o, nrm, bnp.sum(0))
 
@@ -103,7 +103,7 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         _lib.call("bgnn_spmm_bwd", g.bwd.ref(), g.perm_t.data_ptr(), g.fwd.rowptr.data_ptr(), z[:, H:].data_ptr(),
-                  z.stride(0), H, 0, gx.data_ptr(), gx.stride(0), part.data_ptr(), None, s)
+                  z.stride(0), H, 0, gx.data_ptr(), gx.stride(0), part.data_ptr(), None, 0, s)
         e1.record()
         return (e0, e1), (gx[:, :H],)
 
