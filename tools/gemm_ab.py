@@ -23,7 +23,7 @@ import torch  # noqa: E402
 from bgnn import _lib, fused  # noqa: E402
 
 SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872, 512, 512),
-          "fwd_small": (10082, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
+          "fwd_small": (10082, 1024, 512), "fwd3": (80672, 1024, 512), "fwd3r": (80688, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
 
 
 def parse(vs):
