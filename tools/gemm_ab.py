@@ -6,7 +6,8 @@ rounds. Results are checked bit-identical to the first variant.
 
     python tools/gemm_ab.py [--reps 20] [--variants=w,d,w.2] [--shapes fwd,dgrad]
 
-Variants: "xC" the register-staged kernel (bgnn_gemm_f32_scaled) on tile config C (-1 = the
+(Round 6 measured a "+e" variant here, the ragged last row tile scheduled first: no gain beyond
+the first-variant order bias, profiles/r06_gemm_edge_first_l.txt; not kept.) Variants: "xC" the register-staged kernel (bgnn_gemm_f32_scaled) on tile config C (-1 = the
 automatic plan); "w" the pre-split weight path (bgnn_gemm_wsplit + bgnn_gemm_f32_w); "d" the same
 with the drop-add epilogue (src = an [M, N] gradient, p = 0.1: the skip layers' dgrad); "w.C" /
 "d.C" on tile config C. (Round 6 measured the main-loop variants "wP" of the then knob 14 here,
@@ -23,7 +24,7 @@ import torch  # noqa: E402
 from bgnn import _lib, fused  # noqa: E402
 
 SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872, 512, 512),
-          "fwd_small": (10082, 1024, 512), "fwd3": (80672, 1024, 512), "fwd3r": (80688, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
+          "fwd_small": (10082, 1024, 512), "fwd3": (80672, 1024, 512), "fwd3r": (80688, 1024, 512), "fwd0": (80640, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
 
 
 def parse(vs):
