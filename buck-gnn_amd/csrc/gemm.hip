@@ -19,6 +19,8 @@
 
 namespace bgnn {
 
+extern int g_x6_bdma;   // gemm_x6.hip: knob 16 (BGNN_TUNE_GEMM_BDMA)
+
 // LDS row pad (floats): a K-contiguous operand is transposed by scalar ds_write_b32
 // into a [BK][R + PAD] image; PAD is chosen so one wave's 32-lane store groups hit 32
 // distinct banks (4*(R+PAD) = 8 mod 32 for BK = 16, 4 mod 32 for BK = 32). An
@@ -407,6 +409,8 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.x6 = 1;
         p.prec = 1;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
+        // knob 16 = 4: the pre-split products on the pipelined 128 x 128 kernel (gemm_h3p.hip)
+        if (wb && g_x6_bdma == 4 && g_gemm_cfg < 0 && N % 128 == 0 && K % 32 == 0) p.cfg = 0;
         // plane blocks must be whole tiles: fall back to an 8-wave tile that divides them (the
         // 16x16x32 MFMA family, the same rounding as the dense layout's), else the 128x128 tile
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) {
@@ -555,7 +559,7 @@ extern "C" int bgnn_gemm_f32_dropadd_cols(int64_t M, int64_t N, int64_t K, const
 extern "C" int32_t bgnn_gemm_w_tile(int64_t M, int64_t N, int64_t K) {
     if (gemm_mode() != 2 || M <= 0 || N <= 0 || K <= 0) return 0;
     const Plan pl = make_plan(M, N, K, 0, 1, 0, 0, 0, true);
-    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg < 1 || pl.cfg > 4) return 0;
+    if (!pl.x6 || pl.prec != 1 || pl.split != 1 || pl.cfg > 4 || (pl.cfg < 1 && g_x6_bdma != 4)) return 0;
     if (N % pl.bn != 0 || K % 32 != 0) return 0;
     return pl.bn;
 }
@@ -575,6 +579,8 @@ extern "C" int bgnn_gemm_f32_w(int64_t M, int64_t N, int64_t K, const float* A, 
     BGNN_REQUIRE(!src || (ld_src >= N && ld_src % 4 == 0 && N % 4 == 0 && ((uintptr_t)src & 15) == 0),
                  "gemm_f32_w: src must be 16-byte aligned with N and ld_src multiples of 4");
     const Plan pl = make_plan(M, N, K, 0, 1, 0, 0, 0, true);
+    BGNN_REQUIRE(pl.cfg != 0 || (lda % 4 == 0 && aligned16(A)),
+                 "gemm_f32_w: the 128 x 128 pipelined tile needs 16-byte aligned A rows");
     GemmArgs g{A, static_cast<const float*>(wimg), C, nullptr, M, N, K, lda, K, ldc, 1.f, src ? 1.f : 0.f, 0, 1,
                bias, relu, 0, 0, 0, 0, a_amax, b_amax, c_amax};
     g.kchunk = (K + pl.bk - 1) / pl.bk * pl.bk;

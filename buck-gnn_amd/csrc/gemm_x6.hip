@@ -41,6 +41,8 @@ const X6Cfg kX6Cfgs[] = {
 };
 const int kNumX6Cfgs = 5;
 
+int g_x6_bdma = 0;
+
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if (prec == 2 && g.st != 0) launch_x6_bf16_storage(ta, tb, cfg, g.st, grid, s, g);
     else if (prec == 2) launch_x6_prec2(ta, tb, cfg, grid, s, g);

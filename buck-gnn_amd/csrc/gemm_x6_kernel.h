@@ -32,6 +32,65 @@ __device__ __forceinline__ int x6_pos(int row, int chunk) {
     return row * 4 + (chunk ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3));
 }
 
+// LDS-DMA of the pre-split B image (PPV bit 3, round 6; knob BGNN_TUNE_GEMM_BDMA): address spaces
+// of __builtin_amdgcn_global_load_lds, a counted vmcnt wait, and a barrier that drains only the
+// LDS writes (a __syncthreads() would also drain every DMA and A load in flight, vmcnt(0))
+typedef __attribute__((address_space(3))) void x6_lds_t;
+typedef __attribute__((address_space(1))) void x6_gbl_t;
+template <int N>
+__device__ __forceinline__ void x6_wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void x6_barrier_lds() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+extern int g_x6_bdma;   // 1: the pre-split f16x3 GEMMs stage B by LDS-DMA, 2-4: k_gemm_h3p (gemm_x6.hip)
+struct GemmArgs;
+bool h3p_ok(int cfg, const GemmArgs& g);                                // gemm_h3p.hip
+void launch_h3p(int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
+
+// one 32-deep f16x3 slice on 16x16x32 MFMAs from restrict-scoped LDS images (the DMA path: the
+// scopes keep hipcc from draining the B slots' DMA in flight, vmcnt(0), before these reads); the
+// same fragments, products and order as k_gemm_x6's kM16 mma_slice, so the same bits
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void x6_mma16_h3(const uint4* __restrict__ As, const uint4* __restrict__ Bs,
+                                            floatx4 (&acc)[2 * (BM / WM / 32)][2 * (BN / WN / 32)], int wm, int wn,
+                                            int lane) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    const int l16 = lane & 15, lq = lane >> 4;
+    auto fa = [&](int i, int p) { return As[p * BM * 4 + x6_pos(wm * (BM / WM) + i * 16 + l16, lq)]; };
+    auto fb = [&](int j, int p) { return Bs[p * BN * 4 + x6_pos(wn * (BN / WN) + j * 16 + l16, lq)]; };
+    auto mma3 = [&](floatx4& t, const uint4 (&a)[2], const uint4 (&b)[2]) {
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[1]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[1]), as_f16x8(b[0]), t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[0]), as_f16x8(b[0]), t, 0, 0, 0);
+    };
+    if constexpr (TM <= TN) {
+        uint4 a[2 * TM][2];
+#pragma unroll
+        for (int i = 0; i < 2 * TM; ++i) { a[i][0] = fa(i, 0); a[i][1] = fa(i, 1); }
+#pragma unroll
+        for (int j = 0; j < 2 * TN; ++j) {
+            const uint4 b[2] = {fb(j, 0), fb(j, 1)};
+#pragma unroll
+            for (int i = 0; i < 2 * TM; ++i) mma3(acc[i][j], a[i], b);
+        }
+    } else {
+        uint4 b[2 * TN][2];
+#pragma unroll
+        for (int j = 0; j < 2 * TN; ++j) { b[j][0] = fb(j, 0); b[j][1] = fb(j, 1); }
+#pragma unroll
+        for (int i = 0; i < 2 * TM; ++i) {
+            const uint4 a[2] = {fa(i, 0), fa(i, 1)};
+#pragma unroll
+            for (int j = 0; j < 2 * TN; ++j) mma3(acc[i][j], a, b[j]);
+        }
+    }
+}
+
 // One staging unit = 8 consecutive k of one row r (r = m or n) of the tile.
 //   KCONTIG = 1: element (r, k) at P[r * ld + k];   unit idx -> r = idx / 4, chunk = idx % 4
 //   KCONTIG = 0: element (r, k) at P[k * ld + r];   unit idx -> r = idx % R, chunk = idx / R
@@ -300,6 +359,11 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     constexpr int AK = (TA == 0) ? 1 : 0;   // A K-contiguous?
     constexpr int BKc = (TB == 1) ? 1 : 0;  // B K-contiguous?
     constexpr bool kWB = (PPV & 4) != 0;
+    // PPV bit 3 (8, with bit 2): B's image goes global -> LDS by global_load_lds_dwordx4 into NSB
+    // slots (no VGPRs, no ds_write), issued NSB - 1 slices ahead; A keeps the register split at
+    // prefetch distance 2. Only the 16x16x32 8-wave tiles.
+    constexpr bool kDMA = (PPV & 8) != 0;
+    static_assert(!kDMA || (kWB && PREC == 1 && 64 * WM * WN == 512), "B by LDS-DMA: pre-split f16x3, 8 waves");
     // f16x3 main loops run 16x16x32 MFMAs (four per 32x32 block, one per 32-deep slice; round 5):
     // the same cycles per FLOP as 32x32x16, but the chip holds a higher clock under them (guide
     // MI355X_MICROARCH.md, DVFS item 7): isolated dgrad 274 -> 258 us, drop-add dgrad 314 -> 303,
@@ -315,7 +379,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // [buffer][piece][row][4 chunks of 8 16-bit values] for A, then for B; reused by the
     // epilogue as one [TM*32][32] f32 stage per wave
     constexpr int A_U4 = NP * BM * 4, B_U4 = NP * BN * 4;
-    constexpr int TILE_U4 = 2 * (A_U4 + B_U4), STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
+    // B slots of the DMA path: 4 where they fit beside A's two buffers, else 3
+    constexpr int NSB = (2 * A_U4 + 4 * B_U4) * 16 <= 160 * 1024 ? 4 : 3;
+    constexpr int TILE_U4 = 2 * A_U4 + (kDMA ? NSB : 2) * B_U4, STAGE_U4 = WM * WN * TM * 32 * 32 * 4 / 16;
     static_assert((TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4) * 16 <= 160 * 1024, "LDS over 160 KiB");
     __shared__ uint4 smem[TILE_U4 > STAGE_U4 ? TILE_U4 : STAGE_U4];
     uint4 (*As)[A_U4] = reinterpret_cast<uint4 (*)[A_U4]>(smem);
@@ -381,8 +447,9 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     struct RegsWB { float a[x6_nu(BM, NT)][8]; uint4 b[BN * 8 / NT]; };
     struct RegsKQ { float q[4][8]; };
     struct RegsKQ16 { uint2 q[8]; };
-    using Regs = std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ,
-                                    std::conditional_t<kWB, RegsWB, RegsStd>>>;
+    struct RegsWA { float a[x6_nu(BM, NT)][8]; };   // DMA path: A only
+    using Regs = std::conditional_t<kDMA, RegsWA, std::conditional_t<KQ16, RegsKQ16, std::conditional_t<KQ, RegsKQ,
+                                    std::conditional_t<kWB, RegsWB, RegsStd>>>>;
     Regs rs[2];
     const int64_t nk = (ke > kb) ? (ke - kb + X6_BK - 1) / X6_BK : 0;
     const bool full = a_vec && b_vec && (m0 + BM <= g.M) && (n0 + BN <= g.N) && ((ke - kb) % X6_BK == 0);
@@ -397,7 +464,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
         constexpr bool FULL = MODE == 1, KT = MODE == 2;
         auto load_ab = [&](int64_t k0, Regs& r) {
             const float* Ab = plane_base(g.A, TA ? m0 : k0, g.a_blk, g.a_pstride);
-            if constexpr (KQ16) {
+            if constexpr (kDMA) {   // (mainloop_dma)
+            } else if constexpr (KQ16) {
                 if (t < BM) kq_load16<BM, FULL>(Ab, g.lda, g.M, m0, k0, ke, a_vec, r.q, t);
                 else if (t < BM + BN) kq_load16<BN, FULL>(g.B, g.ldb, g.N, n0, k0, ke, b_vec, r.q, t - BM);
             } else if constexpr (KQ) {
@@ -415,7 +483,8 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             }
         };
         auto store_ab = [&](int buf, const Regs& r) {
-            if constexpr (KQ16) {
+            if constexpr (kDMA) {   // (mainloop_dma)
+            } else if constexpr (KQ16) {
                 if (t < BM) kq_store16<BM>(As[buf], r.q, t);
                 else if (t < BM + BN) kq_store16<BN>(Bs[buf], r.q, t - BM);
             } else if constexpr (KQ) {
@@ -523,7 +592,76 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             for (int64_t kt = 0; kt < nk; ++kt) step(kt, rs[1]);
         }
     };
-    if (full) {
+    // The DMA path (kDMA): per step, split A(kt+1) into LDS, DMA B(kt+NSB-1) into its slot, load
+    // A(kt+3), multiply slice kt, wait for this wave's part of B(kt+1) with a counted vmcnt and
+    // barrier. Same LDS images, fragments and MFMA order as the register path: bit-identical.
+    auto mainloop_dma = [&](auto mode_tag) {
+      if constexpr (kDMA) {
+        constexpr bool FULL = decltype(mode_tag)::value == 1;
+        constexpr int PFA = BM * BN > 256 * 128 ? 1 : 2;   // (a second A set spills at 256 x 256)
+        constexpr int LA = 2 * x6_nu(BM, NT);   // A's global_load_dwordx4 per thread and slice (interior)
+        constexpr int GB = BN * 8 / NT;         // B's DMA pieces per thread and slice
+        // VMEM ops issued after B(kt+1) that may stay in flight at the end of step kt: the NSB - 2
+        // later steps' A loads and DMA (each step issues its A loads, then its DMA)
+        constexpr int WAITN = (NSB - 2) * (GB + LA);
+        static_assert(WAITN < 64, "vmcnt range");
+        const uint4* img = reinterpret_cast<const uint4*>(g.B) + (tn * (g.K / X6_BK) + kb / X6_BK) * (BN * 8) + t;
+        uint4* const bslots = smem + 2 * A_U4;
+        // every step issues its B DMA and A loads unconditionally (past the last slice they re-read
+        // slice nk - 1 into a free slot / register set, never used), so that hipcc's own waits for
+        // the A registers count exactly instead of draining everything (vmcnt(0)) at each step
+        auto issue_b = [&](int64_t kt) {   // slice min(kt, nk - 1) into slot kt % NSB
+            const uint4* src = img + (kt < nk ? kt : nk - 1) * (BN * 8);
+            uint4* dst = bslots + (int)(kt % NSB) * B_U4 + wave * 64;
+#pragma unroll
+            for (int q = 0; q < GB; ++q)
+                __builtin_amdgcn_global_load_lds((x6_gbl_t*)(src + NT * q), (x6_lds_t*)(dst + NT * q), 16, 0, 0);
+        };
+        auto load_a = [&](int64_t kt, Regs& r) {
+            x6_load<1, BM, NT, FULL>(g.A, g.lda, g.M, m0, kb + (kt < nk ? kt : nk - 1) * X6_BK, ke, a_vec, r.a, t);
+        };
+        auto step = [&](int64_t kt, Regs& r) {
+            const int cur = (int)(kt & 1);
+            if (kt + 1 < nk) x6_store<1, BM, NT, PREC>(As[cur ^ 1], r.a, t, sa);
+            // (hipcc drains all of vmcnt before the split every other step -- the DMA is a second
+            // event type in the counter -- so the DMA goes after the split, never ahead of that wait)
+            __builtin_amdgcn_sched_barrier(0);
+            load_a(kt + 1 + PFA, r);
+            issue_b(kt + NSB - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            x6_mma16_h3<BM, BN, WM, WN>(As[cur], bslots + (int)(kt % NSB) * B_U4, acc4, wm, wn, lane);
+            // this wave's part of B(kt + 1) has landed (the newer DMA and loads stay in flight); the
+            // barrier then publishes every wave's part and this step's A stores
+            if constexpr (FULL) x6_wait_vmcnt<WAITN>();
+            else x6_wait_vmcnt<0>();
+            x6_barrier_lds();
+        };
+        if (nk > 0) {
+            for (int64_t m = 0; m < NSB - 1; ++m) issue_b(m);
+            load_a(0, rs[0]);
+            x6_store<1, BM, NT, PREC>(As[0], rs[0].a, t, sa);
+            x6_wait_vmcnt<0>();   // B(0) .. B(NSB-2) landed (A(0) was the newest load)
+            load_a(1, rs[1]);
+            if constexpr (PFA == 2) load_a(2, rs[0]);
+        }
+        x6_barrier_lds();
+        int64_t kt = 0;
+        if constexpr (PFA == 2) {
+            for (; kt + 1 < nk; kt += 2) {
+                step(kt, rs[1]);
+                step(kt + 1, rs[0]);
+            }
+        }
+        for (; kt < nk; ++kt) step(kt, rs[1]);
+        // the unused tail DMA must land before the epilogue reuses the LDS as its stage
+        x6_wait_vmcnt<0>();
+        x6_barrier_lds();
+      }
+    };
+    if constexpr (kDMA) {
+        if (full) mainloop_dma(std::integral_constant<int, 1>{});
+        else mainloop_dma(std::integral_constant<int, 0>{});
+    } else if (full) {
         mainloop(std::integral_constant<int, 1>{});
     } else {
         // the last split-K slab of the weight gradient (K = the node count, rarely a multiple of
@@ -559,6 +697,18 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
 template <int PREC, int TA, int TB, int ABL>
 inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if constexpr (PREC == 1 && TA == 0 && TB == 1) {
+        if (g.wb && g_x6_bdma >= 2 && h3p_ok(cfg, g)) {   // the pipelined kernels (gemm_h3p.hip)
+            launch_h3p(ABL, grid, s, g);
+            return;
+        }
+        if (g.wb && g_x6_bdma == 1) {   // the same tiles with B staged by LDS-DMA
+            switch (cfg) {
+                case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 12>), grid, dim3(512), 0, s, g); return;
+                case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 12>), grid, dim3(512), 0, s, g); return;
+                case 3: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL, 12>), grid, dim3(512), 0, s, g); return;
+                default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 12>), grid, dim3(512), 0, s, g); return;
+            }
+        }
         if (g.wb) {   // pre-split B image (bgnn_gemm_f32_w): tiles with BN = the image's column tile
             switch (cfg) {
                 case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;

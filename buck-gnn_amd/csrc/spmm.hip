@@ -1231,6 +1231,12 @@ inline SegArgs args_from_csr(const bgnn_csr_t* c) {
     return A;
 }
 
+extern int g_x6_bdma;   // gemm_x6.hip
+extern int g_h3p_nsb;   // gemm_h3p.hip
+#ifdef BGNN_H3P_ABLATION
+extern int g_h3p_abl;
+#endif
+
 }  // namespace bgnn
 
 using namespace bgnn;
@@ -1362,6 +1368,7 @@ extern "C" int32_t bgnn_get_tuning(int32_t knob) {
         case BGNN_TUNE_ROWS_NT: return rows_nt();
         case BGNN_TUNE_GROUP_BLOCKS: return g_grp_blocks;
         case BGNN_TUNE_ROWS_REV: return rows_rev();
+        case BGNN_TUNE_GEMM_BDMA: return g_x6_bdma == 2 && g_h3p_nsb == 4 ? 3 : g_x6_bdma;
         default: return -1;
     }
 }
@@ -1388,6 +1395,22 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             return BGNN_OK;
         case BGNN_TUNE_ROWS_NT: set_rows_nt(value); return BGNN_OK;
         case BGNN_TUNE_ROWS_REV: set_rows_rev(value); return BGNN_OK;
+        case BGNN_TUNE_GEMM_BDMA:
+#ifdef BGNN_H3P_ABLATION
+            if (value >= 16) {   // measurement build: the pipelined kernel (4 slots) with ablation value / 16
+                g_x6_bdma = 2;
+                g_h3p_nsb = 4;
+                g_h3p_abl = value / 16;
+                return BGNN_OK;
+            }
+            g_h3p_abl = 0;
+#endif
+            BGNN_REQUIRE(value >= 0 && value <= 4,
+                         "set_tuning: gemm B DMA must be 0 (register copy), 1 (LDS-DMA), 2 / 3 (pipelined 128 x 256, "
+                         "3 / 4 slots) or 4 (pipelined 128 x 128, two workgroups per CU)");
+            g_x6_bdma = value == 3 ? 2 : value;
+            g_h3p_nsb = value == 3 ? 4 : 3;
+            return BGNN_OK;
         case BGNN_TUNE_GEMM_MODE:
             BGNN_REQUIRE(value == 0 || value == 2, "set_tuning: gemm mode must be 0 (f32 MFMA) or 2 (f16x3)");
             set_gemm_mode(value);

@@ -86,6 +86,10 @@ const char* bgnn_last_error_string(void);
  * staging, B fragments in registers, interleaved schedule, 32x32x16 MFMAs), the round-6 wave-order
  * swap and static priority, and the row-group max aggregation -- all measured slower or equal;
  * profiles/r05_*, profiles/r06_gemm_ab_b.txt) */
+#define BGNN_TUNE_GEMM_BDMA 16   /* pre-split f16x3 GEMMs (bgnn_gemm_f32_w, the SAGE forward and
+                                    input gradients): 0 = B's image copied into LDS through
+                                    registers, 1 = B's image staged by LDS-DMA
+                                    (global_load_lds_dwordx4, 3-4 slots in flight). Bit-identical */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose

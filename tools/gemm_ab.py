@@ -10,7 +10,8 @@ rounds. Results are checked bit-identical to the first variant.
 the first-variant order bias, profiles/r06_gemm_edge_first_l.txt; not kept.) Variants: "xC" the register-staged kernel (bgnn_gemm_f32_scaled) on tile config C (-1 = the
 automatic plan); "w" the pre-split weight path (bgnn_gemm_wsplit + bgnn_gemm_f32_w); "d" the same
 with the drop-add epilogue (src = an [M, N] gradient, p = 0.1: the skip layers' dgrad); "w.C" /
-"d.C" on tile config C. (Round 6 measured the main-loop variants "wP" of the then knob 14 here,
+"d.C" on tile config C; "W", "D" (and "W.C", "D.C") the same with B staged by LDS-DMA (knob 16 = 1); a suffix "@V" sets
+knob 16 (BGNN_TUNE_GEMM_BDMA) to V for that variant ("w@2": the pipelined kernel gemm_h3p.hip). (Round 6 measured the main-loop variants "wP" of the then knob 14 here,
 profiles/r06_gemm_ab_b.txt.)
 """
 import argparse
@@ -28,11 +29,16 @@ SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872,
 
 
 def parse(vs):
+    """-> (kind, knob-16 value, tile cfg)"""
+    vs, _, kv = vs.partition("@")
     kind = vs[0]
+    if kind in "WD":   # the w / d variants with B staged by LDS-DMA (knob 16 = 1)
+        kind, kv = kind.lower(), kv or "1"
+    knob = int(kv) if kv else 0
     if kind == "x":
-        return kind, 0, int(vs[1:])
+        return kind, knob, int(vs[1:])
     _, _, cfg = vs[1:].partition(".")
-    return kind, 0, int(cfg) if cfg else -1
+    return kind, knob, int(cfg) if cfg else -1
 
 
 def main():
@@ -56,8 +62,9 @@ def main():
         imgs = {}
         for vs in variants:
             kind, pp, cfg = parse(vs)
-            if kind in "wd":
+            if kind[0] in "wd":
                 _lib.call("bgnn_gemm_set_cfg", cfg)
+                _lib.call("bgnn_set_tuning", 16, pp)   # (knob 16 = 4 plans 128-column images)
                 bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
                 img = torch.empty(_lib.query("bgnn_gemm_wsplit_bytes", N, K), dtype=torch.uint8, device=dev)
                 _lib.call("bgnn_gemm_wsplit", b.data_ptr(), 1, 0, N, K, K, am[1:2].data_ptr(), 0, img.data_ptr(),
@@ -69,28 +76,30 @@ def main():
             for vs in variants:
                 kind, pp, cfg = parse(vs)
                 _lib.call("bgnn_gemm_set_cfg", cfg)
+                _lib.call("bgnn_set_tuning", 16, pp)
                 if flush is not None:
                     flush.fill_(float(i))
                 out = outs[vs]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                if kind in "wd":
+                if kind[0] in "wd":
                     img, bn = imgs[vs]
                     _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N,
                               None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None,
-                              src.data_ptr() if kind == "d" else None, N, 0.1, 1234, fused._stream())
+                              src.data_ptr() if kind[0] == "d" else None, N, 0.1, 1234, fused._stream())
                 else:
                     fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 e1.record()
                 if i >= 2:
                     times[vs].append((e0, e1))
         _lib.call("bgnn_gemm_set_cfg", -1)
+        _lib.call("bgnn_set_tuning", 16, 0)
         torch.cuda.synchronize()
         ref = {}
         for vs in variants:
             us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in times[vs])
             med = us[len(us) // 2]
-            kind = vs[0]
+            kind = vs[0].lower()
             r = ref.setdefault(kind == "d", outs[vs])
             same = "ref" if r is outs[vs] else ("bit-identical" if torch.equal(outs[vs], r) else
                                                 f"DIFFERS max {(outs[vs] - r).abs().max().item():.3g}")
