@@ -23,7 +23,7 @@
 
 namespace bgnn {
 
-int g_h3p_nsb = 3;   // B slots (measurement: 3 or 4)
+int g_h3p_nsb = 4;   // B slots (3 or 4; default 4: r06o/r06q, dgrad 269-263 us against 273 with 3)
 
 namespace {
 

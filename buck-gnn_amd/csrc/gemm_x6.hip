@@ -41,7 +41,10 @@ const X6Cfg kX6Cfgs[] = {
 };
 const int kNumX6Cfgs = 5;
 
-int g_x6_bdma = 0;
+// knob 16 (BGNN_TUNE_GEMM_BDMA): default 2 with 4 slots = the pipelined 128 x 256 kernel (gemm_h3p.hip)
+// for the pre-split products planned on that tile (the SAGE input gradients): bit-identical, dgrad
+// 272 -> 263 us, drop-add 321 -> 312, cfg2 step 8.74 -> 8.67 ms (profiles/r06_gemm_h3p_q.txt)
+int g_x6_bdma = 2;
 
 void launch_x6(int prec, int ta, int tb, int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if (prec == 2 && g.st != 0) launch_x6_bf16_storage(ta, tb, cfg, g.st, grid, s, g);

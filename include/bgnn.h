@@ -88,8 +88,13 @@ const char* bgnn_last_error_string(void);
  * profiles/r05_*, profiles/r06_gemm_ab_b.txt) */
 #define BGNN_TUNE_GEMM_BDMA 16   /* pre-split f16x3 GEMMs (bgnn_gemm_f32_w, the SAGE forward and
                                     input gradients): 0 = B's image copied into LDS through
-                                    registers, 1 = B's image staged by LDS-DMA
-                                    (global_load_lds_dwordx4, 3-4 slots in flight). Bit-identical */
+                                    registers (k_gemm_x6), 1 = the same kernel with B's image
+                                    staged by LDS-DMA, 2 / 3 = the pipelined kernel (B by LDS-DMA
+                                    into 3 / 4 slots, next slice's fragments read under the
+                                    current MFMAs) on the 128 x 256 tiles, 4 = the pipelined
+                                    kernel on 128 x 128 tiles, two workgroups per CU (also plans
+                                    128-column images, bgnn_gemm_w_tile). Default 3.
+                                    Bit-identical for every setting                           */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.
  * read: which = 0 the forward aggregations (bgnn_sage_fwd, bgnn_spmm_fwd), 1 the transpose

@@ -251,13 +251,16 @@ def test_gemm_presplit_weights_bit_identical(dev, M, N, K, dropadd, cfg, bdma):
     a = torch.randn(M, K, device=dev)
     w = torch.randn(N, K, device=dev) * 0.03
     am = torch.stack([a.abs().max(), w.abs().max()]).contiguous()
+    default_bdma = _lib.query("bgnn_get_tuning", 16)
     _lib.call("bgnn_gemm_set_cfg", cfg)
+    _lib.call("bgnn_set_tuning", 16, bdma)   # (bdma 4 plans 128-column images)
     try:
         if _lib.query("bgnn_gemm_w_tile", M, N, K) == 0:
             pytest.skip("no pre-split path for this shape and tile")
         img, bn = _wsplit(w, am[1:2], M)
     finally:
         _lib.call("bgnn_gemm_set_cfg", -1)
+        _lib.call("bgnn_set_tuning", 16, default_bdma)
 
     def run_w(*args):
         _lib.call("bgnn_gemm_set_cfg", cfg)
@@ -266,7 +269,7 @@ def test_gemm_presplit_weights_bit_identical(dev, M, N, K, dropadd, cfg, bdma):
             _lib.call("bgnn_gemm_f32_w", *args)
         finally:
             _lib.call("bgnn_gemm_set_cfg", -1)
-            _lib.call("bgnn_set_tuning", 16, 0)
+            _lib.call("bgnn_set_tuning", 16, default_bdma)
     if dropadd:
         src = torch.randn(M, N, device=dev)
         ref = torch.empty(M, N, device=dev)

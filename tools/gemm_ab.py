@@ -93,7 +93,7 @@ def main():
                 if i >= 2:
                     times[vs].append((e0, e1))
         _lib.call("bgnn_gemm_set_cfg", -1)
-        _lib.call("bgnn_set_tuning", 16, 0)
+        _lib.call("bgnn_set_tuning", 16, 3)
         torch.cuda.synchronize()
         ref = {}
         for vs in variants:
