@@ -410,7 +410,9 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.prec = 1;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
         // knob 16 = 4: the pre-split products on the pipelined 128 x 128 kernel (gemm_h3p.hip)
+#ifdef BGNN_H3P_ABLATION
         if (wb && g_x6_bdma == 4 && g_gemm_cfg < 0 && N % 128 == 0 && K % 32 == 0) p.cfg = 0;
+#endif
         // plane blocks must be whole tiles: fall back to an 8-wave tile that divides them (the
         // 16x16x32 MFMA family, the same rounding as the dense layout's), else the 128x128 tile
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) {

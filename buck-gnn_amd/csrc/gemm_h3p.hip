@@ -259,12 +259,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     x6_epilogue<TM, TN, ABL, false>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), n0, 0, lane, ia, ib, stage);
 }
 
+
 }  // namespace
 
 // the plan tile (cfg) must be 128 x 256 (2 x 4 waves, knob 16 = 2 / 3) or 128 x 128 (2 x 2 waves,
 // knob 16 = 4); K % 32 == 0, 16-B aligned A rows
 bool h3p_ok(int cfg, const GemmArgs& g) {
-    const bool tile = (cfg == 2 && (g_x6_bdma == 2 || g_x6_bdma == 3)) || (cfg == 0 && g_x6_bdma == 4);
+    const bool tile = (cfg == 2 && g_x6_bdma == 2) || (cfg == 0 && g_x6_bdma == 4);
     return tile && g.wb && g.split <= 1 && g.a_blk == 0 && g.c_blk == 0 && g.K > 0 && g.K % X6_BK == 0 &&
            g.lda % 4 == 0 && aligned16(g.A);
 }
@@ -295,11 +296,13 @@ void launch_h3p(int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
         default: break;
     }
 #endif
-    if (g_x6_bdma == 4) {   // 128 x 128, two workgroups per CU
+#ifdef BGNN_H3P_ABLATION
+    if (g_x6_bdma == 4) {   // 128 x 128, two workgroups per CU (measurement build only)
         if (abl == 8) hipLaunchKernelGGL((k_gemm_h3p<128, 128, 2, 2, 3, 8, 0, 2>), grid, dim3(256), 0, s, g);
         else hipLaunchKernelGGL((k_gemm_h3p<128, 128, 2, 2, 3, 0, 0, 2>), grid, dim3(256), 0, s, g);
         return;
     }
+#endif
     if (abl == 8) {
         if (g_h3p_nsb == 4) hipLaunchKernelGGL((k_gemm_h3p<128, 256, 2, 4, 4, 8>), grid, dim3(512), 0, s, g);
         else hipLaunchKernelGGL((k_gemm_h3p<128, 256, 2, 4, 3, 8>), grid, dim3(512), 0, s, g);

@@ -701,7 +701,8 @@ inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
             launch_h3p(ABL, grid, s, g);
             return;
         }
-        if (g.wb && g_x6_bdma == 1) {   // the same tiles with B staged by LDS-DMA
+#ifdef BGNN_H3P_ABLATION
+        if (g.wb && g_x6_bdma == 1) {   // the same tiles with B staged by LDS-DMA (measurement build only)
             switch (cfg) {
                 case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 12>), grid, dim3(512), 0, s, g); return;
                 case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 12>), grid, dim3(512), 0, s, g); return;
@@ -709,6 +710,7 @@ inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
                 default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 12>), grid, dim3(512), 0, s, g); return;
             }
         }
+#endif
         if (g.wb) {   // pre-split B image (bgnn_gemm_f32_w): tiles with BN = the image's column tile
             switch (cfg) {
                 case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;

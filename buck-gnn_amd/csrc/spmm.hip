@@ -1405,9 +1405,13 @@ extern "C" int bgnn_set_tuning(int32_t knob, int32_t value) {
             }
             g_h3p_abl = 0;
 #endif
-            BGNN_REQUIRE(value >= 0 && value <= 4,
-                         "set_tuning: gemm B DMA must be 0 (register copy), 1 (LDS-DMA), 2 / 3 (pipelined 128 x 256, "
-                         "3 / 4 slots) or 4 (pipelined 128 x 128, two workgroups per CU)");
+#ifdef BGNN_H3P_ABLATION
+            BGNN_REQUIRE(value >= 0 && value <= 4, "set_tuning: gemm B staging must be 0 .. 4");
+#else
+            BGNN_REQUIRE(value == 0 || value == 2 || value == 3,
+                         "set_tuning: gemm B staging must be 0 (k_gemm_x6, register copy) or 2 / 3 (the pipelined "
+                         "kernel, 3 / 4 slots); 1 and 4 are measurement-build forms (make abl)");
+#endif
             g_x6_bdma = value == 3 ? 2 : value;
             g_h3p_nsb = value == 3 ? 4 : 3;
             return BGNN_OK;

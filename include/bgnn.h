@@ -86,14 +86,11 @@ const char* bgnn_last_error_string(void);
  * staging, B fragments in registers, interleaved schedule, 32x32x16 MFMAs), the round-6 wave-order
  * swap and static priority, and the row-group max aggregation -- all measured slower or equal;
  * profiles/r05_*, profiles/r06_gemm_ab_b.txt) */
-#define BGNN_TUNE_GEMM_BDMA 16   /* pre-split f16x3 GEMMs (bgnn_gemm_f32_w, the SAGE forward and
-                                    input gradients): 0 = B's image copied into LDS through
-                                    registers (k_gemm_x6), 1 = the same kernel with B's image
-                                    staged by LDS-DMA, 2 / 3 = the pipelined kernel (B by LDS-DMA
-                                    into 3 / 4 slots, next slice's fragments read under the
-                                    current MFMAs) on the 128 x 256 tiles, 4 = the pipelined
-                                    kernel on 128 x 128 tiles, two workgroups per CU (also plans
-                                    128-column images, bgnn_gemm_w_tile). Default 3.
+#define BGNN_TUNE_GEMM_BDMA 16   /* pre-split f16x3 GEMMs (bgnn_gemm_f32_w) planned on 128 x 256
+                                    tiles (the SAGE input gradients): 0 = k_gemm_x6 (B's image
+                                    copied into LDS through registers), 2 / 3 = the pipelined
+                                    kernel (gemm_h3p.hip: B by LDS-DMA into 3 / 4 slots, the next
+                                    slice's fragments read under the current MFMAs). Default 3.
                                     Bit-identical for every setting                           */
 /* Heavy-row timing (measurement only): while enabled, every aggregation launch with super-node
  * chunks records a HIP event pair around its chunk + combine kernels. Enabling resets the record.

@@ -238,22 +238,22 @@ def _wsplit(w, w_amax, M):
                                    (1000, 512, 1024), (4097, 1024, 512)])
 @pytest.mark.parametrize("dropadd", [False, True])
 @pytest.mark.parametrize("cfg", [-1, 1, 2])
-@pytest.mark.parametrize("bdma", [0, 1, 2, 3])
+@pytest.mark.parametrize("bdma", [0, 2, 3])
 def test_gemm_presplit_weights_bit_identical(dev, M, N, K, dropadd, cfg, bdma):
     """bgnn_gemm_wsplit + bgnn_gemm_f32_w (the weight operand pre-split once, its image copied into
     LDS) produce exactly the bits of bgnn_gemm_f32_scaled / bgnn_gemm_f32_dropadd on the same
     operands and maxima (the LDS image is the one the register-staged kernel writes), with bias,
     ReLU and max|C| in the plain epilogue and the masked beta source in the drop-add epilogue; on
     the planned tile (cfg -1) and forced 256 x 128 / 128 x 256 tiles; for every B staging of knob 16
-    (register copy, LDS-DMA, and the pipelined kernel gemm_h3p.hip with 3 / 4 slots, which the
-    128 x 256 tile runs: ragged last row tiles, K = 128's four slices)."""
+    (register copy, and the pipelined kernel gemm_h3p.hip with 3 / 4 slots, which the 128 x 256 tile
+    runs: ragged last row tiles, K = 128's four slices)."""
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=dev)
     w = torch.randn(N, K, device=dev) * 0.03
     am = torch.stack([a.abs().max(), w.abs().max()]).contiguous()
     default_bdma = _lib.query("bgnn_get_tuning", 16)
     _lib.call("bgnn_gemm_set_cfg", cfg)
-    _lib.call("bgnn_set_tuning", 16, bdma)   # (bdma 4 plans 128-column images)
+    _lib.call("bgnn_set_tuning", 16, bdma)
     try:
         if _lib.query("bgnn_gemm_w_tile", M, N, K) == 0:
             pytest.skip("no pre-split path for this shape and tile")
