@@ -360,7 +360,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
     constexpr int SLICE_U4 = (BM + BN) * L::CPR;
     static_assert(GA * L::RPI * NW == BM && GB * L::RPI * NW == BN, "rows must split evenly over the waves");
     static_assert((NS - 2) * G < 64, "vmcnt range");
-    constexpr int EPI_U4 = NW * TM * 32 * 32 / 4;
+    // per-wave LDS stage (floats): TM 32-row blocks of 32 columns, or the whole-line bf16 form's
+    // [32][68] pair of blocks, whichever is larger (TM = 2 tiles: the latter)
+    constexpr int STG = (C16 && WIDE && TM * 32 * 32 < 32 * 68) ? 32 * 68 : TM * 32 * 32;
+    constexpr int EPI_U4 = NW * STG / 4;
     constexpr int SMEM_U4 = NS * SLICE_U4 > EPI_U4 ? NS * SLICE_U4 : EPI_U4;
     // WIDE bf16 C with gathered rows: the tile's gi0 / gi1 (BM int64 each) copied to LDS by the
     // waves' first loads, so the epilogue's gather addresses wait on LDS instead of a dependent
@@ -436,13 +439,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_b16(GemmArgs g) {
         b16_mma<BM, BN, BK, WM, WN>(smem + (int)(m % NS) * SLICE_U4, acc, wm, wn, lane);
     }
     __syncthreads();   // every wave's fragment reads done before the epilogue reuses the LDS
-    float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
+    float* stage = reinterpret_cast<float*>(smem) + wave * STG;
     const int64_t* li = reinterpret_cast<const int64_t*>(smem + SMEM_U4) + wm * (BM / WM);
     b16_epilogue<TM, TN, C16, WIDE>(g, acc, m0 + wm * (BM / WM), n0 + wn * (BN / WN), lane, stage,
                                     lidx ? li : nullptr, lidx && g.ga1 ? li + BM : nullptr);
 }
 
 int g_b16_variant = 0;   // 0 = the LDS-DMA kernel (default), -1 = bf16-stored NT products on k_gemm_x6 (A/B)
+// (round 6 measured a 128 x 256 form with two workgroups per CU, k32 x 3 slots, so that one's
+// epilogue runs under the other's main loop: plain 2015 -> 2351 us, gathered 3635 -> 3606, drop-add
+// 2841 -> 2881 at E = 2.86M, profiles/r06_b16_two_per_cu_v.txt; removed. Its stage sizing stays:
+// the whole-line bf16 stage [32][68] is larger than TM = 2 blocks of 32 x 32.)
 
 }  // namespace
 

@@ -187,7 +187,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
             }
 #pragma unroll
             for (int i = 0; i < 2 * TM; ++i) mma3(acc[i][j], F.a[i], F.b[j]);
-            if (j == 0) {
+            // waves 4-7 stage after the third column block instead of the first, so that a SIMD's two
+            // waves do not both leave the MFMA pipe for their staging at once (the guide's stagger;
+            // dgrad 262.5 -> 257.6 us, drop-add 311.7 -> 308.9, bit-identical, r06_gemm_stagger_u.txt)
+            const int jst = (wave >= 4 && !(X & 64)) ? 2 : 0;   // (X & 64: measurement build, no stagger)
+            if (j == jst) {
                 // (the first two steps wait on the prologue's A(2) / A(3), fewer ops behind them)
                 if (kt >= 2) h3p_wait<WAIT_A>(R);
                 else if (kt == 1) h3p_wait<LA + GBW>(R);
@@ -293,6 +297,7 @@ void launch_h3p(int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
         case 31: launch_x<31>(abl, grid, s, g); return;
         case 32: launch_x<32>(abl, grid, s, g); return;
         case 63: launch_x<63>(abl, grid, s, g); return;
+        case 64: launch_x<64>(abl, grid, s, g); return;
         default: break;
     }
 #endif

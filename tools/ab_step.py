@@ -51,8 +51,8 @@ def main():
         apply(s)
         for _ in range(3):
             step()
-    for _ in range(rounds):
-        for s in settings:
+    for r in range(rounds):
+        for s in (settings if r % 2 == 0 else settings[::-1]):   # (alternate the order: no position bias)
             apply(s)
             step()
             torch.cuda.synchronize()

@@ -15,6 +15,7 @@ knob 16 (BGNN_TUNE_GEMM_BDMA) to V for that variant ("w@2": the pipelined kernel
 profiles/r06_gemm_ab_b.txt.)
 """
 import argparse
+import random
 import os
 import sys
 
@@ -47,6 +48,7 @@ def main():
     ap.add_argument("--variants", default="w,d")
     ap.add_argument("--shapes", default="fwd,dgrad")
     ap.add_argument("--no-flush", action="store_true")
+    ap.add_argument("--fixed-order", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     flush = None if args.no_flush else torch.empty(1 << 28, device=dev)
@@ -72,8 +74,12 @@ def main():
                 imgs[vs] = (img, bn)
         _lib.call("bgnn_gemm_set_cfg", -1)
         times = {v: [] for v in variants}
+        rng = random.Random(0)
         for i in range(args.reps + 2):
-            for vs in variants:
+            order = list(variants)
+            if not args.fixed_order:   # (a fixed order favours or penalises the first variant by up to ~10 %)
+                rng.shuffle(order)
+            for vs in order:
                 kind, pp, cfg = parse(vs)
                 _lib.call("bgnn_gemm_set_cfg", cfg)
                 _lib.call("bgnn_set_tuning", 16, pp)
