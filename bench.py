@@ -499,9 +499,9 @@ GEMM_FAMILIES = {
                  "gemm_fwd_h3", "fwd z = x [W_l;W_r]^T, K = 512 layers (5 per step)"),
     "gemm_dgrad": (lambda N, H, K: 2.0 * N * H * (2 * H),
                    lambda N, H, K: 4.0 * (N * 2 * H + 2 * H * H + N * H) + 4.0 * N * H * 4 / 5,
-                   "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8, 4> (skip layers, drop-add epilogue) + "
-                   "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0, 4> (last layer); weights pre-split once per step "
-                   "(bgnn_gemm_f32_w)", "gemm_dgrad", "dgrad dx = [dz_l|dh] [W_l;W_r], K = 512 layers (5 per step; "
+                   "k_gemm_h3p<128, 256, 2, 4, 4, 8> (skip layers, drop-add epilogue) + "
+                   "k_gemm_h3p<128, 256, 2, 4, 4, 0> (last layer): the pipelined pre-split kernel (gemm_h3p.hip); "
+                   "weights pre-split once per step (bgnn_gemm_f32_w)", "gemm_dgrad", "dgrad dx = [dz_l|dh] [W_l;W_r], K = 512 layers (5 per step; "
                    "4 read the drop-add source)"),
     "gemm_wgrad": (lambda N, H, K: 2.0 * (2 * H) * H * N, lambda N, H, K: 4.0 * (N * 2 * H + N * H + 2 * H * H),
                    "k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0> + split-K slab reduce", "gemm_wgrad",

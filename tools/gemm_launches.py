@@ -20,7 +20,9 @@ PEAK = 2500.0 / 3   # f16x3 f32-equivalent ceiling, TF
 FAMS = {
     "gemm_fwd": ["k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0, 4>"],
     "gemm_fwd_fold": ["k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0, 0>"],
-    "gemm_dgrad": ["k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8, 4>", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0, 4>"],
+    # (round 6: the K = 512 input gradients run the pipelined kernel, gemm_h3p.hip)
+    "gemm_dgrad": ["k_gemm_h3p<128, 256, 2, 4, 4, 8", "k_gemm_h3p<128, 256, 2, 4, 4, 0",
+                   "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8, 4>", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0, 4>"],
     "gemm_wgrad": ["k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0, 0>"],
     "gemm_dgrad_fold": ["k_gemm_x6<1, 0, 1, 256, 128, 4, 2, 0, 0>"],
     "gemm_wgrad_fold": ["k_gemm_x6<1, 1, 0, 256, 128, 4, 2, 0, 0>"],

@@ -23,7 +23,8 @@ from collections import defaultdict
 # bench roofline kernels: key -> kernel-name substrings (either matches)
 KERNELS = {
     "gemm_fwd_h3": ("k_gemm_x6<1, 0, 1, 256, 256, 4, 2, 0,",),   # f16x3 forward GEMM (256x256 tiles)
-    "gemm_dgrad": ("k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8,", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0,"),   # dgrad
+    "gemm_dgrad": ("k_gemm_h3p<128, 256, 2, 4, 4,", "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 8,",
+                   "k_gemm_x6<1, 0, 1, 128, 256, 2, 4, 0,"),   # dgrad (pipelined kernel since round 6)
     "gemm_wgrad": ("k_gemm_x6<1, 1, 0, 256, 256, 4, 2, 0,",),   # wgrad (split-K partial products)
     "sage_fwd": ("k_seg_group<2, 0, 1,", "k_seg_sweep<2, 0, 1,"),   # fused SAGE forward aggregation
     "spmm_bwd": ("k_seg_group<2, 0, 0,", "k_seg_sweep<2, 0, 0,"),   # transpose aggregation
