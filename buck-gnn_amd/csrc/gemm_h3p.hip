@@ -126,7 +126,30 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     const uint4* img = reinterpret_cast<const uint4*>(g.B) + tn * nk * (BN * 8) + t;
     // (asm, like A's loads: hipcc would otherwise drain every DMA in flight, vmcnt(0), before each
     // LDS read it cannot prove disjoint from them -- the fragment reads of the next slice)
+    // The drop-add source through LDS (ABL 8 with the plain epilogue of bgnn_gemm_f32_w): the DMA of
+    // the last NSB steps, which would re-read B's last slice, brings the tile's masked-gradient source
+    // rows instead -- quarter q (BM / NSB rows of 1 KiB) into slot (nk + q) % NSB, the same slots and
+    // vmcnt counts -- so the epilogue reads them from LDS instead of waiting on HBM
+    constexpr bool kSrcLds = ABL == 8 && X == 0 && BN * 4 == 1024 && NSB * GB * (NT / 64) == BM;
+    const bool lsrc = kSrcLds && g.bsrc_c0 == 0 && !g.bias && !g.relu && !g.c_amax && !g.ga0 && g.alpha == 1.f &&
+                      g.beta == 1.f && nk >= NSB && g.ld_bsrc % 4 == 0 && ((uintptr_t)g.bsrc & 15) == 0 &&
+                      ((uintptr_t)g.C & 15) == 0 &&
+                      g.ldc % 4 == 0;
     auto issue_b = [&](int64_t kt) {
+        if (kSrcLds && lsrc && kt >= nk) {   // source rows (kt - nk) * BM / NSB + wave * GB + q of the tile
+            const int64_t r0 = m0 + (kt - nk) * (BM / NSB) + wave * GB;
+            const uint32_t dst = (uint32_t)(uintptr_t)(x6_lds_t*)(bslots + (int)(kt % NSB) * B_U4 + wave * GB * 64);
+#pragma unroll
+            for (int q = 0; q < GB; ++q) {
+                const int64_t row = r0 + q < g.M ? r0 + q : g.M - 1;
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                             :
+                             : "s"(__builtin_amdgcn_readfirstlane(dst + q * 1024)),
+                               "v"(g.bsrc + row * g.ld_bsrc + n0 + 4 * lane)
+                             : "memory", "m0");
+            }
+            return;
+        }
         const uint4* src = img + (kt < nk ? kt : nk - 1) * (BN * 8);
         const uint32_t dst = (uint32_t)(uintptr_t)(x6_lds_t*)(bslots + (int)(kt % NSB) * B_U4 + wave * 64);
 #pragma unroll
@@ -252,6 +275,58 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
             for (int j = 0; j < 2 * TN; ++j) v += acc[i][j][0];
         if (g.alpha == -7.f) g.C[t] = v;
         return;
+    }
+    if constexpr (kSrcLds) {
+        if (lsrc) {
+            // x6_epilogue's fast-path arithmetic per element (its general path, (e * ia) * ib, for a
+            // wave whose rows run past M), the source from LDS; one 32 x 32 block at a time through a
+            // 4 KiB per-wave stage in the (now idle) A buffers
+            float* stg = reinterpret_cast<float*>(abuf) + wave * 1024;
+            const int rq = lane >> 3, c4 = (lane & 7) * 4;
+            const int64_t wr0 = m0 + wm * (BM / WM);
+            const bool fastw = wr0 + TM * 32 <= g.M;
+            const float iab = ia * ib;
+            const bool one_mul = fastw && iab != 0.f && iab < 3.0e38f;
+            const float* bl = reinterpret_cast<const float*>(bslots);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+#pragma unroll
+                    for (int si = 0; si < 2; ++si)
+#pragma unroll
+                        for (int sj = 0; sj < 2; ++sj)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                stg[(si * 16 + 4 * lq + r) * 32 + sj * 16 + l16] = acc[2 * i + si][2 * j + sj][r];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int rr = q * 8 + rq;
+                        const int trow = wm * (BM / WM) + i * 32 + rr;   // row in the tile
+                        const int tcol = wn * (BN / WN) + j * 32 + c4;
+                        const int64_t row = m0 + trow, col = n0 + tcol;
+                        const float4 sv = *reinterpret_cast<const float4*>(stg + rr * 32 + c4);
+                        const float4 src = *reinterpret_cast<const float4*>(
+                            bl + (int)((nk + trow / (BM / NSB)) % NSB) * (B_U4 * 4) + (trow % (BM / NSB)) * BN + tcol);
+                        if (row >= g.M) continue;
+                        float pv[4];
+                        beta_mask4(g, row, col, src, pv);
+                        const float e[4] = {sv.x, sv.y, sv.z, sv.w};
+                        float o[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            float v = one_mul ? e[k] * iab : (e[k] * ia) * ib;
+                            v *= g.alpha;
+                            v += g.beta * pv[k];
+                            o[k] = v;
+                        }
+                        st_nt4(g.C + row * g.ldc + col, o);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+            return;
+        }
     }
     float* stage = reinterpret_cast<float*>(smem) + wave * (TM * 32 * 32);
     if (ABL == 8 && n0 < g.bsrc_c0) {   // drop-add GEMM, a column tile left of the beta operand
