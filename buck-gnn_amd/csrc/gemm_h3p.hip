@@ -344,6 +344,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
 // the plan tile (cfg) must be 128 x 256 (2 x 4 waves, knob 16 = 2 / 3) or 128 x 128 (2 x 2 waves,
 // knob 16 = 4); K % 32 == 0, 16-B aligned A rows
 bool h3p_ok(int cfg, const GemmArgs& g) {
+    // (round 6 also measured the forward, N = 1024, on 256 x 128 and 128 x 256 pipelined tiles:
+    // 318 / 298 us against k_gemm_x6's 256 x 256 at 284, profiles/r06_gemm_fwd_tiles_z.txt)
     const bool tile = (cfg == 2 && g_x6_bdma == 2) || (cfg == 0 && g_x6_bdma == 4);
     return tile && g.wb && g.split <= 1 && g.a_blk == 0 && g.c_blk == 0 && g.K > 0 && g.K % X6_BK == 0 &&
            g.lda % 4 == 0 && aligned16(g.A);
@@ -358,7 +360,8 @@ static void launch_x(int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
 }
 #endif
 
-void launch_h3p(int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
+void launch_h3p(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
+    (void)cfg;
 #ifdef BGNN_H3P_ABLATION
     switch (g_h3p_abl) {
         case 1: launch_x<1>(abl, grid, s, g); return;

@@ -50,7 +50,7 @@ __device__ __forceinline__ void x6_barrier_lds() {
 extern int g_x6_bdma;   // 1: the pre-split f16x3 GEMMs stage B by LDS-DMA, 2-4: k_gemm_h3p (gemm_x6.hip)
 struct GemmArgs;
 bool h3p_ok(int cfg, const GemmArgs& g);                                // gemm_h3p.hip
-void launch_h3p(int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
+void launch_h3p(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g);
 
 // one 32-deep f16x3 slice on 16x16x32 MFMAs from restrict-scoped LDS images (the DMA path: the
 // scopes keep hipcc from draining the B slots' DMA in flight, vmcnt(0), before these reads); the
@@ -698,7 +698,7 @@ template <int PREC, int TA, int TB, int ABL>
 inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     if constexpr (PREC == 1 && TA == 0 && TB == 1) {
         if (g.wb && g_x6_bdma >= 2 && h3p_ok(cfg, g)) {   // the pipelined kernels (gemm_h3p.hip)
-            launch_h3p(ABL, grid, s, g);
+            launch_h3p(cfg, ABL, grid, s, g);
             return;
         }
 #ifdef BGNN_H3P_ABLATION
