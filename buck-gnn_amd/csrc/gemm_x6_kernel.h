@@ -363,6 +363,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
     // slots (no VGPRs, no ds_write), issued NSB - 1 slices ahead; A keeps the register split at
     // prefetch distance 2. Only the 16x16x32 8-wave tiles.
     constexpr bool kDMA = (PPV & 8) != 0;
+    // PPV bit 4 (16): waves in the second half stage between the two halves of their MFMA block, so
+    // that a SIMD's two waves do not leave the matrix pipe for their staging together (the guide's
+    // stagger; the pre-split 256 x 256 forward)
+    constexpr bool kSTG = (PPV & 16) != 0;
     static_assert(!kDMA || (kWB && PREC == 1 && 64 * WM * WN == 512), "B by LDS-DMA: pre-split f16x3, 8 waves");
     // f16x3 main loops run 16x16x32 MFMAs (four per 32x32 block, one per 32-deep slice; round 5):
     // the same cycles per FLOP as 32x32x16, but the chip holds a higher clock under them (guide
@@ -563,10 +567,49 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_x6(GemmArgs g) {
             }
             }
         };
+        // (kSTG: the held-A form of mma_slice split at column block TN, for the staggered step)
+        auto mma_half = [&](int cur, const uint4 (&a)[2 * TM][2], int j0) {
+            if constexpr (kSTG && kM16 && PREC == 1 && TM <= TN) {
+                const int l16 = lane & 15, lq = lane >> 4;
+#pragma unroll
+                for (int jj = 0; jj < TN; ++jj) {
+                    const int j = j0 + jj;
+                    const uint4 b[2] = {Bs[cur][x6_pos(wn * (BN / WN) + j * 16 + l16, lq)],
+                                        Bs[cur][BN * 4 + x6_pos(wn * (BN / WN) + j * 16 + l16, lq)]};
+#pragma unroll
+                    for (int i = 0; i < 2 * TM; ++i) {
+                        floatx4 t = acc4[i][j];
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[i][0]), as_f16x8(b[1]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[i][1]), as_f16x8(b[0]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(a[i][0]), as_f16x8(b[0]), t, 0, 0, 0);
+                        acc4[i][j] = t;
+                    }
+                }
+            }
+        };
         // one pipeline step: split slice kt+1 (register set S) into LDS buffer (kt+1)&1, refill
         // set S with slice kt+1+PF, multiply slice kt, barrier. S = (kt+1) & 1 for PF = 2.
         auto step = [&](int64_t kt, Regs& r) {
             const int cur = (int)(kt & 1);
+            if constexpr (kSTG && kM16 && PREC == 1 && TM <= TN) {
+                if (wave >= WM * WN / 2) {
+                    const int l16 = lane & 15, lq = lane >> 4;
+                    uint4 a[2 * TM][2];
+#pragma unroll
+                    for (int i = 0; i < 2 * TM; ++i) {
+                        a[i][0] = As[cur][x6_pos(wm * (BM / WM) + i * 16 + l16, lq)];
+                        a[i][1] = As[cur][BM * 4 + x6_pos(wm * (BM / WM) + i * 16 + l16, lq)];
+                    }
+                    mma_half(cur, a, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (kt + 1 < nk) store_ab(cur ^ 1, r);
+                    if (kt + 1 + PF < nk) load_ab(kb + (kt + 1 + PF) * X6_BK, r);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mma_half(cur, a, TN);
+                    __syncthreads();
+                    return;
+                }
+            }
             if (kt + 1 < nk) store_ab(cur ^ 1, r);
             if (kt + 1 + PF < nk) load_ab(kb + (kt + 1 + PF) * X6_BK, r);
             // keep the staging (split VALU, LDS writes, global loads) out of the MFMA block
@@ -716,7 +759,9 @@ inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
                 case 1: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 128, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;
                 case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
                 case 3: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL, 4>), grid, dim3(512), 0, s, g); return;
-                default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 4>), grid, dim3(512), 0, s, g); return;
+                // (the forward's 256 x 256 tile with the staggered staging, PPV 16: 290.5 -> 283.5 us,
+                // bit-identical, profiles/r06_gemm_fwd_stagger_aa.txt)
+                default: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL, 20>), grid, dim3(512), 0, s, g); return;
             }
         }
     }
