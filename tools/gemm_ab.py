@@ -25,7 +25,7 @@ import torch  # noqa: E402
 
 from bgnn import _lib, fused  # noqa: E402
 
-SHAPES = {"fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872, 512, 512),
+SHAPES = {"wgrad": (1024, 512, 80656), "fwd": (80656, 1024, 512), "dgrad": (80656, 512, 1024), "ea": (715872, 512, 512),
           "fwd_small": (10082, 1024, 512), "fwd3": (80672, 1024, 512), "fwd3r": (80688, 1024, 512), "fwd0": (80640, 1024, 512), "fwd_fold": (80656, 1024, 128), "dgrad_fold": (80656, 128, 1024)}
 
 
@@ -38,6 +38,8 @@ def parse(vs):
     knob = int(kv) if kv else 0
     if kind == "x":
         return kind, knob, int(vs[1:])
+    if kind == "t":   # the TN weight-gradient product on its automatic plan
+        return kind, knob, -1
     _, _, cfg = vs[1:].partition(".")
     return kind, knob, int(cfg) if cfg else -1
 
@@ -56,8 +58,9 @@ def main():
     for name in args.shapes.split(","):
         M, N, K = SHAPES[name]
         torch.manual_seed(0)
-        a = torch.randn(M, K, device=dev)
-        b = torch.randn(N, K, device=dev) * 0.05
+        # ("t" variants: the TN product C = a^T b of the weight gradient, a [K, M], b [K, N])
+        a = torch.randn(K, M, device=dev) if name == "wgrad" else torch.randn(M, K, device=dev)
+        b = torch.randn(K, N, device=dev) * 0.05 if name == "wgrad" else torch.randn(N, K, device=dev) * 0.05
         am = torch.stack([a.abs().max(), b.abs().max()]).contiguous()
         src = torch.randn(M, N, device=dev)
         outs = {v: torch.empty(M, N, device=dev) for v in variants}
@@ -93,6 +96,8 @@ def main():
                     _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N,
                               None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None,
                               src.data_ptr() if kind[0] == "d" else None, N, 0.1, 1234, fused._stream())
+                elif kind[0] == "t":
+                    fused.gemm(a, b, True, False, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 else:
                     fused.gemm(a, b, False, True, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 e1.record()
