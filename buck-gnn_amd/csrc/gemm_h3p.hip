@@ -85,7 +85,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     uint4* const abuf = smem;
     uint4* const bslots = smem + 2 * A_U4;
 
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // (the wave index through readfirstlane: wave-uniform branches on it stay scalar)
+    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int64_t ntn = (g.N + BN - 1) / BN;
     const int tiles = (int)(((g.M + BM - 1) / BM) * ntn);

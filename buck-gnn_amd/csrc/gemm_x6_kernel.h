@@ -769,6 +769,8 @@ inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
     // be the plan's tile (bgnn_gemm_f32_scaled sizes the grid from it).
     if constexpr (PREC >= 1) {
         if (cfg == 3) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); return; }
+        // (round 6: the staggered staging on the weight gradient's 256 x 256 tile measured 259.9 ->
+        // 260.7 us, profiles/r06_gemm_wgrad_stagger_ac.txt; not used)
         if (cfg == 4) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL>), grid, dim3(512), 0, s, g); return; }
     }
     switch (cfg) {
