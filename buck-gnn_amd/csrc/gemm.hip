@@ -317,7 +317,14 @@ int gemm_mode() { return g_gemm_mode; }
 // 256x256 tiles 293 us (256x128: 341); dgrad 80656x512x1024 128x256 311 us (256x128: 329,
 // 256x256: 323, under-filled last wave); wgrad 1024x512x80656 256x256 + split-K 302 us
 // (256x128: 604 -- half the operand re-reads).
-inline int pick_x6_cfg(int64_t M, int64_t N, int64_t K, int prec) {
+inline int pick_x6_cfg(int64_t M, int64_t N, int64_t K, int prec, bool h3_nt = false) {
+    // (h3_nt: the f16x3 family's NT product, C = A B^T -- the only one built with cfg 5)
+    if (h3_nt && M >= 4096 && N == 128 && (M + 255) / 256 < 384) {
+        // a tall N = 128 product has one column tile: 256-row tiles give 1.2 rounds of 256 CUs (the
+        // folded layer's input gradient, 316 tiles), 8-wave 128 x 128 tiles 2.5 rounds; the same
+        // 16x16x32 MFMA order per element, so the same bits
+        return 5;
+    }
     if (prec == 1) {
         if (M >= 4096 && N >= 1024) return 4;
         if (M >= 4096 && N >= 256) return 2;
@@ -398,6 +405,7 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
         p.x6 = 1;
         p.prec = 2;
         p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, 1);
+        if (p.cfg == 5) p.cfg = 1;   // (the 8-wave 128 x 128 tile is built for f16x3 only)
         // plane blocks must be whole tiles (every bf16 tile gives the same bits: 16x16x32 MFMAs
         // in increasing k), else the 128x128 tile
         if (!planes_ok(kX6Cfgs[p.cfg].bm, kX6Cfgs[p.cfg].bn, 32)) p.cfg = 0;
@@ -408,7 +416,9 @@ static Plan make_plan(int64_t M, int64_t N, int64_t K, int ta, int tb, int64_t a
     if (g_gemm_mode == 2) {
         p.x6 = 1;
         p.prec = 1;
-        p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec);
+        p.cfg = g_gemm_cfg >= 0 ? g_gemm_cfg % kNumX6Cfgs : pick_x6_cfg(M, N, K, p.prec, ta == 0 && tb == 1);
+        // (cfg 5 is built for the f16x3 NT product only: a forced cfg 5 elsewhere takes 256 x 128)
+        if (p.cfg == 5 && !(ta == 0 && tb == 1)) p.cfg = 1;
         // knob 16 = 4: the pre-split products on the pipelined 128 x 128 kernel (gemm_h3p.hip)
 #ifdef BGNN_H3P_ABLATION
         if (wb && g_x6_bdma == 4 && g_gemm_cfg < 0 && N % 128 == 0 && K % 32 == 0) p.cfg = 0;

@@ -38,8 +38,9 @@ const X6Cfg kX6Cfgs[] = {
     {128, 256, 8, 1},   // 2: 2x4 waves of 64x64
     {256, 256, 8, 1},   // 3: 2x4 waves of 128x64
     {256, 256, 8, 1},   // 4: 4x2 waves of 64x128
+    {128, 128, 8, 1},   // 5: 2x4 waves of 64x32 (f16x3 NT only: tall N = 128 products with few 256-row tiles)
 };
-const int kNumX6Cfgs = 5;
+const int kNumX6Cfgs = 6;
 
 // knob 16 (BGNN_TUNE_GEMM_BDMA): default 2 with 4 slots = the pipelined 128 x 256 kernel (gemm_h3p.hip)
 // for the pre-split products planned on that tile (the SAGE input gradients): bit-identical, dgrad

@@ -773,6 +773,9 @@ inline void launch_x6_a(int cfg, dim3 grid, hipStream_t s, const GemmArgs& g) {
         // 260.7 us, profiles/r06_gemm_wgrad_stagger_ac.txt; not used)
         if (cfg == 4) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 256, 256, 4, 2, ABL>), grid, dim3(512), 0, s, g); return; }
     }
+    if constexpr (PREC == 1 && TA == 0 && TB == 1) {
+        if (cfg == 5) { hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 128, 2, 4, ABL>), grid, dim3(512), 0, s, g); return; }
+    }
     switch (cfg) {
         case 0: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 128, 2, 2, ABL>), grid, dim3(256), 0, s, g); break;
         case 2: hipLaunchKernelGGL((k_gemm_x6<PREC, TA, TB, 128, 256, 2, 4, ABL>), grid, dim3(512), 0, s, g); break;

@@ -340,3 +340,41 @@ def test_gemm_dropadd_cols_bit_identical(dev, M):
         _lib.call("bgnn_gemm_f32_dropadd_cols", M, 2 * C, H, a.data_ptr(), H, w.data_ptr(), H, out.data_ptr(),
                   2 * C, am[0:1].data_ptr(), am[1:2].data_ptr(), src.data_ptr(), C, 100, 0.1, 77, ws.data_ptr(),
                   ws_bytes, fused._stream())
+
+
+# tall N = 128 products (the folded layer's input gradient dh = dz Wf, 80656 x 128 x 1024; the
+# encoder's last Linear) plan the 8-wave 128 x 128 tile (cfg 5): the same 16x16x32 MFMAs per
+# element in the same k order as the 256 x 128 tile, so the same bits, with the plain epilogue's
+# bias / ReLU / max|C| and the drop-add epilogue; ragged last row tiles included
+@pytest.mark.parametrize("M,K", [(80656, 1024), (80656, 64), (4100, 256)])
+@pytest.mark.parametrize("dropadd", [False, True])
+def test_gemm_tall_n128_tile_bit_identical(dev, M, K, dropadd):
+    N = 128
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=dev)
+    w = torch.randn(N, K, device=dev) * 0.05
+    am = torch.stack([a.abs().max(), w.abs().max()]).contiguous()
+    outs = []
+    for cfg in (-1, 1):   # automatic (cfg 5) against the forced 256 x 128 tile
+        _lib.call("bgnn_gemm_set_cfg", cfg)
+        try:
+            if dropadd:
+                src = torch.randn(M, N, device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+                out = torch.full((M, N), float("nan"), device=dev)
+                ws_bytes = _lib.query("bgnn_gemm_ws_bytes_ex", M, N, K, 0, 1, 0)
+                ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+                _lib.call("bgnn_gemm_f32_dropadd", 0, 1, M, N, K, a.data_ptr(), K, w.data_ptr(), K, out.data_ptr(), N,
+                          am[0:1].data_ptr(), am[1:2].data_ptr(), src.data_ptr(), N, 0.1, 99, ws.data_ptr(),
+                          ws_bytes, fused._stream())
+                outs.append((out, None))
+            else:
+                bias = torch.randn(N, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+                ca = torch.zeros(1, device=dev)
+                out = fused.gemm(a, w, False, True, bias=bias, relu=True, a_amax=am[0:1], b_amax=am[1:2], c_amax=ca)
+                outs.append((out, ca))
+        finally:
+            _lib.call("bgnn_gemm_set_cfg", -1)
+    assert not torch.isnan(outs[0][0]).any()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if not dropadd:
+        assert torch.equal(outs[0][1], outs[1][1])
