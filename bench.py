@@ -48,7 +48,7 @@ FP32_MFMA_PEAK_TFS = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.m
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md)
 X6_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6   # f32-equivalent ceiling of the 6-product bf16 split GEMM
 H3_PEAK_TFS = BF16_MFMA_PEAK_TFS / 3   # f32-equivalent ceiling of the 3-product f16 split GEMM (f16 = bf16 rate)
-TRAFFIC_FILE = "traffic_r05o.json"   # rocprofv3 PMC passes of this bench (tools/gpu_check.sh TAG pmc)
+TRAFFIC_FILE = "traffic_r06af.json"   # rocprofv3 PMC passes of this bench (tools/gpu_check.sh TAG pmc)
 METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"   # BASELINE.json
 
 
