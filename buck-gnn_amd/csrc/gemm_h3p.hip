@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     uint4* const bslots = smem + 2 * A_U4;
 
     // (the wave index through readfirstlane: wave-uniform branches on it stay scalar)
-    const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int t = threadIdx.x, lane = t & 63, wave = (X & 128) ? (t >> 6) : __builtin_amdgcn_readfirstlane(t >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int64_t ntn = (g.N + BN - 1) / BN;
     const int tiles = (int)(((g.M + BM - 1) / BM) * ntn);
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     // the last NSB steps, which would re-read B's last slice, brings the tile's masked-gradient source
     // rows instead -- quarter q (BM / NSB rows of 1 KiB) into slot (nk + q) % NSB, the same slots and
     // vmcnt counts -- so the epilogue reads them from LDS instead of waiting on HBM
-    constexpr bool kSrcLds = ABL == 8 && X == 0 && BN * 4 == 1024 && NSB * GB * (NT / 64) == BM;
+    constexpr bool kSrcLds = ABL == 8 && (X & ~128) == 0 && BN * 4 == 1024 && NSB * GB * (NT / 64) == BM;
     const bool lsrc = kSrcLds && g.bsrc_c0 == 0 && !g.bias && !g.relu && !g.c_amax && !g.ga0 && g.alpha == 1.f &&
                       g.beta == 1.f && nk >= NSB && g.ld_bsrc % 4 == 0 && ((uintptr_t)g.bsrc & 15) == 0 &&
                       ((uintptr_t)g.C & 15) == 0 &&
@@ -376,6 +376,7 @@ void launch_h3p(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
         case 31: launch_x<31>(abl, grid, s, g); return;
         case 32: launch_x<32>(abl, grid, s, g); return;
         case 63: launch_x<63>(abl, grid, s, g); return;
+        case 128: launch_x<128>(abl, grid, s, g); return;
         case 64: launch_x<64>(abl, grid, s, g); return;
         default: break;
     }
