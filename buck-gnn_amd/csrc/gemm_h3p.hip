@@ -94,6 +94,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     const int64_t tm = lt / ntn, tn = lt % ntn;
     const int64_t m0 = tm * BM, n0 = tn * BN;
     const int64_t nk = g.K / X6_BK;
+    if constexpr ((X & 768) != 0) {   // (measurement build: half of each XCD's first-round workgroups start late)
+        if (blockIdx.x < 256 && ((blockIdx.x >> 3) & 1))
+            for (int i = 0; i < ((X >> 8) & 3) * 2; ++i) __builtin_amdgcn_s_sleep(127);
+    }
 
     float sa, ia, sb, ib;
     h3_scale(*g.a_amax, sa, ia);
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void k_gemm_h3p(GemmArgs g) {
     // the last NSB steps, which would re-read B's last slice, brings the tile's masked-gradient source
     // rows instead -- quarter q (BM / NSB rows of 1 KiB) into slot (nk + q) % NSB, the same slots and
     // vmcnt counts -- so the epilogue reads them from LDS instead of waiting on HBM
-    constexpr bool kSrcLds = ABL == 8 && (X & ~128) == 0 && BN * 4 == 1024 && NSB * GB * (NT / 64) == BM;
+    constexpr bool kSrcLds = ABL == 8 && (X & ~896) == 0 && BN * 4 == 1024 && NSB * GB * (NT / 64) == BM;
     const bool lsrc = kSrcLds && g.bsrc_c0 == 0 && !g.bias && !g.relu && !g.c_amax && !g.ga0 && g.alpha == 1.f &&
                       g.beta == 1.f && nk >= NSB && g.ld_bsrc % 4 == 0 && ((uintptr_t)g.bsrc & 15) == 0 &&
                       ((uintptr_t)g.C & 15) == 0 &&
@@ -377,6 +381,9 @@ void launch_h3p(int cfg, int abl, dim3 grid, hipStream_t s, const GemmArgs& g) {
         case 32: launch_x<32>(abl, grid, s, g); return;
         case 63: launch_x<63>(abl, grid, s, g); return;
         case 128: launch_x<128>(abl, grid, s, g); return;
+        case 256: launch_x<256>(abl, grid, s, g); return;
+        case 512: launch_x<512>(abl, grid, s, g); return;
+        case 768: launch_x<768>(abl, grid, s, g); return;
         case 64: launch_x<64>(abl, grid, s, g); return;
         default: break;
     }

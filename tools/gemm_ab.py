@@ -9,7 +9,8 @@ rounds. Results are checked bit-identical to the first variant.
 (Round 6 measured a "+e" variant here, the ragged last row tile scheduled first: no gain beyond
 the first-variant order bias, profiles/r06_gemm_edge_first_l.txt; not kept.) Variants: "xC" the register-staged kernel (bgnn_gemm_f32_scaled) on tile config C (-1 = the
 automatic plan); "w" the pre-split weight path (bgnn_gemm_wsplit + bgnn_gemm_f32_w); "d" the same
-with the drop-add epilogue (src = an [M, N] gradient, p = 0.1: the skip layers' dgrad); "w.C" /
+with the drop-add epilogue (src = an [M, N] gradient, p = 0.1: the skip layers' dgrad), "n" that epilogue
+with p = 0 (no dropout mask); "w.C" /
 "d.C" on tile config C; "W", "D" (and "W.C", "D.C") the same with B staged by LDS-DMA (knob 16 = 1); a suffix "@V" sets
 knob 16 (BGNN_TUNE_GEMM_BDMA) to V for that variant ("w@2": the pipelined kernel gemm_h3p.hip). (Round 6 measured the main-loop variants "wP" of the then knob 14 here,
 profiles/r06_gemm_ab_b.txt.)
@@ -67,7 +68,7 @@ def main():
         imgs = {}
         for vs in variants:
             kind, pp, cfg = parse(vs)
-            if kind[0] in "wd":
+            if kind[0] in "wdn":
                 _lib.call("bgnn_gemm_set_cfg", cfg)
                 _lib.call("bgnn_set_tuning", 16, pp)   # (knob 16 = 4 plans 128-column images)
                 bn = _lib.query("bgnn_gemm_w_tile", M, N, K)
@@ -91,11 +92,12 @@ def main():
                 out = outs[vs]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                if kind[0] in "wd":
+                if kind[0] in "wdn":
                     img, bn = imgs[vs]
                     _lib.call("bgnn_gemm_f32_w", M, N, K, a.data_ptr(), K, img.data_ptr(), bn, out.data_ptr(), N,
                               None, 0, am[0:1].data_ptr(), am[1:2].data_ptr(), None,
-                              src.data_ptr() if kind[0] == "d" else None, N, 0.1, 1234, fused._stream())
+                              src.data_ptr() if kind[0] in "dn" else None, N,
+                              0.0 if kind[0] == "n" else 0.1, 1234, fused._stream())
                 elif kind[0] == "t":
                     fused.gemm(a, b, True, False, out=out, a_amax=am[0:1], b_amax=am[1:2])
                 else:
@@ -111,7 +113,7 @@ def main():
             us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in times[vs])
             med = us[len(us) // 2]
             kind = vs[0].lower()
-            r = ref.setdefault(kind == "d", outs[vs])
+            r = ref.setdefault(kind, outs[vs])
             same = "ref" if r is outs[vs] else ("bit-identical" if torch.equal(outs[vs], r) else
                                                 f"DIFFERS max {(outs[vs] - r).abs().max().item():.3g}")
             print(f"{name:9s} {M}x{N}x{K} {vs:>6s}: median {med:7.1f} us  min {us[0]:7.1f}  "
