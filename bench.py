@@ -52,6 +52,50 @@ TRAFFIC_FILE = "traffic_r06af.json"   # rocprofv3 PMC passes of this bench (tool
 METRIC = "graphs/sec (fwd+bwd) 6-layer SAGE h=512, ~5k-node meshes, batch 16, 1/2/4/8 GPU"   # BASELINE.json
 
 
+class HipTimingEvent:
+    """A HIP event for the per-launch timers (bgnn.fused.TIMER_EVENT), created with
+    hipEventDisableSystemFence: torch.cuda.Event's record ends in a system-scope release (cache
+    writeback + invalidate) that idles the GPU ~5 us per event between the timed kernels (rocprofv3
+    trace: 5.7 us before and 10.4 us between timed launches, ~0.3 ms per cfg2 step). Same
+    record / elapsed_time interface; recorded on torch's current stream (the launching stream).
+    The library is the HIP runtime torch already loaded (same soname)."""
+    _hip = None
+
+    def __init__(self):
+        import ctypes
+        import torch
+        if HipTimingEvent._hip is None:
+            torch.cuda.current_stream()
+            hip = ctypes.CDLL("libamdhip64.so.7")
+            hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            HipTimingEvent._hip = hip
+        self._torch = torch
+        self.h = ctypes.c_void_p()
+        rc = HipTimingEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.h), 0x20000000)  # DisableSystemFence
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
+
+    def record(self):
+        rc = HipTimingEvent._hip.hipEventRecord(self.h, self._torch.cuda.current_stream().cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def elapsed_time(self, end) -> float:
+        import ctypes
+        ms = ctypes.c_float(0.0)
+        rc = HipTimingEvent._hip.hipEventElapsedTime(ctypes.byref(ms), self.h, end.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
+        return float(ms.value)
+
+    def __del__(self):
+        if HipTimingEvent._hip is not None and self.h:
+            HipTimingEvent._hip.hipEventDestroy(self.h)
+
+
 def metric_name(model: str, bsz: int) -> str:
     """BASELINE.json's metric for the SAGE models at batch 16; EA_GNN (configs[4]) is named for
     what it measures."""
@@ -103,6 +147,10 @@ def parse():
                          "timed run (epochs x shard/16)")
     ap.add_argument("--dataset-graphs", type=int, default=0,
                     help="global dataset size for --epochs (default: --store-graphs per rank)")
+    ap.add_argument("--timer-every", type=int, default=4,
+                    help="record the per-launch roofline events on every N-th timed step (1 = all)")
+    ap.add_argument("--torch-events", action="store_true",
+                    help="time the launches with torch.cuda.Event (system-fenced records; A/B of HipTimingEvent)")
     ap.add_argument("--lr", type=float, default=None,
                     help="Adam learning rate (default 1e-2, TRAIN_FINAL.py:37; EA_GNN 1e-3: at 1e-2 the h=512 "
                          "EA_GNN diverges in the reference too, tests/test_gpu_ea_train.py)")
@@ -158,6 +206,7 @@ def run_infer(args, model, dev, world, rank):
     for _ in range(max(1, args.warmup)):
         fwd()
     torch.cuda.synchronize()
+    fused.TIMER_EVENT = None if args.torch_events else HipTimingEvent
     fused.TIMERS = {}
     if world > 1:
         torch.distributed.barrier()
@@ -326,20 +375,25 @@ def measure_train(args, config, model_name, dev, world, rank, steps, warmup, hea
         state["order"] = iter(())
         state["epoch"] = -1
     torch.cuda.synchronize()
+    fused.TIMER_EVENT = None if args.torch_events else HipTimingEvent
     fused.TIMERS = {}
     if heavy_timing:
         _lib.call("bgnn_heavy_timing", 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    timers = fused.TIMERS
+    every = max(1, args.timer_every)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
+        # per-launch events on every `every`-th timed step (each event record idles the GPU ~4 us)
+        fused.TIMERS = timers if i % every == 0 else None
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timers, fused.TIMERS = fused.TIMERS, None
+    fused.TIMERS = None
     heavy = None
     if heavy_timing:
         import ctypes
@@ -356,7 +410,8 @@ def measure_train(args, config, model_name, dev, world, rank, steps, warmup, hea
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = {"elapsed": elapsed, "timers": timers, "batch": batch, "batch_cpu": batch_cpu, "loss": float(loss.item()),
-           "lr": lr, "state0": state0, "bsz": bsz, "steps": steps, "heavy": heavy}
+           "lr": lr, "state0": state0, "bsz": bsz, "steps": steps, "heavy": heavy,
+           "event_steps": len(range(0, steps, every))}
     del model, opt, store
     return res
 
@@ -365,7 +420,7 @@ def roofline_blocks(args, m, model_name):
     """The roofline objects of one measured run (bench line keys roofline, roofline_gemm,
     roofline_hbm, roofline_agg_bwd) from its per-launch HIP events."""
     from bgnn import _lib
-    timers, steps = m["timers"], m["steps"]
+    timers, steps = m["timers"], m["event_steps"]   # (the steps whose launches carry events)
     batch = m["batch"]
 
     def avg_ms(name):
@@ -584,6 +639,11 @@ def main():
     batch = m["batch"]
     is_ea = args.model.startswith("EA_GNN")
     blocks = roofline_blocks(args, m, args.model)
+    blocks["launch_timing"] = {
+        "events": "torch.cuda.Event" if args.torch_events else "hipEventDisableSystemFence (HipTimingEvent)",
+        "event_steps": m["event_steps"], "of_timed_steps": steps,
+        "note": "per-launch roofline events recorded on every timed step i with i % timer_every == 0 "
+                "(inside the timed region, on the launching stream)"}
     graphs = bsz * world * steps
     out = {
         "metric": metric_name(args.model, bsz),
@@ -653,7 +713,7 @@ def main():
             "traffic": traffic.get("ea_edge_b16") if (args.bf16 and ea_mod.BF16_STORAGE) else None,
             "algorithmic_bytes": ea_bytes,
             "avg_launch_ms": round(ea_ms, 5), "launches": n_ea,
-            "ms_per_step": round(ea_ms * n_ea / steps, 4) if n_ea else float("nan"),
+            "ms_per_step": round(ea_ms * n_ea / m["event_steps"], 4) if n_ea else float("nan"),
             "mfma": {"achieved": round(ea_tfs, 2), "peak": ea_peak, "unit": "TFLOP/s",
                      "frac": round(ea_tfs / ea_peak, 4), "algorithmic_flop": ea_flop},
         }

@@ -65,6 +65,10 @@ WSPLIT = True
 # Optional per-launch timing (bench.py): name -> list of (start, end) HIP events recorded
 # on the launching stream around the named launch.
 TIMERS = None
+# event factory for TIMERS (None: torch.cuda.Event(enable_timing=True)); bench.py installs HIP events
+# created with hipEventDisableSystemFence: a default event's record does a system-scope release (cache
+# writeback + invalidate) that leaves the GPU idle ~5 us per event between the timed kernels
+TIMER_EVENT = None
 
 
 class _timed:
@@ -76,7 +80,8 @@ class _timed:
 
     def __enter__(self):
         if TIMERS is not None:
-            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            mk = TIMER_EVENT or (lambda: torch.cuda.Event(enable_timing=True))
+            self.ev = (mk(), mk())
             self.ev[0].record()
         return self
 
