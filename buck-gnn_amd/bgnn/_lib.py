@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # BGNN_LIBRARY: a measurement build of the same ABI (make -C buck-gnn_amd m16), for tools/ only
 LIB_PATH = os.environ.get("BGNN_LIBRARY") or os.path.join(_HERE, "_lib", "libbgnn.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lock = threading.Lock()
 _lib = None
@@ -103,7 +103,7 @@ SIGNATURES = {
     "bgnn_bn_eval_coeffs": (c_i32, [c_i32, c_p, c_p, c_f32, c_p, c_p, c_p, c_p, c_p]),
     "bgnn_sage_apply": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_f32, c_u64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "bgnn_rows_slots": (c_i32, [c_i64]),
-    "bgnn_sage_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i64, c_i32, c_p, c_p]),
+    "bgnn_sage_bwd_stats": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i64, c_i32, c_p, c_p]),
     "bgnn_reduce_partials": (c_i32, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p]),
     "bgnn_linear_bwd_prep_slots": (c_i32, []),
     "bgnn_linear_bwd_prep": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
@@ -115,7 +115,7 @@ SIGNATURES = {
     "bgnn_rel_error_loss": (c_i32, [c_p, c_p, c_i64, c_f32, c_f32, c_f32, c_p, c_p, c_p]),
     "bgnn_small_linear_fwd": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_i32, c_i32, c_p, c_p]),
     "bgnn_small_linear_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p]),
-    "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
+    "bgnn_sage_bwd_rows": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_f32, c_u64, c_i32, c_i64,
                                    c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),
     "bgnn_l2norm_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p]),
     "bgnn_gemm_bf16": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64,

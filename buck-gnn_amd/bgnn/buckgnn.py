@@ -37,6 +37,10 @@ from .ops import segment_reduce
 FUSED_ENCODER = True
 # fold the node encoder's last Linear into the first fused SAGE layer (BuckGNN._foldable_encoder)
 FOLD_ENCODER = True
+# buckling + mean pooling on the fused sum / mean layer loop: the last layer also returns the
+# per-graph mean pool (fused.SageLayerFn pool), so its backward reads the pooled gradient through
+# the batch vector instead of an [N, H] broadcast (A/B switch; the same bits)
+FUSED_POOL = True
 
 _SAGE_VARIANTS = {
     # model_name: (ModuleList attribute, aggr, has BatchNorm)
@@ -259,7 +263,9 @@ class BuckGNN(nn.Module):
                 and x.size(0) >= 1024 and self.num_layers >= 1)
 
     def _sage_loop(self, x: Tensor, edge_index: Tensor, convs, bns, aggr: str, skip_last_excluded: bool,
-                   x_amax: Optional[Tensor] = None, x_in: Optional[nn.Linear] = None):
+                   x_amax: Optional[Tensor] = None, x_in: Optional[nn.Linear] = None, pool=None):
+        """The SAGE layer loop; pool (a SegmentIndex; fused sum / mean loop only): returns
+        (x, mean pool of x per segment) from the last fused layer instead of x."""
         L = len(convs) if convs is not None else self.num_layers
         p = self.dropout.p
         if self._sage_fused(x, aggr):
@@ -285,12 +291,16 @@ class BuckGNN(nn.Module):
                 fold = x_in if i == 0 else None
                 rng = (RangeRows(x_full=x_full, x_amax=bufs[i - 1, 3:4] if x_full is not None else None,
                                  out=i < L - 1, out_amax=bufs[i, 3:4]) if rng_on else None)
-                x, amax = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
-                                     skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
-                                     amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
-                                     b_in=None if fold is None else fold.bias, wprep=wprep[i], count_batch=False,
-                                     fold_amax=fold_amax, rng=rng)
+                pl = pool if (i == L - 1 and red != 2) else None
+                out = sage_layer(x, conv.lin_l.weight, conv.lin_l.bias, conv.lin_r.weight, bn, graph, red,
+                                 skip, p, self.training, self._seed(), x_amax=amax, return_amax=True,
+                                 amax_buf=bufs[i], w_in=None if fold is None else fold.weight,
+                                 b_in=None if fold is None else fold.bias, wprep=wprep[i], count_batch=False,
+                                 fold_amax=fold_amax, rng=rng, pool=pl)
+                x, amax = out[0], out[1]
                 x_full = rng.holder[0] if (rng is not None and rng.holder) else None
+            if pool is not None:
+                return x, (out[2] if (red != 2 and L > 0) else segment_reduce(x, pool, "mean"))
             return x
         if x_in is not None:   # (only reached when the caller folded the encoder's last Linear)
             x = x_in(x)
@@ -304,7 +314,7 @@ class BuckGNN(nn.Module):
             if 0 < i < L - 1:
                 x = x + x_prev
             x = self.dropout(x)
-        return x
+        return (x, segment_reduce(x, pool, "mean")) if pool is not None else x
 
     def _count_bn_batches(self, bns) -> None:
         """BatchNorm1d's num_batches_tracked += 1 for every module of a fused loop in one launch
@@ -393,8 +403,16 @@ class BuckGNN(nn.Module):
                 else:
                     x, e = self.shared_gn_block(x, edge_index, e)
                 x, e = self._skip_dropout(x, e, x_prev, e_prev, 0 < i < self.num_layers - 1, ea_fused)
+        # the buckling decoder's mean pool from the last fused sum / mean layer (FUSED_POOL)
+        pool = (batch_segments(batch) if (FUSED_POOL and self.prediction_type == "buckling"
+                                          and self.pooling_layer == "mean" and batch is not None
+                                          and (name == "GraphSage_addAggr_Shared" or name in _SAGE_VARIANTS)
+                                          and self._sage_fused(x, sage) and sage != "max") else None)
+        pooled = None
         if name == "GraphSage_addAggr_Shared":
-            x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax, x_in)
+            x = self._sage_loop(x, edge_index, None, None, "add", True, x_amax, x_in, pool=pool)
+            if pool is not None:
+                x, pooled = x
         elif name == "EA_GNN":
             if not ea_fused:
                 e = self.edge_encoder(edge_attr)
@@ -410,7 +428,10 @@ class BuckGNN(nn.Module):
                 x, e = self._skip_dropout(x, e, x_prev, e_prev, 0 < i < L - 1, ea_fused, e_slot=slot)
         elif name in _SAGE_VARIANTS:
             attr, aggr, _ = _SAGE_VARIANTS[name]
-            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax, x_in)
+            x = self._sage_loop(x, edge_index, getattr(self, attr), self.batch_norms, aggr, True, x_amax, x_in,
+                                pool=pool)
+            if pool is not None:
+                x, pooled = x
         elif name in ("GraphSage_addAggr_woBatchNorm", "GraphSage_MLP"):
             getattr(self, "sage_blocks_add")  # AttributeError, as in the reference (:405,473)
         elif name == "GraphSage_sumAggr_woBatchNorm":
@@ -436,7 +457,8 @@ class BuckGNN(nn.Module):
                 x, e = x + x_prev, e + e_prev
 
         if self.prediction_type == "buckling":
-            pooled = self.get_pooling_layer(x, edge_index, batch)
+            if pooled is None:
+                pooled = self.get_pooling_layer(x, edge_index, batch)
             return self._decode(pooled).squeeze(), batch
         if "static" in self.prediction_type or "mode_shape" in self.prediction_type:
             if "super" in self.pooling_layer:

@@ -680,9 +680,10 @@ def _glue_fwd(o, bn_part, slots, x_prev, gamma, beta, running_mean, running_var,
     return x_next, (scale, shift, mean, invstd)
 
 
-def _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg: LayerConfig):
+def _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg: LayerConfig, g_rows=None):
     """BatchNorm backward statistics of the layer glue (bgnn_sage_bwd_stats + one slot reduce):
-    (dgamma, dbeta, sum_g2, sum_g2xhat) -- all None without BN; eval mode uses zero sums."""
+    (dgamma, dbeta, sum_g2, sum_g2xhat) -- all None without BN; eval mode uses zero sums.
+    g_rows (int64 [N] or None): row r's gradient is row g_rows[r] of g (the pooled gradient)."""
     if not cfg.bn:
         return None, None, None, None
     N, H = o.shape
@@ -690,7 +691,7 @@ def _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg: LayerConfig):
     s = _stream()
     rs = _lib.query("bgnn_rows_slots", N)
     part2 = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
-    _lib.call("bgnn_sage_bwd_stats", g.data_ptr(), o.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+    _lib.call("bgnn_sage_bwd_stats", g.data_ptr(), _ptr(g_rows), o.data_ptr(), scale.data_ptr(), shift.data_ptr(),
               mean.data_ptr(), invstd.data_ptr(), float(cfg.p), cfg.seed, N, H, part2.data_ptr(), s)
     sums = torch.empty(2, H, dtype=torch.float32, device=dev)
     _lib.call("bgnn_reduce_partials", part2.data_ptr(), rs, H, sums[0].data_ptr(), sums[1].data_ptr(), 0, s)
@@ -703,11 +704,16 @@ def _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg: LayerConfig):
 
 class SageLayerFn(torch.autograd.Function):
     """Outputs (x_next, max|x_next|): the second output (non-differentiable) is the f16x3 GEMM
-    operand scale of the next layer, folded in by bgnn_sage_apply at no extra pass."""
+    operand scale of the next layer, folded in by bgnn_sage_apply at no extra pass.
+    pool (a SegmentIndex, the batch vector's segments): a third output, the mean pool of x_next
+    per segment (global_mean_pool, Models/BuckGNN.py:246-249; the same segment kernel as
+    bgnn.ops.segment_reduce). Its gradient reaches the backward row passes as the pooled
+    gradient / count read through the batch vector (g_rows), not as a materialised [N, H]
+    broadcast (the pool's index_select) read twice -- the same g values, so the same bits."""
 
     @staticmethod
     def forward(ctx, x_prev, x_amax, w_l, b_l, w_r, gamma, beta, running_mean, running_var, graph: Graph,
-                cfg: LayerConfig, amax=None, w_in=None, b_in=None, wprep=None):
+                cfg: LayerConfig, amax=None, w_in=None, b_in=None, wprep=None, pool=None):
         dev = x_prev.device
         x_prev = x_prev.contiguous()
         H = w_l.size(0)
@@ -813,14 +819,28 @@ class SageLayerFn(torch.autograd.Function):
                               invstd if invstd is not None else torch.empty(0, device=dev),
                               x_amax, w_amax, dz_amax)
         ctx.mark_non_differentiable(next_amax)
+        ctx.pool = pool
+        if pool is not None:
+            from .ops import spmm_fwd
+            pooled, _ = spmm_fwd(pool.fwd, x_next, 1, pool.num_rows)
+            return x_next, next_amax, pooled
         return x_next, next_amax
 
     @staticmethod
-    def backward(ctx, g, _g_amax):
-        if g is None:   # (materialize_grads off: the layer output did not reach the loss)
-            return (None,) * 15
-        x_prev, o, nrm, wcat, gamma, scale, shift, mean, invstd, x_amax, w_amax, dz_amax = ctx.saved_tensors
+    def backward(ctx, g, _g_amax, g_pool=None):
         cfg: LayerConfig = ctx.cfg
+        g_rows = None
+        if g_pool is not None:   # mean pool: segment gradient / count (bgnn.ops._SegmentReduce.backward)
+            seg = ctx.pool
+            gp = g_pool.contiguous() / seg.fwd.degree().clamp_min(1).to(g_pool.dtype).unsqueeze(1)
+            if g is None and not cfg.skip:
+                g, g_rows = gp, seg.index
+            else:
+                gb = gp.index_select(0, seg.index)
+                g = gb if g is None else g + gb
+        if g is None:   # (materialize_grads off: the layer output did not reach the loss)
+            return (None,) * 16
+        x_prev, o, nrm, wcat, gamma, scale, shift, mean, invstd, x_amax, w_amax, dz_amax = ctx.saved_tensors
         graph: Graph = ctx.graph
         g = g.contiguous()
         N, H = o.shape
@@ -828,7 +848,7 @@ class SageLayerFn(torch.autograd.Function):
         dev = o.device
         s = _stream()
         bn = cfg.bn
-        dgamma, dbeta, sum_g2, sum_g2xhat = _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg)
+        dgamma, dbeta, sum_g2, sum_g2xhat = _glue_bwd_stats(g, o, scale, shift, mean, invstd, cfg, g_rows)
         if planes:   # dz = [dz_l ; dh] as two dense [N, H] planes
             dzt = torch.empty(2, N, H, dtype=torch.float32, device=dev)
             dz, dzl, dh, lddz = Planes(dzt), dzt[0], dzt[1], H
@@ -847,7 +867,7 @@ class SageLayerFn(torch.autograd.Function):
         rb = (cfg.rng is not None and cfg.rng.bwd and not planes and bw.ranges is not None)
         rp = (torch.empty(_lib.query("bgnn_range_partial_bytes", N, H) // 4, dtype=torch.float32, device=dev)
               if rb else None)
-        _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), o.data_ptr(), nrm.data_ptr(),
+        _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), _ptr(g_rows), o.data_ptr(), nrm.data_ptr(),
                   _ptr(scale) if bn else None, _ptr(shift) if bn else None,
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
@@ -898,7 +918,7 @@ class SageLayerFn(torch.autograd.Function):
                 db_in = gemm(wcat, dbf.view(-1, 1), trans_a=True, trans_b=False, a_amax=fa[0],
                              b_amax=fa[4]).view(-1)                                        # [H]
             return (dx, None, dw[:H], db, dw[H:], dgamma if has_affine else None, dbeta if has_affine else None,
-                    None, None, None, None, None, dw_in, db_in, None)
+                    None, None, None, None, None, dw_in, db_in, None, None)
         # dx = dz · Wcat (+ skip gradient);  dWcat = dz^T · x_prev
         # [W_l;W_r] transposed once (2 MB) so the dgrad reads its B operand K-contiguous
         wcat_t = (ctx.wcat_t if ctx.wcat_t is not None else wcat.t().contiguous()) if DGRAD_WT else wcat
@@ -931,7 +951,7 @@ class SageLayerFn(torch.autograd.Function):
             dw = gemm(dz, x_prev, trans_a=True, trans_b=False, a_amax=dz_amax, b_amax=x_amax)  # [2H, H]
         dw_l, dw_r = dw[:H], dw[H:]
         return (dx, None, dw_l, db, dw_r, dgamma if has_affine else None, dbeta if has_affine else None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def _max_transform(x, w_l, w_r, graph: Graph, x_amax, w_amax, name: str):
@@ -1107,7 +1127,7 @@ class SageMaxLayerFn(torch.autograd.Function):
         dh = torch.empty(N, H, dtype=torch.float32, device=dev)
         rs = _lib.query("bgnn_rows_slots", N)
         part_db = torch.empty(rs, 2, H, dtype=torch.float32, device=dev)
-        _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), o.data_ptr(), nrm.data_ptr(),
+        _lib.call("bgnn_sage_bwd_rows", g.data_ptr(), None, o.data_ptr(), nrm.data_ptr(),
                   _ptr(scale) if bn else None, _ptr(shift) if bn else None,
                   _ptr(gamma) if (bn and gamma.numel()) else None,
                   _ptr(mean) if bn else None, _ptr(invstd) if bn else None, _ptr(sum_g2), _ptr(sum_g2xhat),
@@ -1230,14 +1250,16 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                bn_module, graph: Graph, reduce: int, skip: bool, p: float, training: bool,
                seed: int, x_amax: torch.Tensor = None, return_amax: bool = False, amax_buf=None,
                w_in: torch.Tensor = None, b_in: torch.Tensor = None, wprep=None, count_batch: bool = True,
-               fold_amax: torch.Tensor = None, rng: RangeRows = None):
+               fold_amax: torch.Tensor = None, rng: RangeRows = None, pool=None):
     """Run one fused layer. `bn_module` is a torch.nn.BatchNorm1d (or None for no BN).
     x_amax: optional device scalar >= max|x_prev| (the previous layer's second output), which
     spares the GEMM a pass over x_prev; return_amax: also return max|x_next|.
     w_in / b_in: fold a preceding Linear into this layer (x_prev is then that Linear's INPUT h,
     and the layer computes on x = h W_in^T + b_in without materialising x); only for a layer
     without skip connection (the reference's first SAGE layer after the node encoder).
-    rng: the range-row plumbing of a stiffened batch (RangeRows; sum / mean only)."""
+    rng: the range-row plumbing of a stiffened batch (RangeRows; sum / mean only).
+    pool: a SegmentIndex (sum / mean only): also return the mean pool of x_next per segment as the
+    last element (SageLayerFn)."""
     require_cuda(x_prev, w_l, b_l, w_r, what="sage_layer")
     H = w_l.size(0)
     if w_in is None and x_prev.size(1) != H:
@@ -1248,6 +1270,8 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
         raise ValueError("sage_layer: reduce must be 0 (sum), 1 (mean) or 2 (max)")
     if reduce == 2 and w_in is not None:
         raise ValueError("sage_layer: max aggregation needs its input rows (no folded input transform)")
+    if reduce == 2 and pool is not None:
+        raise ValueError("sage_layer: the fused mean pool is for sum / mean layers")
     if bn_module is not None:
         use_batch_stats = training or not bn_module.track_running_stats
         momentum = bn_module.momentum
@@ -1268,7 +1292,7 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
         else:
             out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, bn_module.weight, bn_module.bias,
                                     bn_module.running_mean, bn_module.running_var, graph, cfg, amax_buf, w_in, b_in,
-                                    wprep)
+                                    wprep, pool)
     else:
         cfg = LayerConfig(reduce, False, training, 0.0, 0.0, skip, p, seed)
         cfg.famax = fold_amax if w_in is not None else None
@@ -1278,7 +1302,9 @@ def sage_layer(x_prev: torch.Tensor, w_l: torch.Tensor, b_l: torch.Tensor, w_r: 
                                        wprep)
         else:
             out = SageLayerFn.apply(x_prev, x_amax, w_l, b_l, w_r, None, None, None, None, graph, cfg, amax_buf,
-                                    w_in, b_in, wprep)
+                                    w_in, b_in, wprep, pool)
+    if pool is not None:
+        return out if return_amax else (out[0], out[2])
     return out if return_amax else out[0]
 
 

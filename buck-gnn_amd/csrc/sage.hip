@@ -360,7 +360,9 @@ __global__ __launch_bounds__(256) void k_sage_apply_rows(const float* __restrict
 
 // Backward pass 1: partial sums over rows of g2 and g2*xhat per channel.
 // Thread layout: H4 = H/4 threads per row, 256/H4 rows per step.
-__global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict__ g, const float* __restrict__ o,
+__global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict__ g,
+                                                        const int64_t* __restrict__ g_rows,
+                                                        const float* __restrict__ o,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ shift,
                                                         const float* __restrict__ mean,
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict_
         const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
         for (int64_t r = r0 + ph; r < r1; r += rpi) {
             const int64_t i4 = r * H4 + c4;
-            const float4 gv = reinterpret_cast<const float4*>(g)[i4];
+            const float4 gv = reinterpret_cast<const float4*>(g)[(g_rows ? g_rows[r] : r) * H4 + c4];
             const float4 ov = reinterpret_cast<const float4*>(o)[i4];
             float gg[4] = {gv.x, gv.y, gv.z, gv.w}, oo[4] = {ov.x, ov.y, ov.z, ov.w};
             uint32_t m = 0xF;
@@ -427,8 +429,8 @@ __global__ __launch_bounds__(256) void k_sage_bwd_stats(const float* __restrict_
 // no dropout), i.e. only the L2-normalize backward.
 template <int NV, bool RELU = true, bool RANGES = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_sage_bwd_rows(
-    const float* __restrict__ g, const float* __restrict__ o, const float* __restrict__ nrm,
-    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ g, const int64_t* __restrict__ g_rows, const float* __restrict__ o,
+    const float* __restrict__ nrm, const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sum_g2,
     const float* __restrict__ sum_g2xhat, uint32_t thr, float inv_keep, uint64_t seed, int skip,
     int64_t n_rows, int H, int64_t rows_per_block, float* __restrict__ dh, int64_t lddh,
@@ -495,10 +497,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // kernel is latency-bound on these loads, not bandwidth-bound); same rows, same order
     float4 gn[NV], on[NV];
     auto fetch = [&](int64_t rr) {
+        const int64_t gr = g_rows ? g_rows[rr] : rr;   // (g_rows: row rr's gradient is row g_rows[rr] of g)
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             const int64_t i4 = rr * H4 + (cok[v] ? (cpos[v] >> 2) : 0);
-            gn[v] = reinterpret_cast<const float4*>(g)[i4];
+            gn[v] = reinterpret_cast<const float4*>(g)[gr * H4 + (cok[v] ? (cpos[v] >> 2) : 0)];
             on[v] = reinterpret_cast<const float4*>(o)[i4];
         }
     };
@@ -921,7 +924,8 @@ extern "C" int32_t bgnn_rows_slots(int64_t n_rows) {
     return (int32_t)rows_grid(n_rows, 4, &rpb);
 }
 
-extern "C" int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, const float* shift,
+extern "C" int bgnn_sage_bwd_stats(const float* g, const int64_t* g_rows, const float* o, const float* scale,
+                                   const float* shift,
                                    const float* mean, const float* invstd, float p, uint64_t seed, int64_t n_rows,
                                    int32_t H, float* partial2, void* stream) {
     BGNN_REQUIRE(H > 0 && H % 4 == 0 && H <= 1024, "sage_bwd_stats: H=%d unsupported", H);
@@ -933,13 +937,14 @@ extern "C" int bgnn_sage_bwd_stats(const float* g, const float* o, const float* 
     const int64_t blocks = rows_grid(n_rows, 4, &rpb);
     const uint32_t thr = dropout_threshold(p);
     const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
-    hipLaunchKernelGGL(k_sage_bwd_stats, dim3((unsigned)blocks), dim3(256), 0, s, g, o, scale, shift, mean, invstd,
+    hipLaunchKernelGGL(k_sage_bwd_stats, dim3((unsigned)blocks), dim3(256), 0, s, g, g_rows, o, scale, shift, mean, invstd,
                        thr, inv_keep, seed, n_rows, H, rpb, partial2);
     BGNN_CHECK_LAUNCH();
     return BGNN_OK;
 }
 
-extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm, const float* scale,
+extern "C" int bgnn_sage_bwd_rows(const float* g, const int64_t* g_rows, const float* o, const float* nrm,
+                                  const float* scale,
                                   const float* shift, const float* gamma, const float* mean, const float* invstd,
                                   const float* sum_g2, const float* sum_g2xhat, float p, uint64_t seed,
                                   int32_t skip, int64_t n_rows, int32_t H, float* dh, int64_t lddh, float* gskip,
@@ -960,7 +965,8 @@ extern "C" int bgnn_sage_bwd_rows(const float* g, const float* o, const float* n
     const uint32_t thr = dropout_threshold(p);
     const float inv_keep = thr ? 1.f / (1.f - p) : 1.f;
 #define BGNN_ROWS(NV, R)                                                                                              \
-    hipLaunchKernelGGL((k_sage_bwd_rows<NV, true, R>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, scale,    \
+    hipLaunchKernelGGL((k_sage_bwd_rows<NV, true, R>), dim3((unsigned)blocks), dim3(256), 0, s, g, g_rows, o, nrm,   \
+                       scale,                                                                                       \
                        shift, gamma, mean, invstd, sum_g2, sum_g2xhat, thr, inv_keep, seed, skip, n_rows, H, rpb,    \
                        dh, lddh, gskip, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), w_rowptr, w_mode,  \
                        rows_rev() & 1, ranges, range_w_rowptr, range_partial)
@@ -990,12 +996,12 @@ extern "C" int bgnn_l2norm_bwd(const float* g, const float* o, const float* nrm,
     int64_t rpb = 0;
     const int64_t blocks = rows_grid(n_rows, 4, &rpb);
     if (H > 256)
-        hipLaunchKernelGGL((k_sage_bwd_rows<2, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
+        hipLaunchKernelGGL((k_sage_bwd_rows<2, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, nullptr, o, nrm, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
                            rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
                            0, rows_rev() & 1, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_sage_bwd_rows<1, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, o, nrm, nullptr,
+        hipLaunchKernelGGL((k_sage_bwd_rows<1, false>), dim3((unsigned)blocks), dim3(256), 0, s, g, nullptr, o, nrm, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0u, 1.f, (uint64_t)0, 0, n_rows, H,
                            rpb, dh, lddh, nullptr, partial_db, reinterpret_cast<uint32_t*>(amax), rows_nt(), nullptr,
                            0, rows_rev() & 1, nullptr, nullptr, nullptr);

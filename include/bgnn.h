@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BGNN_ABI_VERSION 12
+#define BGNN_ABI_VERSION 13
 
 #define BGNN_OK 0
 #define BGNN_E_ARG 1001       /* invalid argument (shape, null pointer, size)    */
@@ -311,9 +311,13 @@ int bgnn_sage_apply(const float* o, const float* scale, const float* shift,
  * row-blocked form of the same element-wise pass (the same x_next bits). */
 
 /* Backward pass 1: BatchNorm statistics of the incoming gradient g (= dL/dx_next):
- *   g2 = relu'(o*scale+shift) * dropout'(g);  partial sums of g2 and g2*xhat. */
+ *   g2 = relu'(o*scale+shift) * dropout'(g);  partial sums of g2 and g2*xhat.
+ * g_rows (ABI 13; NULL: g is [n_rows, H]): row r's gradient is row g_rows[r] of g -- the last
+ * layer under a mean pool (Models/BuckGNN.py:246-249 global_mean_pool) reads the pooled gradient
+ * [graphs, H] / count through the batch vector instead of a materialised [N, H] broadcast. */
 int32_t bgnn_rows_slots(int64_t n_rows);
-int bgnn_sage_bwd_stats(const float* g, const float* o, const float* scale, const float* shift,
+int bgnn_sage_bwd_stats(const float* g, const int64_t* g_rows, const float* o, const float* scale,
+                        const float* shift,
                         const float* mean, const float* invstd, float p, uint64_t seed,
                         int64_t n_rows, int32_t H, float* partial2, void* stream);
 
@@ -347,8 +351,8 @@ int bgnn_reduce_partials(const float* partial, int32_t n_slots, int32_t H,
  * the layer's reduce (1 for sum, 2 for mean) that is the column sum of dz_l = A^T dh, the bias
  * gradient of a Linear folded into the layer (fused.sage_layer w_in).
  * sum_g2 / sum_g2xhat are the reduced stats of pass 1 (NULL when BatchNorm is off).
- * amax (optional): *amax = max(*amax, max |dh|). */
-int bgnn_sage_bwd_rows(const float* g, const float* o, const float* nrm,
+ * amax (optional): *amax = max(*amax, max |dh|). g_rows: as for bgnn_sage_bwd_stats. */
+int bgnn_sage_bwd_rows(const float* g, const int64_t* g_rows, const float* o, const float* nrm,
                        const float* scale, const float* shift, const float* gamma,
                        const float* mean, const float* invstd,
                        const float* sum_g2, const float* sum_g2xhat,

@@ -318,3 +318,39 @@ def test_small_mlp_matches_fp64(dev, dims, rows):
     again = torch.autograd.grad(fused.small_mlp(seq, x), [x] + list(seq.parameters()), gy)
     for g, g2 in zip(grads, again):   # deterministic
         assert torch.equal(g, g2)
+
+
+@pytest.mark.parametrize("model_name,n,super_node", [("GraphSage_addAggr", 45, False), ("GraphSage_meanAggr", 45, False),
+                                                     ("GraphSage_addAggr_Shared", 45, False),
+                                                     ("GraphSage_addAggr", 71, True)])
+def test_fused_mean_pool_bit_identical(dev, monkeypatch, model_name, n, super_node):
+    """Buckling + mean pooling: the last fused layer returning the per-graph mean pool
+    (SageLayerFn pool; its backward reads the pooled gradient / count through the batch vector,
+    bgnn_sage_bwd_stats / _rows g_rows) gives the same bits as the separate pool + [N, H]
+    broadcast: prediction, loss, every parameter gradient and the BatchNorm running statistics
+    (train mode, dropout 0.1; 71x71 meshes with super nodes: range rows on the last layer)."""
+    import copy as _copy
+    import bgnn
+    from bgnn import buckgnn
+    b = S.make_batch(n, 8 if n == 45 else 16, super_node=super_node).to(dev)
+    torch.manual_seed(0)
+    model0 = bgnn.BuckGNN(16, 5, hidden_channels=512, num_layers=6, dropout_rate=0.1,
+                          model_name=model_name).to(dev).train()
+    res = {}
+    for flag in (True, False):
+        monkeypatch.setattr(buckgnn, "FUSED_POOL", flag)
+        m = _copy.deepcopy(model0)
+        torch.manual_seed(123)
+        out, _ = m(b.x, b.edge_index, b.edge_attr, b.batch)
+        loss = (out - torch.linspace(0.5, 1.5, out.numel(), device=dev)).square().mean()
+        loss.backward()
+        res[flag] = ([out.detach(), loss.detach()] + [p.grad for p in m.parameters()]
+                     + [t for k, t in m.state_dict().items() if "running" in k])
+    assert len(res[True]) == len(res[False])
+    n_grads = 0
+    for a, c in zip(res[True], res[False]):
+        assert (a is None) == (c is None)   # (modules the model does not use get no gradient)
+        if a is not None:
+            n_grads += 1
+            assert torch.equal(a, c)
+    assert n_grads >= 5
